@@ -1,0 +1,226 @@
+"""Benchmark: depth maps/s of the cascade forward on MI355X (BASELINE.json metric), ms per stage,
+roofline of the dominant kernel and the CPU baseline — one JSON line on rank 0.
+
+  python bench.py [--gpus N --steps K --warmup W] [--config cfgC] [--batch B] [--no-cpu-baseline]
+
+Workload (BASELINE.json configs[2]): DTU 1600x1184, 5 views, 3-stage 48/32/8 hypotheses, bf16 storage
+on 1x MI355X; synthetic seeded images/cameras, synthetic weights with calibrated BN statistics
+(no checkpoints or datasets exist offline). One step = one full CascadeMVSNet forward
+(front-end + 3 x (hypotheses, [GeoFeatureFusion], DepthNet)) over one batch per GPU, inputs resident
+in HBM. Multi-GPU: one process per GPU, each processing its own batch (reference views are
+independent units: weak scaling, no collective in the data path); timing = max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+CONFIGS = {
+    # name: (H, W, views, ndepths, dtype, description)
+    "cfgA": (256, 320, 3, (48, 32, 8), torch.float32, "DTU 320x256, ref+2 src, fp32"),
+    "cfgB": (512, 640, 5, (48, 32, 8), torch.float32, "DTU 640x512, 5 views, 3-stage 48/32/8, fp32"),
+    "cfgC": (1184, 1600, 5, (48, 32, 8), torch.bfloat16, "DTU 1600x1184, 5 views, 3-stage 48/32/8, bf16"),
+    "cfgD": (1184, 1600, 7, (64, 32, 8), torch.bfloat16, "DTU 1600x1184, 7 views, 3-stage 64/32/8, bf16"),
+    "cfgE": (1056, 1920, 11, (64, 32, 8), torch.bfloat16, "T&T 1920x1056, 11 views, 3-stage 64/32/8, bf16"),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def build_model(ndepths, dtype, device):
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.weights import synthetic_state_dict, apply_bn_stats
+    net = CascadeMVSNet(ndepths=list(ndepths), compute_dtype=dtype,
+                        frontend_dtype=torch.bfloat16 if dtype == torch.bfloat16 else None)
+    sd = synthetic_state_dict(net.state_dict(), 0)
+    g = np.load(os.path.join(REPO, "tests", "golden", "forward_cfgB_640x512.npz"))
+    sd = apply_bn_stats(sd, {k[4:]: g[k] for k in g.files if k.startswith("bn::")})
+    net.load_state_dict(sd)
+    return net.to(device).eval(), sd
+
+
+def make_inputs(B, N, H, W, device=None, seed=0):
+    from damvsnet_amd import synth
+    proj, ins, dv = synth.cameras(B, N, H, W)
+    imgs = torch.from_numpy(synth.images(B, N, H, W, seed=seed))
+    proj = {k: torch.from_numpy(v) for k, v in proj.items()}
+    ins = {k: torch.from_numpy(v) for k, v in ins.items()}
+    dv = torch.from_numpy(dv)
+    if device is not None:
+        imgs, dv = imgs.to(device), dv.to(device)
+        proj = {k: v.to(device) for k, v in proj.items()}
+        ins = {k: v.to(device) for k, v in ins.items()}
+    return imgs, proj, dv, ins
+
+
+class StageTimer:
+    """Records a HIP event on the current stream at every phase boundary (no host sync)."""
+
+    def __init__(self):
+        self.marks = []
+
+    def __call__(self, name):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.marks.append((name, e))
+
+    def per_phase_ms(self):
+        out = {}
+        for (n0, e0), (_, e1) in zip(self.marks, self.marks[1:]):
+            out.setdefault(n0, []).append(e0.elapsed_time(e1))
+        return out
+
+
+def warp_roofline(net, imgs, proj, dv, ins, stage, dtype, iters=20):
+    """Time the fused warp+aggregation kernel of one stage alone (HIP events on its stream).
+
+    Algorithmic bytes per launch: e * (N*C*h*w [features, read once]
+    + C*D*h*w [volume write]) + 4*D*h*w [fp32 hypotheses] + 4*B*(N-1)*12 [cameras].
+    """
+    from damvsnet_amd.depthnet import to_nhwc
+    from damvsnet_amd.engine import hypotheses
+    name = "stage%d" % (stage + 1)
+    B, N, _, H, W = imgs.shape
+    scale = (4, 2, 1)[stage]
+    with torch.no_grad():
+        feats = net.extract_features(imgs)
+        fs = [to_nhwc(f[name], dtype) for f in feats]
+        hyps = hypotheses(dv, net.ndepths[stage], H, W, scale)
+        eng = net.DepthNet.engine(stage, net.cost_regularization[stage], imgs.device)
+        eng.warp_aggregate(fs, proj[name], hyps)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            eng.warp_aggregate(fs, proj[name], hyps)
+        e1.record()
+        torch.cuda.synchronize()
+    # eng.warp_aggregate also runs proj_prepare (one tiny launch); measured with it.
+    ms = e0.elapsed_time(e1) / iters
+    D = net.ndepths[stage]
+    h, w, C = fs[0].shape[1], fs[0].shape[2], fs[0].shape[3]
+    es = 2 if dtype == torch.bfloat16 else 4
+    alg = es * (N * C * h * w * B + C * D * h * w * B) + 4 * D * h * w * B + 4 * B * (N - 1) * 12
+    return ms, alg
+
+
+def cpu_baseline(cfg, budget_s=60.0):
+    """The oracle (PyTorch CPU restatement of the reference forward, fp32) on this host's cores."""
+    from oracle import mvs_oracle as O
+    H, W, N, nd, _, _ = CONFIGS[cfg]
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.weights import synthetic_state_dict, apply_bn_stats
+    sd = synthetic_state_dict(CascadeMVSNet(ndepths=list(nd)).state_dict(), 0)
+    g = np.load(os.path.join(REPO, "tests", "golden", "forward_cfgB_640x512.npz"))
+    sd = apply_bn_stats(sd, {k[4:]: g[k] for k in g.files if k.startswith("bn::")})
+    imgs, proj, dv, _ = make_inputs(1, N, H, W)
+    times = []
+    t_start = time.time()
+    with torch.no_grad():
+        while True:
+            t0 = time.time()
+            O.cascade_forward(sd, imgs, proj, dv, nd, "adaptive")
+            times.append(time.time() - t0)
+            if len(times) >= 3 or time.time() - t_start + times[-1] > budget_s:
+                break
+    t = statistics.median(times)
+    return {"value": round(1.0 / t, 5), "unit": "depth maps/s", "cores": cores, "kind": "port",
+            "sample": "%d full forward(s) at %s (B=1, fp32, PyTorch CPU restatement of the reference), median %.2f s"
+                      % (len(times), cfg, t)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfgC", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=1, help="depth maps (reference views) per GPU per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=60.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    H, W, N, nd, dtype, desc = CONFIGS[args.config]
+    net, _ = build_model(nd, dtype, device)
+    imgs, proj, dv, ins = make_inputs(args.batch, N, H, W, device, seed=rank)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            net(imgs, proj, dv, ins)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        timer = StageTimer()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            net(imgs, proj, dv, ins, stage_hook=timer)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=device)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(t.item())
+    maps = args.steps * args.batch * world
+    phases = {k: round(statistics.mean(v), 3) for k, v in timer.per_phase_ms().items()}
+
+    result = None
+    if rank == 0:
+        ms, alg = warp_roofline(net, imgs, proj, dv, ins, 1, dtype)
+        achieved = alg / (ms * 1e-3) / 1e9
+        result = {
+            "metric": "depth maps/sec (full CascadeMVSNet forward)",
+            "value": round(maps / elapsed, 4),
+            "unit": "depth maps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
+            "data": "synthetic (seeded DTU-like images/cameras, synthetic weights with calibrated BN stats)",
+            "config": {"workload": "%s: %s" % (args.config, desc), "batch_per_gpu": args.batch,
+                       "global_batch": args.batch * world, "height": H, "width": W, "views": N,
+                       "ndepths": list(nd), "parallelism": "replicas x%d (reference views sharded over ranks)" % world},
+            "ms_per_stage": phases,
+            "roofline": {"kernel": "warp_aggregate stage2 (fused homography warp + adaptive aggregation)",
+                         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "ms_per_launch": round(ms, 4), "algorithmic_bytes": int(alg)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

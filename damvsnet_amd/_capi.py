@@ -1,0 +1,102 @@
+"""ctypes binding of libdamvs.so (include/damvs.h).
+
+The library is loaded from the package directory only (built in-tree by
+``damvsnet_amd.build``); there is no fallback: if it is missing or fails to load, every
+product entry point raises. ``torch`` is imported first so that the HIP runtime PyTorch
+already mapped (soname libamdhip64.so.7) is the one the library binds to.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the library load: shared HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdamvs.so")
+
+DAMVS_F32, DAMVS_BF16 = 0, 1
+DAMVS_AGG_ADAPTIVE, DAMVS_AGG_VARIANCE = 0, 1
+ERRORS = {-1: "DAMVS_E_ARG", -2: "DAMVS_E_SHAPE", -3: "DAMVS_E_DTYPE", -4: "DAMVS_E_HIP", -5: "DAMVS_E_NOMEM",
+          -6: "DAMVS_E_WORKSPACE"}
+
+c_int, c_float, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+
+
+class DamvsBN(ctypes.Structure):
+    _fields_ = [("weight", c_void_p), ("bias", c_void_p), ("running_mean", c_void_p), ("running_var", c_void_p),
+                ("eps", c_float)]
+
+
+class DamvsCostregParams(ctypes.Structure):
+    _fields_ = [("in_channels", c_int), ("base_channels", c_int), ("conv_weight", c_void_p * 10), ("bn", DamvsBN * 10),
+                ("prob_weight", c_void_p)]
+
+
+class DamvsAggweightParams(ctypes.Structure):
+    _fields_ = [("in_channels", c_int), ("w1", c_void_p), ("bn1", DamvsBN), ("w2", c_void_p), ("bn2", DamvsBN)]
+
+
+# (name, restype, argtypes) — the full exported surface of include/damvs.h
+SIGNATURES = (
+    ("damvs_abi_version", c_int, ()),
+    ("damvs_last_error_string", ctypes.c_char_p, ()),
+    ("damvs_stage_create", c_int, (ctypes.POINTER(DamvsCostregParams), ctypes.POINTER(DamvsAggweightParams), c_int,
+                                   c_int, ctypes.POINTER(c_void_p))),
+    ("damvs_stage_destroy", c_int, (c_void_p,)),
+    ("damvs_stage_workspace_size", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_size_t))),
+    ("damvs_stage_forward", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_void_p),
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
+                                    c_void_p)),
+    ("damvs_proj_prepare", c_int, (c_void_p, c_int, c_int, c_void_p, c_void_p)),
+    ("damvs_homo_warp", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                c_void_p)),
+    ("damvs_warp_aggregate", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_void_p),
+                                     c_void_p, c_void_p, c_void_p)),
+    ("damvs_costreg_logits", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t,
+                                     c_void_p)),
+    ("damvs_regress", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_void_p)),
+    ("damvs_hypotheses", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                 c_int, c_int, c_void_p)),
+)
+
+_lib = None
+
+
+class DamvsError(RuntimeError):
+    def __init__(self, rc, msg):
+        super().__init__("%s (%d): %s" % (ERRORS.get(rc, "DAMVS_E_?"), rc, msg))
+        self.rc = rc
+
+
+def load_library(path: str = LIB_PATH):
+    """Load and type the HIP library; raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError("libdamvs.so not found at %s — build it with `python -m damvsnet_amd.build` "
+                           "(the product has no CPU/eager fallback)" % path)
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = list(args)
+    if lib.damvs_abi_version() != 1:
+        raise RuntimeError("libdamvs ABI mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc: int):
+    if rc != 0:
+        raise DamvsError(rc, _lib.damvs_last_error_string().decode(errors="replace"))
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,133 @@
+"""Drop-in ``CascadeMVSNet`` (models/cas_mvsnet.py:137-319) on the MI355X engine.
+
+Same constructor arguments (including the misspelt ``depth_interals_ratio``), the same
+``state_dict`` keys (reference checkpoints load with strict=True, test_uni.py:223-224) and the
+same ``forward(imgs, proj_matrices, depth_values, intrinsics_matrices)`` -> dict (per-stage dicts
+plus the last stage's keys at top level). Two extra keyword arguments select precision:
+
+* ``compute_dtype``  storage of features / cost volumes in the HIP path: torch.float32 (parity
+  path, exact-f32 MFMA) or torch.bfloat16 (bf16 MFMA, fp32 accumulate, fp32 regression).
+* ``frontend_dtype`` autocast dtype of the 2D front-end (FeatureNet, GeoFeatureFusion), which runs
+  on PyTorch-ROCm in channels-last memory (SURVEY.md section 8(f) row f1 — next to be moved to HIP).
+
+Per stage: hypotheses (HIP) -> [GeoFeatureFusion, stages 2/3] -> DepthNet (HIP). The reference's
+host syncs (depth_values .cpu(), :191-193; stage-3 debug prints, :275-285) are not reproduced.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .depthnet import DepthNet
+from .engine import hypotheses
+from .frontend import FeatureNet, GeoFeatureFusion, ConvBNReLU2d
+from .layers import CostRegNet
+
+STAGE_SCALE = {"stage1": 4, "stage2": 2, "stage3": 1}
+
+
+class RefineNet(nn.Module):
+    """Key holder for models/module.py:594-606 (its forward is broken in the reference: F.cat)."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv1 = ConvBNReLU2d(4, 32, 3, 1, 1)
+        self.conv2 = ConvBNReLU2d(32, 32, 3, 1, 1)
+        self.conv3 = ConvBNReLU2d(32, 32, 3, 1, 1)
+        self.res = ConvBNReLU2d(32, 1, 3, 1, 1)
+
+
+class CascadeMVSNet(nn.Module):
+    def __init__(self, refine=False, ndepths=[64, 32, 8], depth_interals_ratio=[4, 2, 1], share_cr=False,
+                 grad_method="detach", arch_mode="fpn", cr_base_chs=[8, 8, 8], agg_mode="adaptive",
+                 compute_dtype=torch.float32, frontend_dtype=None):
+        super().__init__()
+        assert len(ndepths) == len(depth_interals_ratio)
+        if len(ndepths) != 3:
+            raise NotImplementedError("the reference wires GeoFeatureFusion for exactly 3 stages")
+        self.refine, self.share_cr = refine, share_cr
+        self.ndepths, self.depth_interals_ratio = list(ndepths), list(depth_interals_ratio)
+        self.grad_method, self.arch_mode, self.cr_base_chs = grad_method, arch_mode, list(cr_base_chs)
+        self.num_stage = len(ndepths)
+        self.stage_infos = {k: {"scale": float(v)} for k, v in STAGE_SCALE.items()}
+        self.compute_dtype = compute_dtype
+        self.frontend_dtype = frontend_dtype
+
+        self.feature = FeatureNet(base_channels=8, stride=4, num_stage=self.num_stage, arch_mode=arch_mode)
+        self.GeoFeatureFusionNet = GeoFeatureFusion(convolutional_layer_encoding="z", mask_type="basic",
+                                                    add_origin_feat_flag=True)
+        self.geo_reg_encodings = ["std", "z", "z", "z"]
+        if share_cr:
+            self.cost_regularization = CostRegNet(in_channels=self.feature.out_channels, base_channels=8)
+        else:
+            self.cost_regularization = nn.ModuleList(
+                [CostRegNet(in_channels=self.feature.out_channels[i], base_channels=self.cr_base_chs[i])
+                 for i in range(self.num_stage)])
+        if refine:
+            self.refine_network = RefineNet()
+        self.DepthNet = DepthNet(agg_mode, self.feature.out_channels, compute_dtype=compute_dtype)
+        self._channels_last = False
+
+    def _frontend_ctx(self, device):
+        if self.frontend_dtype is None or self.frontend_dtype == torch.float32:
+            return contextlib.nullcontext()
+        return torch.autocast(device_type="cuda", dtype=self.frontend_dtype)
+
+    def _prepare_frontend(self):
+        if not self._channels_last:
+            self.feature.to(memory_format=torch.channels_last)
+            self.GeoFeatureFusionNet.to(memory_format=torch.channels_last)
+            self._channels_last = True
+
+    def _apply(self, fn, *a, **k):
+        self._channels_last = False
+        return super()._apply(fn, *a, **k)
+
+    def extract_features(self, imgs):
+        """FeatureNet over all views in one batched call (BN in eval is per-sample)."""
+        B, N = imgs.shape[:2]
+        x = imgs.reshape(B * N, *imgs.shape[2:]).contiguous(memory_format=torch.channels_last)
+        with self._frontend_ctx(imgs.device):
+            f = self.feature(x)
+        return [{k: v.reshape(B, N, *v.shape[1:])[:, i] for k, v in f.items()} for i in range(N)]
+
+    def forward(self, imgs, proj_matrices, depth_values, intrinsics_matrices=None, stage_hook=None):
+        if self.refine:
+            raise NotImplementedError("refine=True: the reference RefineNet forward is not runnable "
+                                      "(models/module.py:602 calls F.cat)")
+        if not imgs.is_cuda:
+            raise ValueError("damvsnet_amd is a GPU engine: move the model and inputs to a HIP device")
+        hook = stage_hook or (lambda name: None)
+        self._prepare_frontend()
+        B, N, _, H, W = imgs.shape
+        hook("features")
+        features = self.extract_features(imgs)
+        outputs = {}
+        depth = exp_var = conf = None
+        for s in range(self.num_stage):
+            name = "stage%d" % (s + 1)
+            scale = STAGE_SCALE[name]
+            fs = [f[name] for f in features]
+            if s >= 1:
+                hook(name + ".geofusion")
+                with self._frontend_ctx(imgs.device):
+                    ref_img = F.interpolate(imgs[:, 0], scale_factor=1.0 / 2 ** (2 - s), mode="bilinear",
+                                            align_corners=False)
+                    dl = F.interpolate(depth.unsqueeze(1), scale_factor=2, mode="bilinear", align_corners=False)
+                    cl = F.interpolate(conf.unsqueeze(1), scale_factor=2, mode="bilinear", align_corners=False)
+                    fs[0] = self.GeoFeatureFusionNet(ref_img.contiguous(memory_format=torch.channels_last), dl, cl,
+                                                     depth_values, s, fs[0],
+                                                     None if intrinsics_matrices is None else intrinsics_matrices[name])
+            hook(name + ".hypotheses")
+            hyps = hypotheses(depth_values, self.ndepths[s], H, W, scale, depth, exp_var)
+            hook(name + ".depthnet")
+            cr = self.cost_regularization if self.share_cr else self.cost_regularization[s]
+            out = self.DepthNet(s, fs, proj_matrices[name], hyps, self.ndepths[s], cr)
+            depth, conf, exp_var = out["depth"], out["photometric_confidence"], out["variance"]
+            outputs[name] = out
+            outputs.update(out)
+        hook("end")
+        return outputs

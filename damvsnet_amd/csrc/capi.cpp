@@ -1,0 +1,476 @@
+// C ABI of libdamvs.so (include/damvs.h): parameter folding/packing at create time and
+// stream-ordered orchestration of the per-stage kernels.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "damvs.h"
+#include "damvs_internal.h"
+
+using namespace damvs;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return DAMVS_OK;
+  return fail(DAMVS_E_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define DAMVS_TRY(expr)            \
+  do {                             \
+    int _rc = (expr);              \
+    if (_rc != DAMVS_OK) return _rc; \
+  } while (0)
+
+uint16_t to_bf16(float f) {  // round to nearest even; NaN stays NaN
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+enum LayerKind { CONV_S1 = 0, CONV_S2 = 1, DECONV_S2 = 2 };
+
+struct LayerPlan {
+  int kind = 0, cin = 0, cout = 0, mt = 0, nphase = 0;
+  ConvPhase ph[kMaxPhases];
+  void* wpack = nullptr;
+  float* bias = nullptr;
+};
+
+size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+}  // namespace
+
+struct damvs_stage {
+  int C = 0, base = 0, mode = 0, dtype = 0, device = 0;
+  LayerPlan L[10];
+  float* prob_w = nullptr;  // device [kd][kh][kw][c]
+  float k1[32] = {0};
+  float s1 = 0, t1 = 0, s2 = 0, t2 = 0;
+};
+
+namespace {
+
+// Weight tap lists. Conv: t = kd*9 + kh*3 + kw at input offset k-1 (input = q*stride + k - 1).
+// ConvTranspose k3 s2 p1 op1, output parity p per dim: p = 0 -> {k=1 at input q},
+// p = 1 -> {k=0 at input q+1, k=2 at input q}   (from o = 2i - 1 + k).
+void build_phases(LayerPlan& P, int kchunk_k) {
+  auto kch = [&](int ntaps) { return (ntaps * P.cin + kchunk_k - 1) / kchunk_k; };
+  std::memset(P.ph, 0, sizeof(P.ph));
+  if (P.kind != DECONV_S2) {
+    P.nphase = 1;
+    ConvPhase& ph = P.ph[0];
+    ph.ntaps = 27;
+    for (int t = 0; t < 27; ++t) {
+      ph.tap[t][0] = (signed char)(t / 9 - 1);
+      ph.tap[t][1] = (signed char)((t / 3) % 3 - 1);
+      ph.tap[t][2] = (signed char)(t % 3 - 1);
+      ph.tap[t][3] = (signed char)t;  // weight tap index
+    }
+    ph.kchunks = kch(27);
+    return;
+  }
+  P.nphase = 8;
+  const int ks[2][2] = {{1, -1}, {0, 2}};
+  const int off[2][2] = {{0, 0}, {1, 0}};
+  const int cnt[2] = {1, 2};
+  for (int p = 0; p < 8; ++p) {
+    ConvPhase& ph = P.ph[p];
+    ph.pd = (p >> 2) & 1;
+    ph.ph = (p >> 1) & 1;
+    ph.pw = p & 1;
+    int t = 0;
+    for (int a = 0; a < cnt[ph.pd]; ++a)
+      for (int b = 0; b < cnt[ph.ph]; ++b)
+        for (int c = 0; c < cnt[ph.pw]; ++c) {
+          ph.tap[t][0] = (signed char)off[ph.pd][a];
+          ph.tap[t][1] = (signed char)off[ph.ph][b];
+          ph.tap[t][2] = (signed char)off[ph.pw][c];
+          ph.tap[t][3] = (signed char)(ks[ph.pd][a] * 9 + ks[ph.ph][b] * 3 + ks[ph.pw][c]);
+          ++t;
+        }
+    ph.ntaps = t;
+    ph.kchunks = kch(t);
+  }
+}
+
+// Pack BN-folded weights wf[co][ci][27] into A-fragment order:
+//   element ((w_off + s*MT + m) * 64 + lane) * E + e  =  W[co = m*16 + (lane & 15)][k = s*KC + (lane >> 4)*E + e]
+// with k -> (tap t = k / cin, ci = k % cin), zero beyond ntaps / cout.
+template <typename S>
+void pack_layer(LayerPlan& P, const std::vector<float>& wf, int E, std::vector<S>& out, S (*cvt)(float)) {
+  const int KC = 4 * E;
+  int w_off = 0;
+  for (int p = 0; p < P.nphase; ++p) {
+    ConvPhase& ph = P.ph[p];
+    ph.w_off = w_off;
+    for (int s = 0; s < ph.kchunks; ++s)
+      for (int m = 0; m < P.mt; ++m)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e = 0; e < E; ++e) {
+            const int co = m * 16 + (lane & 15);
+            const int k = s * KC + (lane >> 4) * E + e;
+            const int t = k / P.cin, ci = k % P.cin;
+            float v = 0.f;
+            if (co < P.cout && t < ph.ntaps) v = wf[((size_t)co * P.cin + ci) * 27 + (unsigned char)ph.tap[t][3]];
+            out.push_back(cvt(v));
+          }
+    w_off += ph.kchunks * P.mt;
+  }
+}
+
+float cvt_f32(float v) { return v; }
+uint16_t cvt_bf16(float v) { return to_bf16(v); }
+
+int fold_bn(const damvs_bn& bn, int c, std::vector<float>& scale, std::vector<float>& shift) {
+  if (!bn.weight || !bn.bias || !bn.running_mean || !bn.running_var) return fail(DAMVS_E_ARG, "null BatchNorm tensor");
+  scale.resize(c);
+  shift.resize(c);
+  for (int i = 0; i < c; ++i) {
+    const double inv = 1.0 / std::sqrt((double)bn.running_var[i] + (double)bn.eps);
+    scale[i] = (float)(inv * bn.weight[i]);
+    shift[i] = (float)(bn.bias[i] - bn.running_mean[i] * inv * bn.weight[i]);
+  }
+  return DAMVS_OK;
+}
+
+int upload(const void* host, size_t bytes, void** dev) {
+  if (hipMalloc(dev, bytes) != hipSuccess) return fail(DAMVS_E_NOMEM, "hipMalloc(%zu) failed", bytes);
+  return hip_check(hipMemcpy(*dev, host, bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
+}
+
+struct Shapes {
+  int D[4], H[4], W[4];  // level 0 (full), 1 (/2), 2 (/4), 3 (/8)
+};
+
+Shapes level_shapes(int D, int h, int w) {
+  Shapes s;
+  for (int l = 0; l < 4; ++l) {
+    s.D[l] = D >> l;
+    s.H[l] = h >> l;
+    s.W[l] = w >> l;
+  }
+  return s;
+}
+
+struct Workspace {
+  size_t rt, vol, c[7], logits, total;
+};
+
+// c[i] holds conv_i's output for i = 0..6 (conv7/9/11 accumulate in place into c4/c2/c0).
+Workspace plan_ws(const damvs_stage* st, int B, int N, int D, int h, int w) {
+  const size_t es = st->dtype == DAMVS_BF16 ? 2 : 4;
+  const size_t V = (size_t)B * D * h * w;
+  const int b = st->base;
+  const size_t sz[7] = {V * b, V / 8 * 2 * b, V / 8 * 2 * b, V / 64 * 4 * b, V / 64 * 4 * b, V / 512 * 8 * b,
+                        V / 512 * 8 * b};
+  Workspace ws;
+  size_t o = 0;
+  ws.rt = o;
+  o += align_up((size_t)B * (N > 1 ? N - 1 : 1) * 12 * 4);
+  ws.vol = o;
+  o += align_up(V * st->C * es);
+  for (int i = 0; i < 7; ++i) {
+    ws.c[i] = o;
+    o += align_up(sz[i] * es);
+  }
+  ws.logits = o;
+  o += align_up(V * 4);
+  ws.total = o;
+  return ws;
+}
+
+int check_stage_shape(const damvs_stage* st, int B, int N, int D, int h, int w) {
+  if (B < 1 || N < 2 || N > kMaxViews) return fail(DAMVS_E_SHAPE, "need B >= 1 and 2 <= N <= %d (got B=%d N=%d)", kMaxViews, B, N);
+  if (D < 8 || h < 8 || w < 8 || D % 8 || h % 8 || w % 8)
+    return fail(DAMVS_E_SHAPE, "D, h, w must be positive multiples of 8 (got D=%d h=%d w=%d)", D, h, w);
+  (void)st;
+  return DAMVS_OK;
+}
+
+ConvArgs conv_args(const damvs_stage* st, int li, int B, const Shapes& S, int lin, int lout, const void* in, void* out,
+                   const void* resid) {
+  const LayerPlan& P = st->L[li];
+  ConvArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.in = in;
+  a.out = out;
+  a.resid = resid;
+  a.wpack = P.wpack;
+  a.bias = P.bias;
+  a.B = B;
+  a.Cin = P.cin;
+  a.Cout = P.cout;
+  a.MT = P.mt;
+  a.Di = S.D[lin]; a.Hi = S.H[lin]; a.Wi = S.W[lin];
+  a.Do = S.D[lout]; a.Ho = S.H[lout]; a.Wo = S.W[lout];
+  if (P.kind == DECONV_S2) {  // iterate over the input grid, one phase per output parity
+    a.Dq = a.Di; a.Hq = a.Hi; a.Wq = a.Wi;
+    a.in_stride = 1;
+    a.out_stride = 2;
+  } else {
+    a.Dq = a.Do; a.Hq = a.Ho; a.Wq = a.Wo;
+    a.in_stride = P.kind == CONV_S2 ? 2 : 1;
+    a.out_stride = 1;
+  }
+  a.relu = 1;
+  a.nphase = P.nphase;
+  std::memcpy(a.ph, P.ph, sizeof(a.ph));
+  return a;
+}
+
+int run_costreg(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, const void* vol, char* ws,
+                const Workspace& W, float* logits, const float* prob_init) {
+  const Shapes S = level_shapes(D, h, w);
+  void* c[7];
+  for (int i = 0; i < 7; ++i) c[i] = ws + W.c[i];
+  // encoder: (layer, in level, out level, input, output)
+  struct Step { int li, lin, lout; const void* in; void* out; const void* res; };
+  const Step steps[10] = {
+      {0, 0, 0, vol, c[0], nullptr},  {1, 0, 1, c[0], c[1], nullptr}, {2, 1, 1, c[1], c[2], nullptr},
+      {3, 1, 2, c[2], c[3], nullptr}, {4, 2, 2, c[3], c[4], nullptr}, {5, 2, 3, c[4], c[5], nullptr},
+      {6, 3, 3, c[5], c[6], nullptr}, {7, 3, 2, c[6], c[4], c[4]},    {8, 2, 1, c[4], c[2], c[2]},
+      {9, 1, 0, c[2], c[0], c[0]}};
+  for (const Step& k : steps) {
+    ConvArgs a = conv_args(st, k.li, B, S, k.lin, k.lout, k.in, k.out, k.res);
+    DAMVS_TRY(hip_check(launch_conv3d(s, st->dtype, a), "conv3d launch"));
+  }
+  DAMVS_TRY(hip_check(launch_prob_conv(s, st->dtype, B, st->base, D, h, w, c[0], st->prob_w, prob_init, logits),
+                      "prob conv launch"));
+  return DAMVS_OK;
+}
+
+WarpArgs warp_args(const damvs_stage* st, int B, int N, int C, int D, int h, int w, const void* const* feats,
+                   const float* rt, const float* hyps, void* out) {
+  WarpArgs a;
+  std::memset(&a, 0, sizeof(a));
+  for (int v = 0; v < N; ++v) a.feats[v] = feats[v];
+  a.rt = rt;
+  a.hyps = hyps;
+  a.out = out;
+  a.B = B; a.N = N; a.C = C; a.D = D; a.h = h; a.w = w;
+  if (st) {
+    std::memcpy(a.k1, st->k1, sizeof(a.k1));
+    a.s1 = st->s1; a.t1 = st->t1; a.s2 = st->s2; a.t2 = st->t2;
+  }
+  return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+int damvs_abi_version(void) { return DAMVS_ABI_VERSION; }
+
+const char* damvs_last_error_string(void) { return g_err.c_str(); }
+
+int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_params* aw, int agg_mode, int dtype,
+                       damvs_stage** out) {
+  if (!cr || !out) return fail(DAMVS_E_ARG, "null argument");
+  if (dtype != DAMVS_F32 && dtype != DAMVS_BF16) return fail(DAMVS_E_DTYPE, "dtype %d unsupported", dtype);
+  if (agg_mode != DAMVS_AGG_ADAPTIVE && agg_mode != DAMVS_AGG_VARIANCE) return fail(DAMVS_E_ARG, "agg_mode %d", agg_mode);
+  if (agg_mode == DAMVS_AGG_ADAPTIVE && !aw) return fail(DAMVS_E_ARG, "adaptive aggregation needs weight-net params");
+  const int C = cr->in_channels, b = cr->base_channels;
+  if (C != 8 && C != 16 && C != 32) return fail(DAMVS_E_SHAPE, "in_channels %d not in {8,16,32}", C);
+  if (b != 8 && b != 16) return fail(DAMVS_E_SHAPE, "base_channels %d not in {8,16}", b);
+  if (aw && aw->in_channels != C) return fail(DAMVS_E_SHAPE, "weight-net channels %d != %d", aw->in_channels, C);
+  for (int i = 0; i < 10; ++i)
+    if (!cr->conv_weight[i]) return fail(DAMVS_E_ARG, "null conv weight %d", i);
+  if (!cr->prob_weight) return fail(DAMVS_E_ARG, "null prob weight");
+
+  damvs_stage* st = new damvs_stage();
+  st->C = C;
+  st->base = b;
+  st->mode = agg_mode;
+  st->dtype = dtype;
+  (void)hipGetDevice(&st->device);
+  const int E = dtype == DAMVS_BF16 ? 8 : 4;
+  // (cin, cout, kind) of conv0..conv6, conv7, conv9, conv11
+  const int spec[10][3] = {{C, b, CONV_S1},         {b, 2 * b, CONV_S2},     {2 * b, 2 * b, CONV_S1},
+                           {2 * b, 4 * b, CONV_S2}, {4 * b, 4 * b, CONV_S1}, {4 * b, 8 * b, CONV_S2},
+                           {8 * b, 8 * b, CONV_S1}, {8 * b, 4 * b, DECONV_S2}, {4 * b, 2 * b, DECONV_S2},
+                           {2 * b, b, DECONV_S2}};
+  int rc = DAMVS_OK;
+  for (int li = 0; li < 10 && rc == DAMVS_OK; ++li) {
+    LayerPlan& P = st->L[li];
+    P.cin = spec[li][0];
+    P.cout = spec[li][1];
+    P.kind = spec[li][2];
+    P.mt = (P.cout + 15) / 16;
+    if (P.mt == 3) P.mt = 4;
+    build_phases(P, 4 * E);
+    std::vector<float> scale, shift;
+    rc = fold_bn(cr->bn[li], P.cout, scale, shift);
+    if (rc != DAMVS_OK) break;
+    // normalise to wf[co][ci][27] with BN scale folded in
+    std::vector<float> wf((size_t)P.cout * P.cin * 27);
+    const float* W = cr->conv_weight[li];
+    for (int co = 0; co < P.cout; ++co)
+      for (int ci = 0; ci < P.cin; ++ci)
+        for (int t = 0; t < 27; ++t) {
+          const float v = P.kind == DECONV_S2 ? W[((size_t)ci * P.cout + co) * 27 + t] : W[((size_t)co * P.cin + ci) * 27 + t];
+          wf[((size_t)co * P.cin + ci) * 27 + t] = v * scale[co];
+        }
+    if (dtype == DAMVS_BF16) {
+      std::vector<uint16_t> pk;
+      pack_layer<uint16_t>(P, wf, E, pk, cvt_bf16);
+      rc = upload(pk.data(), pk.size() * 2, &P.wpack);
+    } else {
+      std::vector<float> pk;
+      pack_layer<float>(P, wf, E, pk, cvt_f32);
+      rc = upload(pk.data(), pk.size() * 4, &P.wpack);
+    }
+    if (rc == DAMVS_OK) rc = upload(shift.data(), shift.size() * 4, reinterpret_cast<void**>(&P.bias));
+  }
+  if (rc == DAMVS_OK) {
+    std::vector<float> pw((size_t)27 * b);  // [kd][kh][kw][c] from [1][c][kd][kh][kw]
+    for (int c = 0; c < b; ++c)
+      for (int t = 0; t < 27; ++t) pw[(size_t)t * b + c] = cr->prob_weight[(size_t)c * 27 + t];
+    rc = upload(pw.data(), pw.size() * 4, reinterpret_cast<void**>(&st->prob_w));
+  }
+  if (rc == DAMVS_OK && agg_mode == DAMVS_AGG_ADAPTIVE) {
+    std::vector<float> sc1, sh1, sc2, sh2;
+    rc = fold_bn(aw->bn1, 1, sc1, sh1);
+    if (rc == DAMVS_OK) rc = fold_bn(aw->bn2, 1, sc2, sh2);
+    if (rc == DAMVS_OK) {
+      if (!aw->w1 || !aw->w2) {
+        rc = fail(DAMVS_E_ARG, "null weight-net conv");
+      } else {
+        for (int c = 0; c < C; ++c) st->k1[c] = aw->w1[c];
+        st->s1 = sc1[0];
+        st->t1 = sh1[0];
+        st->s2 = aw->w2[0] * sc2[0];
+        st->t2 = sh2[0];
+      }
+    }
+  }
+  if (rc != DAMVS_OK) {
+    damvs_stage_destroy(st);
+    return rc;
+  }
+  *out = st;
+  return DAMVS_OK;
+}
+
+int damvs_stage_destroy(damvs_stage* st) {
+  if (!st) return DAMVS_OK;
+  for (auto& P : st->L) {
+    if (P.wpack) (void)hipFree(P.wpack);
+    if (P.bias) (void)hipFree(P.bias);
+  }
+  if (st->prob_w) (void)hipFree(st->prob_w);
+  delete st;
+  return DAMVS_OK;
+}
+
+int damvs_stage_workspace_size(const damvs_stage* st, int B, int N, int D, int h, int w, size_t* bytes) {
+  if (!st || !bytes) return fail(DAMVS_E_ARG, "null argument");
+  DAMVS_TRY(check_stage_shape(st, B, N, D, h, w));
+  *bytes = plan_ws(st, B, N, D, h, w).total;
+  return DAMVS_OK;
+}
+
+int damvs_stage_forward(const damvs_stage* st, void* stream, int B, int N, int D, int h, int w,
+                        const void* const* feats, const float* proj, const float* hyps, const float* prob_init,
+                        void* workspace, size_t workspace_bytes, float* depth, float* conf, float* var,
+                        float* prob) {
+  if (!st || !feats || !proj || !hyps || !workspace || !depth || !conf || !var) return fail(DAMVS_E_ARG, "null argument");
+  DAMVS_TRY(check_stage_shape(st, B, N, D, h, w));
+  for (int v = 0; v < N; ++v)
+    if (!feats[v]) return fail(DAMVS_E_ARG, "null feature pointer for view %d", v);
+  const Workspace W = plan_ws(st, B, N, D, h, w);
+  if (workspace_bytes < W.total) return fail(DAMVS_E_WORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, W.total);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  char* ws = reinterpret_cast<char*>(workspace);
+  float* rt = reinterpret_cast<float*>(ws + W.rt);
+  DAMVS_TRY(hip_check(launch_proj_prepare(s, B, N, proj, rt), "proj_prepare launch"));
+  WarpArgs wa = warp_args(st, B, N, st->C, D, h, w, feats, rt, hyps, ws + W.vol);
+  DAMVS_TRY(hip_check(launch_warp_aggregate(s, st->dtype, st->mode, wa), "warp_aggregate launch"));
+  float* logits = reinterpret_cast<float*>(ws + W.logits);
+  DAMVS_TRY(run_costreg(st, s, B, D, h, w, ws + W.vol, ws, W, logits, prob_init));
+  DAMVS_TRY(hip_check(launch_regress(s, B, D, h, w, logits, hyps, depth, conf, var, prob), "regress launch"));
+  return DAMVS_OK;
+}
+
+int damvs_proj_prepare(void* stream, int B, int N, const float* proj, float* rt) {
+  if (!proj || !rt) return fail(DAMVS_E_ARG, "null argument");
+  if (B < 1 || N < 2) return fail(DAMVS_E_SHAPE, "need B >= 1, N >= 2");
+  return hip_check(launch_proj_prepare(reinterpret_cast<hipStream_t>(stream), B, N, proj, rt), "proj_prepare launch");
+}
+
+int damvs_homo_warp(void* stream, int dtype, int B, int C, int D, int h, int w, const void* src, const float* rt,
+                    const float* hyps, void* out) {
+  if (!src || !rt || !hyps || !out) return fail(DAMVS_E_ARG, "null argument");
+  if (dtype != DAMVS_F32 && dtype != DAMVS_BF16) return fail(DAMVS_E_DTYPE, "dtype %d unsupported", dtype);
+  if (C != 8 && C != 16 && C != 32) return fail(DAMVS_E_SHAPE, "C %d not in {8,16,32}", C);
+  if (B < 1 || D < 1 || h < 2 || w < 2) return fail(DAMVS_E_SHAPE, "bad shape");
+  const void* feats[2] = {src, src};
+  WarpArgs a = warp_args(nullptr, B, 2, C, D, h, w, feats, rt, hyps, out);
+  return hip_check(launch_warp_aggregate(reinterpret_cast<hipStream_t>(stream), dtype, AGG_WARP_ONLY, a),
+                   "homo_warp launch");
+}
+
+int damvs_warp_aggregate(const damvs_stage* st, void* stream, int B, int N, int D, int h, int w,
+                         const void* const* feats, const float* rt, const float* hyps, void* volume) {
+  if (!st || !feats || !rt || !hyps || !volume) return fail(DAMVS_E_ARG, "null argument");
+  if (B < 1 || N < 2 || N > kMaxViews || D < 1 || h < 2 || w < 2) return fail(DAMVS_E_SHAPE, "bad shape");
+  WarpArgs a = warp_args(st, B, N, st->C, D, h, w, feats, rt, hyps, volume);
+  return hip_check(launch_warp_aggregate(reinterpret_cast<hipStream_t>(stream), st->dtype, st->mode, a),
+                   "warp_aggregate launch");
+}
+
+int damvs_costreg_logits(const damvs_stage* st, void* stream, int B, int D, int h, int w, const void* volume,
+                         void* workspace, size_t workspace_bytes, float* logits) {
+  if (!st || !volume || !workspace || !logits) return fail(DAMVS_E_ARG, "null argument");
+  DAMVS_TRY(check_stage_shape(st, B, 2, D, h, w));
+  const Workspace W = plan_ws(st, B, 2, D, h, w);
+  if (workspace_bytes < W.total) return fail(DAMVS_E_WORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, W.total);
+  return run_costreg(st, reinterpret_cast<hipStream_t>(stream), B, D, h, w, volume,
+                     reinterpret_cast<char*>(workspace), W, logits, nullptr);
+}
+
+int damvs_regress(void* stream, int B, int D, int h, int w, const float* logits, const float* hyps,
+                  const float* prob_init, float* depth, float* conf, float* var, float* prob) {
+  if (!logits || !hyps || !depth || !conf || !var) return fail(DAMVS_E_ARG, "null argument");
+  if (prob_init) return fail(DAMVS_E_ARG, "prob_init is applied by damvs_stage_forward; add it to the logits");
+  if (B < 1 || D < 1 || h < 1 || w < 1) return fail(DAMVS_E_SHAPE, "bad shape");
+  return hip_check(launch_regress(reinterpret_cast<hipStream_t>(stream), B, D, h, w, logits, hyps, depth, conf, var,
+                                  prob),
+                   "regress launch");
+}
+
+int damvs_hypotheses(void* stream, int B, int D, int H, int W, int scale, const float* depth_values, int Dv,
+                     const float* prev_depth, const float* prev_var, int hp, int wp, float* hyps) {
+  if (!hyps) return fail(DAMVS_E_ARG, "null argument");
+  if (B < 1 || D < 2 || H < 1 || W < 1 || scale < 1 || H % scale || W % scale) return fail(DAMVS_E_SHAPE, "bad shape");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!prev_depth) {
+    if (!depth_values || Dv < 2) return fail(DAMVS_E_ARG, "stage 1 needs depth_values with Dv >= 2");
+    return hip_check(launch_hyp_linear(s, B, D, H / scale, W / scale, depth_values, Dv, hyps), "hyp_linear launch");
+  }
+  if (!prev_var) return fail(DAMVS_E_ARG, "refinement needs prev_var");
+  if (scale != 1 && scale != 2) return fail(DAMVS_E_SHAPE, "refinement scale must be 1 or 2 (got %d)", scale);
+  if (hp < 1 || wp < 1) return fail(DAMVS_E_SHAPE, "bad previous-stage shape");
+  return hip_check(launch_hyp_refine(s, B, D, H, W, scale, prev_depth, prev_var, hp, wp, hyps), "hyp_refine launch");
+}
+
+}  // extern "C"

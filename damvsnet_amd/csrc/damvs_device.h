@@ -1,0 +1,62 @@
+// Device-side helpers: storage conversion and 16-byte vector access for NHWC / NDHWC data.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "damvs_internal.h"
+
+namespace damvs {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+__device__ __forceinline__ float bf2f(uint32_t u16) { return __uint_as_float(u16 << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+
+// Storage traits: E = elements per 16-byte chunk.
+template <typename T> struct Stor;
+template <> struct Stor<float> {
+  static constexpr int E = 4;
+  __device__ __forceinline__ static void load16(const float* p, float* v) {
+    float4 q = *reinterpret_cast<const float4*>(p);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  }
+  __device__ __forceinline__ static void store16(float* p, const float* v) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  __device__ __forceinline__ static float ld(const float* p) { return *p; }
+};
+template <> struct Stor<bf16_t> {
+  static constexpr int E = 8;
+  __device__ __forceinline__ static void load16(const bf16_t* p, float* v) {
+    uint4 q = *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ __forceinline__ static void store16(bf16_t* p, const float* v) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  __device__ __forceinline__ static float ld(const bf16_t* p) { return bf2f(*p); }
+};
+
+// Load / store C contiguous channels (C a multiple of Stor<T>::E).
+template <typename T, int C>
+__device__ __forceinline__ void load_vec(const T* p, float* v) {
+#pragma unroll
+  for (int i = 0; i < C; i += Stor<T>::E) Stor<T>::load16(p + i, v + i);
+}
+template <typename T, int C>
+__device__ __forceinline__ void store_vec(T* p, const float* v) {
+#pragma unroll
+  for (int i = 0; i < C; i += Stor<T>::E) Stor<T>::store16(p + i, v + i);
+}
+
+}  // namespace damvs

@@ -1,0 +1,75 @@
+// Internal declarations shared by the HIP kernels and the C-ABI layer (not installed).
+//
+// Layouts (all device, row-major, innermost last):
+//   features  [B][h][w][C]            (NHWC, T = float | bf16)
+//   volume    [B][D][h][w][C]         (NDHWC, T)
+//   hyps      [B][D][h][w]            float
+//   rt        [B][N-1][12]            float: R row-major (9) then t (3) of P_src * inv(P_ref)
+//   logits    [B][D][h][w]            float
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace damvs {
+
+typedef uint16_t bf16_t;  // bf16 storage (upper half of an IEEE f32)
+
+enum StoreType { ST_F32 = 0, ST_BF16 = 1 };
+enum AggMode { AGG_ADAPTIVE = 0, AGG_VARIANCE = 1, AGG_WARP_ONLY = 2 };
+
+constexpr int kMaxViews = 16;
+constexpr int kMaxPhases = 8;
+
+// ---------------------------------------------------------------- warp + aggregation
+struct WarpArgs {
+  const void* feats[kMaxViews];  // N views, view 0 = reference
+  const float* rt;               // [B][N-1][12]
+  const float* hyps;             // [B][D][h][w]
+  void* out;                     // [B][D][h][w][C]
+  int B, N, C, D, h, w;
+  // adaptive weight net, BN folded: a = relu(sum_c k1[c] x_c * s1 + t1); wt = relu(a * s2 + t2)
+  float k1[32];
+  float s1, t1, s2, t2;
+};
+
+// ---------------------------------------------------------------- MFMA implicit-GEMM conv3d
+// A "phase" is one regular sub-convolution: for an iteration-grid point q,
+//   input  coord = q * in_stride + tap_offset        (zero outside the input)
+//   output coord = q * out_stride + (pd, ph, pw)
+// Conv3d k3 s1/s2 has one phase with 27 taps; ConvTranspose3d k3 s2 p1 op1 is 8 phases of
+// 1..8 taps each (sub-pixel decomposition), so no MFMA work is spent on structural zeros.
+struct ConvPhase {
+  int ntaps, kchunks, w_off, pd, ph, pw;
+  signed char tap[27][4];  // dz, dy, dx, (pad)
+};
+
+struct ConvArgs {
+  const void* in;
+  void* out;
+  const void* resid;   // added after ReLU (may alias out); nullptr if none
+  const void* wpack;   // packed A fragments, see pack_conv_weights()
+  const float* bias;   // [Cout] (folded BN shift)
+  int B, Cin, Cout, MT;
+  int Di, Hi, Wi;
+  int Dq, Hq, Wq;
+  int Do, Ho, Wo;
+  int in_stride, out_stride;
+  int relu;
+  int nphase;
+  ConvPhase ph[kMaxPhases];
+};
+
+// ---------------------------------------------------------------- launchers (return hipError_t)
+hipError_t launch_proj_prepare(hipStream_t s, int B, int N, const float* proj, float* rt);
+hipError_t launch_hyp_linear(hipStream_t s, int B, int D, int h, int w, const float* dv, int Dv, float* out);
+hipError_t launch_hyp_refine(hipStream_t s, int B, int D, int H, int W, int scale, const float* pd,
+                             const float* pv, int hp, int wp, float* out);
+hipError_t launch_warp_aggregate(hipStream_t s, int store, int mode, const WarpArgs& a);
+hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a);
+hipError_t launch_prob_conv(hipStream_t s, int store, int B, int Cb, int D, int h, int w, const void* feat,
+                            const float* wprob, const float* prob_init, float* logits);
+hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float* logits, const float* hyps,
+                          float* depth, float* conf, float* var, float* prob);
+
+}  // namespace damvs

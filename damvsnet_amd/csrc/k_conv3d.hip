@@ -1,0 +1,192 @@
+// MFMA implicit-GEMM 3D convolution for the cost-regularisation U-Net (CostRegNet,
+// models/module.py:510-541; wrappers Conv3d :117-159 and Deconv3d :161-202).
+//
+// Every layer is conv(bias=False) + BatchNorm3d (eval) + ReLU, optionally followed by a skip add
+// (:537-539). BN is folded into the packed weights (scale) and a per-channel bias (shift); the
+// ReLU and skip add run in the epilogue, so each layer is one read of its input and one write of
+// its output (the skip tensor is read and overwritten in place).
+//
+// GEMM mapping (per 64-lane wave, 16x16 MFMA tiles):
+//   A (M x K)  = folded weights, M = output channels (16 per tile, padded), K = taps x Cin
+//   B (K x N)  = input patches,  N = 16 consecutive output voxels (one per lane column)
+//   C (M x N)  = lane holds 4 consecutive output channels of one voxel -> one 8/16-byte store.
+// With the NDHWC layout the B fragment of a lane is ONE 16-byte load: 8 bf16 (16x16x32 MFMA) or
+// 4 f32 (16x16x4 f32 MFMA, exact fp32 — no xf32 on gfx950) consecutive input channels of one
+// neighbouring voxel. Weights are pre-packed host side in exactly the A-fragment lane order.
+//
+// ConvTranspose3d(k3, s2, p1, op1) runs as 8 output-parity phases, each a dense sub-convolution
+// with 1..8 taps (sub-pixel decomposition): no MFMA work on the structural zeros a
+// zero-inserted transposed conv would carry.
+#include "damvs_device.h"
+
+namespace damvs {
+
+namespace {
+
+template <typename T> struct Frag;
+template <> struct Frag<float> {
+  typedef float4 raw;
+  __device__ __forceinline__ static void mma(const raw& w, const raw& x, f32x4_t& acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, x.w, acc, 0, 0, 0);
+  }
+  __device__ __forceinline__ static raw zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+};
+template <> struct Frag<bf16_t> {
+  typedef uint4 raw;
+  __device__ __forceinline__ static void mma(const raw& w, const raw& x, f32x4_t& acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, w), __builtin_bit_cast(bf16x8_t, x),
+                                                  acc, 0, 0, 0);
+  }
+  __device__ __forceinline__ static raw zero() { return make_uint4(0u, 0u, 0u, 0u); }
+};
+
+template <typename T>
+__device__ __forceinline__ void store4(T* p, const float* r);
+template <>
+__device__ __forceinline__ void store4<float>(float* p, const float* r) {
+  *reinterpret_cast<float4*>(p) = make_float4(r[0], r[1], r[2], r[3]);
+}
+template <>
+__device__ __forceinline__ void store4<bf16_t>(bf16_t* p, const float* r) {
+  uint32_t lo = (uint32_t)f2bf(r[0]) | ((uint32_t)f2bf(r[1]) << 16);
+  uint32_t hi = (uint32_t)f2bf(r[2]) | ((uint32_t)f2bf(r[3]) << 16);
+  *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
+}
+
+template <typename T>
+__device__ __forceinline__ void load4(const T* p, float* r);
+template <>
+__device__ __forceinline__ void load4<float>(const float* p, float* r) {
+  float4 v = *reinterpret_cast<const float4*>(p);
+  r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+}
+template <>
+__device__ __forceinline__ void load4<bf16_t>(const bf16_t* p, float* r) {
+  uint2 v = *reinterpret_cast<const uint2*>(p);
+  r[0] = __uint_as_float(v.x << 16); r[1] = __uint_as_float(v.x & 0xffff0000u);
+  r[2] = __uint_as_float(v.y << 16); r[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+
+constexpr int kGroups = 4;  // 16-voxel column groups per wave (64 output voxels per wave)
+
+template <typename T, int MT>
+__global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a) {
+  typedef typename Frag<T>::raw raw;
+  constexpr int E = Stor<T>::E;  // input channels per lane per K-chunk
+  constexpr int KC = 4 * E;      // K per chunk (4 lane groups)
+  const ConvPhase& ph = a.ph[blockIdx.y];
+  __shared__ int s_tap[32];
+  if (threadIdx.x < 27) {
+    const signed char* t = ph.tap[threadIdx.x];
+    s_tap[threadIdx.x] = ((int)(t[0] + 8)) | ((int)(t[1] + 8) << 8) | ((int)(t[2] + 8) << 16);
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const long long Qtot = (long long)a.B * a.Dq * a.Hq * a.Wq;
+  const long long base = ((long long)blockIdx.x * 4 + wave) * (kGroups * 16);
+  if (base >= Qtot) return;
+
+  int vb[kGroups], vz[kGroups], vy[kGroups], vx[kGroups];
+  bool valid[kGroups];
+#pragma unroll
+  for (int j = 0; j < kGroups; ++j) {
+    long long q = base + j * 16 + n;
+    valid[j] = q < Qtot;
+    if (!valid[j]) q = 0;
+    vx[j] = (int)(q % a.Wq); q /= a.Wq;
+    vy[j] = (int)(q % a.Hq); q /= a.Hq;
+    vz[j] = (int)(q % a.Dq);
+    vb[j] = (int)(q / a.Dq);
+  }
+
+  f32x4_t acc[kGroups][MT];
+#pragma unroll
+  for (int j = 0; j < kGroups; ++j)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
+  const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + (size_t)ph.w_off * 64 + lane;
+  const int IS = a.in_stride;
+
+  for (int s = 0; s < ph.kchunks; ++s) {
+    const int k0 = s * KC + g * E;
+    const int t = k0 / a.Cin;
+    const int ci = k0 - t * a.Cin;
+    const bool tv = t < ph.ntaps;
+    const int code = s_tap[tv ? t : 0];
+    const int dz = (code & 0xff) - 8, dy = ((code >> 8) & 0xff) - 8, dx = ((code >> 16) & 0xff) - 8;
+    raw wf[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * MT + m) * 64];
+    raw xf[kGroups];
+#pragma unroll
+    for (int j = 0; j < kGroups; ++j) {
+      const int iz = vz[j] * IS + dz, iy = vy[j] * IS + dy, ix = vx[j] * IS + dx;
+      const bool ok = valid[j] && tv && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+                      (unsigned)ix < (unsigned)a.Wi;
+      const size_t off = ok ? ((((size_t)vb[j] * a.Di + iz) * a.Hi + iy) * a.Wi + ix) * a.Cin + ci : 0;
+      raw v = *reinterpret_cast<const raw*>(in + off);  // unconditional load, select after
+      xf[j] = ok ? v : Frag<T>::zero();
+    }
+#pragma unroll
+    for (int j = 0; j < kGroups; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) Frag<T>::mma(wf[m], xf[j], acc[j][m]);
+  }
+
+  T* __restrict__ out = reinterpret_cast<T*>(a.out);
+  const T* __restrict__ res = reinterpret_cast<const T*>(a.resid);
+  const int OS = a.out_stride;
+#pragma unroll
+  for (int j = 0; j < kGroups; ++j) {
+    if (!valid[j]) continue;
+    const int oz = vz[j] * OS + ph.pd, oy = vy[j] * OS + ph.ph, ox = vx[j] * OS + ph.pw;
+    const size_t ob = ((((size_t)vb[j] * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * a.Cout;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int co = m * 16 + g * 4;
+      if (co >= a.Cout) continue;
+      float r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        r[i] = acc[j][m][i] + a.bias[co + i];
+        if (a.relu) r[i] = fmaxf(r[i], 0.f);
+      }
+      if (res) {
+        float q[4];
+        load4<T>(res + ob + co, q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] += q[i];
+      }
+      store4<T>(out + ob + co, r);
+    }
+  }
+}
+
+template <typename T>
+hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
+  long long Qtot = (long long)a.B * a.Dq * a.Hq * a.Wq;
+  long long per_block = 4LL * kGroups * 16;
+  dim3 grid((unsigned)((Qtot + per_block - 1) / per_block), a.nphase);
+  switch (a.MT) {
+    case 1: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1>), grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 2>), grid, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 4>), grid, dim3(256), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a) {
+  return store == ST_BF16 ? launch_t<bf16_t>(s, a) : launch_t<float>(s, a);
+}
+
+}  // namespace damvs

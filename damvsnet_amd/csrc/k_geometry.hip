@@ -1,0 +1,182 @@
+// Camera composition and depth-hypothesis generation.
+//
+//  proj_prepare : models/cas_mvsnet.py:44-47 (P = [K E[:3,:4]; E[3]]) and models/module.py:308-310
+//                 (M = P_src inv(P_ref), rot = M[:3,:3], trans = M[:3,3]) — one thread per (b, src view).
+//  hyp_linear   : stage-1 samples, models/module.py:1003-1010, then the identity trilinear of
+//                 models/cas_mvsnet.py:293-296.
+//  hyp_refine   : stage 2/3 uncertainty-aware samples, models/module.py:1011-1035, on the bilinear
+//                 upsample of the previous depth / exp-variance (models/cas_mvsnet.py:250-253) and the
+//                 trilinear downsample to stage resolution (:293-296), never materialising the
+//                 full-resolution (B,D,H,W) tensor the reference builds.
+#include "damvs_device.h"
+
+namespace damvs {
+
+namespace {
+
+__device__ void compose(const float* P, double out[4][4]) {
+  // P: [2][4][4]; P[0] extrinsic, P[1][:3][:3] intrinsics
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) out[i][j] = P[i * 4 + j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 4; ++j) {
+      double s = 0.0;
+      for (int k = 0; k < 3; ++k) s += (double)P[16 + i * 4 + k] * (double)P[k * 4 + j];
+      out[i][j] = (float)s;  // reference composes in fp32
+    }
+}
+
+__device__ bool invert4(const double a_in[4][4], double inv[4][4]) {
+  double a[4][8];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 8; ++j) a[i][j] = j < 4 ? a_in[i][j] : (j - 4 == i ? 1.0 : 0.0);
+  for (int c = 0; c < 4; ++c) {
+    int piv = c;
+    for (int r = c + 1; r < 4; ++r)
+      if (fabs(a[r][c]) > fabs(a[piv][c])) piv = r;
+    if (a[piv][c] == 0.0) return false;
+    if (piv != c)
+      for (int j = 0; j < 8; ++j) { double t = a[c][j]; a[c][j] = a[piv][j]; a[piv][j] = t; }
+    double d = 1.0 / a[c][c];
+    for (int j = 0; j < 8; ++j) a[c][j] *= d;
+    for (int r = 0; r < 4; ++r) {
+      if (r == c) continue;
+      double f = a[r][c];
+      for (int j = 0; j < 8; ++j) a[r][j] -= f * a[c][j];
+    }
+  }
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) inv[i][j] = a[i][j + 4];
+  return true;
+}
+
+__global__ void proj_prepare_kernel(int B, int N, const float* __restrict__ proj, float* __restrict__ rt) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * (N - 1)) return;
+  int b = i / (N - 1), v = i % (N - 1) + 1;
+  double R[4][4], S[4][4], Ri[4][4];
+  compose(proj + (size_t)(b * N) * 32, R);
+  compose(proj + (size_t)(b * N + v) * 32, S);
+  float* o = rt + (size_t)i * 12;
+  if (!invert4(R, Ri)) {
+    for (int k = 0; k < 12; ++k) o[k] = __builtin_nanf("");
+    return;
+  }
+  double M[3][4];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 4; ++c) {
+      double s = 0.0;
+      for (int k = 0; k < 4; ++k) s += S[r][k] * Ri[k][c];
+      M[r][c] = s;
+    }
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) o[r * 3 + c] = (float)M[r][c];
+  for (int r = 0; r < 3; ++r) o[9 + r] = (float)M[r][3];
+}
+
+__global__ void hyp_linear_kernel(int B, int D, int hw, const float* __restrict__ dv, int Dv, float* __restrict__ out) {
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  int d = blockIdx.y, b = blockIdx.z;
+  if (p >= hw) return;
+  float dmin = dv[b * Dv], dmax = dv[b * Dv + Dv - 1];
+  float itv = (dmax - dmin) / (float)(D - 1);
+  out[((size_t)b * D + d) * hw + p] = dmin + (float)d * itv;
+}
+
+// Bilinear (align_corners=False) source index, as aten's area_pixel_compute_source_index.
+__device__ __forceinline__ void src_index(float scale, int dst, int in_size, int& i0, int& i1, float& l0, float& l1) {
+  float s = scale * ((float)dst + 0.5f) - 0.5f;
+  s = s < 0.f ? 0.f : s;
+  i0 = (int)s;
+  i1 = i0 + (i0 < in_size - 1 ? 1 : 0);
+  l1 = s - (float)i0;
+  l0 = 1.f - l1;
+}
+
+struct FullResPoint {
+  float cur, var, low, step, mx, sum;
+};
+
+__device__ __forceinline__ float bilerp(const float* m, int wp, int y0, int y1, int x0, int x1, float ly0, float ly1,
+                                        float lx0, float lx1) {
+  return ly0 * (lx0 * m[y0 * wp + x0] + lx1 * m[y0 * wp + x1]) + ly1 * (lx0 * m[y1 * wp + x0] + lx1 * m[y1 * wp + x1]);
+}
+
+__global__ void hyp_refine_kernel(int B, int D, int H, int W, int scale, const float* __restrict__ pd,
+                                  const float* __restrict__ pv, int hp, int wp, float* __restrict__ out) {
+  const int h = H / scale, w = W / scale;
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  int b = blockIdx.y;
+  if (p >= h * w) return;
+  int y = p / w, x = p % w;
+  const float eps = 1e-12f;
+  const float sh = (float)hp / (float)H, sw = (float)wp / (float)W;
+  const float* md = pd + (size_t)b * hp * wp;
+  const float* mv = pv + (size_t)b * hp * wp;
+  const float rden = (float)D - 1.f;
+
+  FullResPoint P[4];
+  const int n = scale * scale;  // 1 or 4 full-resolution points feed this output
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k >= n) break;
+    int Y = y * scale + (k >> 1), X = x * scale + (k & 1);
+    if (scale == 1) { Y = y; X = x; }
+    int y0, y1, x0, x1;
+    float ly0, ly1, lx0, lx1;
+    src_index(sh, Y, hp, y0, y1, ly0, ly1);
+    src_index(sw, X, wp, x0, x1, lx0, lx1);
+    FullResPoint q;
+    q.cur = bilerp(md, wp, y0, y1, x0, x1, ly0, ly1, lx0, lx1);
+    q.var = bilerp(mv, wp, y0, y1, x0, x1, ly0, ly1, lx0, lx1);
+    q.low = -fminf(q.cur, q.var);
+    q.step = (q.var - q.low) / rden;
+    float den = q.var + eps;
+    float mx = -INFINITY;
+    for (int i = 0; i < D; ++i) mx = fmaxf(mx, 3.f * (q.low + q.step * (float)i) / den);
+    float s = 0.f;
+    for (int i = 0; i < D; ++i) s += expf(3.f * (q.low + q.step * (float)i) / den - mx);
+    q.mx = mx;
+    q.sum = s;
+    P[k] = q;
+  }
+  float* o = out + (size_t)b * D * h * w + p;
+  for (int i = 0; i < D; ++i) {
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k >= n) break;
+      const FullResPoint& q = P[k];
+      float den = q.var + eps;
+      float off = expf(3.f * (q.low + q.step * (float)i) / den - q.mx) / q.sum;
+      v[k] = (q.cur + q.low + q.step * (float)i + eps) + off * q.step;
+    }
+    float r = (scale == 1) ? v[0] : 0.5f * (0.5f * v[0] + 0.5f * v[1]) + 0.5f * (0.5f * v[2] + 0.5f * v[3]);
+    o[(size_t)i * h * w] = r;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_proj_prepare(hipStream_t s, int B, int N, const float* proj, float* rt) {
+  int n = B * (N - 1);
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(proj_prepare_kernel, dim3((n + 63) / 64), dim3(64), 0, s, B, N, proj, rt);
+  return hipGetLastError();
+}
+
+hipError_t launch_hyp_linear(hipStream_t s, int B, int D, int h, int w, const float* dv, int Dv, float* out) {
+  int hw = h * w;
+  hipLaunchKernelGGL(hyp_linear_kernel, dim3((hw + 255) / 256, D, B), dim3(256), 0, s, B, D, hw, dv, Dv, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_hyp_refine(hipStream_t s, int B, int D, int H, int W, int scale, const float* pd, const float* pv,
+                             int hp, int wp, float* out) {
+  int hw = (H / scale) * (W / scale);
+  hipLaunchKernelGGL(hyp_refine_kernel, dim3((hw + 255) / 256, B), dim3(256), 0, s, B, D, H, W, scale, pd, pv, hp, wp,
+                     out);
+  return hipGetLastError();
+}
+
+}  // namespace damvs

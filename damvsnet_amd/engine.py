@@ -1,0 +1,164 @@
+"""Host-side engine: owns one ``damvs_stage`` per (cascade stage, device, dtype) and launches the
+per-stage hot path through the C ABI on PyTorch's current HIP stream.
+
+PyTorch is plumbing here: device buffers come from its caching allocator and the stream is
+its current stream; all compute of the hot path happens in libdamvs.so.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _capi
+from ._capi import check, ptr
+
+DTYPES = {torch.float32: _capi.DAMVS_F32, torch.bfloat16: _capi.DAMVS_BF16}
+
+
+def _host(t):
+    return t.detach().to("cpu", torch.float32).contiguous()
+
+
+def _param_version(mod):
+    return tuple(t._version for t in list(mod.parameters()) + list(mod.buffers()))
+
+
+class StageEngine:
+    """Folded, packed weights of one stage (CostRegNet + weight net) resident on one device."""
+
+    def __init__(self, costreg, aggw, agg_mode: str, dtype: torch.dtype, device: torch.device):
+        lib = _capi.load_library()
+        if dtype not in DTYPES:
+            raise TypeError("compute dtype must be float32 or bfloat16, got %r" % (dtype,))
+        self.dtype, self.device, self.C = dtype, device, costreg.in_channels
+        self.mode = _capi.DAMVS_AGG_ADAPTIVE if agg_mode == "adaptive" else _capi.DAMVS_AGG_VARIANCE
+        keep = []  # host tensors must outlive the create call
+
+        def h(t):
+            t = _host(t)
+            keep.append(t)
+            return t.data_ptr()
+
+        def bn(m):
+            return _capi.DamvsBN(h(m.weight), h(m.bias), h(m.running_mean), h(m.running_var), float(m.eps))
+
+        layers = [getattr(costreg, n) for n in costreg.ENCODER + costreg.DECODER]
+        cp = _capi.DamvsCostregParams()
+        cp.in_channels, cp.base_channels = costreg.in_channels, costreg.base_channels
+        for i, m in enumerate(layers):
+            cp.conv_weight[i] = h(m.conv.weight)
+            cp.bn[i] = bn(m.bn)
+        cp.prob_weight = h(costreg.prob.weight)
+        ap = None
+        if self.mode == _capi.DAMVS_AGG_ADAPTIVE:
+            w0, w1 = aggw.w_net[0], aggw.w_net[1]
+            ap = _capi.DamvsAggweightParams(aggw.in_channels, h(w0.conv.weight), bn(w0.bn), h(w1.conv.weight), bn(w1.bn))
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            check(lib.damvs_stage_create(ctypes.byref(cp), ctypes.byref(ap) if ap is not None else None, self.mode,
+                                         DTYPES[dtype], ctypes.byref(handle)))
+        self.handle = handle
+        self._lib = lib
+        self._ws = None
+        self.version = _param_version(costreg) + (_param_version(aggw) if aggw is not None else ())
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                self._lib.damvs_stage_destroy(h)
+            except Exception:
+                pass
+
+    def workspace(self, B, N, D, h, w):
+        n = ctypes.c_size_t()
+        check(self._lib.damvs_stage_workspace_size(self.handle, B, N, D, h, w, ctypes.byref(n)))
+        if self._ws is None or self._ws.numel() < n.value:
+            self._ws = torch.empty(n.value, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def forward(self, feats_nhwc, proj, hyps, prob_init=None, want_prob=True):
+        """feats_nhwc: list of N (B,h,w,C) tensors of self.dtype; proj (B,N,2,4,4); hyps (B,D,h,w) float32."""
+        N = len(feats_nhwc)
+        B, h, w, C = feats_nhwc[0].shape
+        D = hyps.shape[1]
+        dev = self.device
+        ws = self.workspace(B, N, D, h, w)
+        depth = torch.empty(B, h, w, device=dev, dtype=torch.float32)
+        conf = torch.empty_like(depth)
+        var = torch.empty_like(depth)
+        prob = torch.empty(B, D, h, w, device=dev, dtype=torch.float32) if want_prob else None
+        fptrs = (ctypes.c_void_p * N)(*[f.data_ptr() for f in feats_nhwc])
+        check(self._lib.damvs_stage_forward(self.handle, _capi.stream_ptr(dev), B, N, D, h, w, fptrs, ptr(proj),
+                                            ptr(hyps), ptr(prob_init), ptr(ws), ws.numel(), ptr(depth), ptr(conf),
+                                            ptr(var), ptr(prob)))
+        return depth, conf, var, prob
+
+    # ---- split entry points (parity tests / sharded execution)
+    def warp_aggregate(self, feats_nhwc, proj, hyps):
+        N = len(feats_nhwc)
+        B, h, w, C = feats_nhwc[0].shape
+        D = hyps.shape[1]
+        rt = proj_prepare(proj)
+        vol = torch.empty(B, D, h, w, C, device=self.device, dtype=self.dtype)
+        fptrs = (ctypes.c_void_p * N)(*[f.data_ptr() for f in feats_nhwc])
+        check(self._lib.damvs_warp_aggregate(self.handle, _capi.stream_ptr(self.device), B, N, D, h, w, fptrs, ptr(rt),
+                                             ptr(hyps), ptr(vol)))
+        return vol
+
+    def costreg_logits(self, vol):
+        B, D, h, w, C = vol.shape
+        ws = self.workspace(B, 2, D, h, w)
+        logits = torch.empty(B, D, h, w, device=self.device, dtype=torch.float32)
+        check(self._lib.damvs_costreg_logits(self.handle, _capi.stream_ptr(self.device), B, D, h, w, ptr(vol), ptr(ws),
+                                              ws.numel(), ptr(logits)))
+        return logits
+
+
+def _check_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("damvsnet_amd runs on the GPU only; got a %s tensor" % t.device)
+
+
+def proj_prepare(proj):
+    """(B,N,2,4,4) -> (B,N-1,12) [R|t] of P_src inv(P_ref)."""
+    lib = _capi.load_library()
+    _check_cuda(proj)
+    proj = proj.float().contiguous()
+    B, N = proj.shape[:2]
+    rt = torch.empty(B, N - 1, 12, device=proj.device, dtype=torch.float32)
+    check(lib.damvs_proj_prepare(_capi.stream_ptr(proj.device), B, N, ptr(proj), ptr(rt)))
+    return rt
+
+
+def regress(logits, hyps, want_prob=True):
+    lib = _capi.load_library()
+    _check_cuda(logits, hyps)
+    B, D, h, w = logits.shape
+    logits, hyps = logits.float().contiguous(), hyps.float().contiguous()
+    depth = torch.empty(B, h, w, device=logits.device)
+    conf, var = torch.empty_like(depth), torch.empty_like(depth)
+    prob = torch.empty_like(logits) if want_prob else None
+    check(lib.damvs_regress(_capi.stream_ptr(logits.device), B, D, h, w, ptr(logits), ptr(hyps), None, ptr(depth),
+                            ptr(conf), ptr(var), ptr(prob)))
+    return depth, conf, var, prob
+
+
+def hypotheses(depth_values, ndepth, H, W, scale, prev_depth=None, prev_var=None):
+    """Stage hypotheses (B, ndepth, H/scale, W/scale) — see damvs_hypotheses in include/damvs.h."""
+    lib = _capi.load_library()
+    dev = depth_values.device
+    _check_cuda(depth_values, prev_depth, prev_var)
+    B = depth_values.shape[0]
+    out = torch.empty(B, ndepth, H // scale, W // scale, device=dev, dtype=torch.float32)
+    dv = depth_values.float().contiguous()
+    if prev_depth is None:
+        check(lib.damvs_hypotheses(_capi.stream_ptr(dev), B, ndepth, H, W, scale, ptr(dv), dv.shape[1], None, None, 0, 0,
+                                   ptr(out)))
+    else:
+        pd, pv = prev_depth.float().contiguous(), prev_var.float().contiguous()
+        check(lib.damvs_hypotheses(_capi.stream_ptr(dev), B, ndepth, H, W, scale, ptr(dv), dv.shape[1], ptr(pd), ptr(pv),
+                                   pd.shape[-2], pd.shape[-1], ptr(out)))
+    return out

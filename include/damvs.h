@@ -1,0 +1,140 @@
+/* damvs.h — C ABI of the MI355X cascade-MVS cost-volume engine (libdamvs.so).
+ *
+ * Drop-in boundary for the per-stage hot path of wsmtht520/DAMVSNet. The reference has no
+ * native/FFI layer; its boundary is the Python module API, which the
+ * package damvsnet_amd mirrors on top of this ABI. Each entry point names the reference
+ * interface it replaces (paths relative to the reference repo).
+ *
+ * Conventions
+ *   - Plain C types only. Tensor arguments are DEVICE pointers owned by the caller; parameter
+ *     structs passed to damvs_stage_create are HOST pointers (copied, BN-folded, packed).
+ *   - No allocation, no host synchronisation inside the *_forward / kernel entry points: work is
+ *     enqueued on `stream` (a hipStream_t, NULL = default stream) and is graph-capturable.
+ *   - Return 0 (DAMVS_OK) or a negative DAMVS_E_* code; damvs_last_error_string() gives the
+ *     message of the last failure on the calling thread.
+ *   - A damvs_stage is immutable after create and may be used concurrently from several threads
+ *     on different streams (workspaces must differ).
+ *   - Layouts: features NHWC [B][h][w][C]; cost volume NDHWC [B][D][h][w][C]; hypotheses,
+ *     logits and probabilities [B][D][h][w] float; projections [B][N][2][4][4] float with
+ *     [..,0,:,:] the world->camera extrinsic and [..,1,:3,:3] the stage intrinsics
+ *     (datasets/general_eval.py:158-175).
+ */
+#ifndef DAMVS_H
+#define DAMVS_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DAMVS_ABI_VERSION 1
+
+enum {
+  DAMVS_OK = 0,
+  DAMVS_E_ARG = -1,       /* null pointer / bad enum */
+  DAMVS_E_SHAPE = -2,     /* unsupported or inconsistent shape */
+  DAMVS_E_DTYPE = -3,     /* unsupported storage type */
+  DAMVS_E_HIP = -4,       /* HIP runtime error */
+  DAMVS_E_NOMEM = -5,     /* device allocation failed (create only) */
+  DAMVS_E_WORKSPACE = -6  /* workspace too small */
+};
+
+enum { DAMVS_F32 = 0, DAMVS_BF16 = 1 };                       /* storage of features / volumes */
+enum { DAMVS_AGG_ADAPTIVE = 0, DAMVS_AGG_VARIANCE = 1 };      /* models/cas_mvsnet.py:11-16 */
+
+/* BatchNorm in eval form: y = (x - running_mean) / sqrt(running_var + eps) * weight + bias. */
+typedef struct {
+  const float* weight;
+  const float* bias;
+  const float* running_mean;
+  const float* running_var;
+  float eps;
+} damvs_bn;
+
+/* CostRegNet (models/module.py:510-541). conv_weight[i] for i = 0..9 is
+ * conv0..conv6 (Conv3d, [Cout][Cin][3][3][3]) then conv7, conv9, conv11
+ * (ConvTranspose3d, [Cin][Cout][3][3][3]); bn[i] the matching BatchNorm3d;
+ * prob_weight is prob.weight [1][base][3][3][3] (no bias, no BN). */
+typedef struct {
+  int in_channels;
+  int base_channels;
+  const float* conv_weight[10];
+  damvs_bn bn[10];
+  const float* prob_weight;
+} damvs_costreg_params;
+
+/* AggWeightNetVolume (models/module.py:544-563): w_net.0 = Conv3d(C,1,1)+BN+ReLU (w1 is [C]),
+ * w_net.1 = Conv3d(1,1,1)+BN+ReLU (w2 is [1]). conv0 is unused by the reference forward. */
+typedef struct {
+  int in_channels;
+  const float* w1;
+  damvs_bn bn1;
+  const float* w2;
+  damvs_bn bn2;
+} damvs_aggweight_params;
+
+typedef struct damvs_stage damvs_stage;
+
+int damvs_abi_version(void);
+const char* damvs_last_error_string(void);
+
+/* One cascade stage's weights (replaces DepthNet.weight_net[s] + cost_regularization[s],
+ * models/cas_mvsnet.py:16,180-182). `aggw` may be NULL for DAMVS_AGG_VARIANCE. Uses the
+ * current HIP device. */
+int damvs_stage_create(const damvs_costreg_params* costreg, const damvs_aggweight_params* aggw, int agg_mode,
+                       int dtype, damvs_stage** out);
+int damvs_stage_destroy(damvs_stage* st);
+
+/* Bytes of device workspace damvs_stage_forward needs for this problem size. */
+int damvs_stage_workspace_size(const damvs_stage* st, int B, int N, int D, int h, int w, size_t* bytes);
+
+/* DepthNet.forward (models/cas_mvsnet.py:18-134) for one stage: warp + aggregation,
+ * CostRegNet, softmax regression, confidence, exp-variance.
+ *   feats[N]  : N device pointers (host array), view 0 = reference, each [B][h][w][C] of dtype
+ *   proj      : [B][N][2][4][4]      hyps: [B][D][h][w]      prob_init: NULL or [B][D][h][w]
+ *   depth, conf, var : [B][h][w]     prob: NULL or [B][D][h][w] (prob_volume output)
+ * D, h, w must be multiples of 8 (three stride-2 levels, models/module.py:515-528). */
+int damvs_stage_forward(const damvs_stage* st, void* stream, int B, int N, int D, int h, int w,
+                        const void* const* feats, const float* proj, const float* hyps, const float* prob_init,
+                        void* workspace, size_t workspace_bytes, float* depth, float* conf, float* var,
+                        float* prob);
+
+/* ---- split entry points (used by the parity tests and by sharded execution) ---- */
+
+/* Per (b, src view): 3x4 [R|t] of P_src * inv(P_ref) with P = [K E[:3,:4]; E[3]]
+ * (models/cas_mvsnet.py:44-47, models/module.py:308-310). rt: [B][N-1][12]. */
+int damvs_proj_prepare(void* stream, int B, int N, const float* proj, float* rt);
+
+/* homo_warping(src_fea, src_proj, ref_proj, depth_values) (models/module.py:297-332) for one source
+ * view: src [B][h][w][C], rt [B][12] (from damvs_proj_prepare with N = 2), hyps [B][D][h][w],
+ * out [B][D][h][w][C]. C in {8, 16, 32}. */
+int damvs_homo_warp(void* stream, int dtype, int B, int C, int D, int h, int w, const void* src, const float* rt,
+                    const float* hyps, void* out);
+
+/* Aggregated cost volume (models/cas_mvsnet.py:26-87): volume [B][D][h][w][C]. */
+int damvs_warp_aggregate(const damvs_stage* st, void* stream, int B, int N, int D, int h, int w,
+                         const void* const* feats, const float* rt, const float* hyps, void* volume);
+
+/* CostRegNet forward incl. the final prob conv (models/module.py:532-541): logits [B][D][h][w]. */
+int damvs_costreg_logits(const damvs_stage* st, void* stream, int B, int D, int h, int w, const void* volume,
+                         void* workspace, size_t workspace_bytes, float* logits);
+
+/* Softmax regression on logits (models/cas_mvsnet.py:105-124). prob_init / prob may be NULL. */
+int damvs_regress(void* stream, int B, int D, int h, int w, const float* logits, const float* hyps,
+                  const float* prob_init, float* depth, float* conf, float* var, float* prob);
+
+/* Stage hypotheses at stage resolution h = H/scale, w = W/scale (models/cas_mvsnet.py:238-296 with
+ * uncertainty_aware_samples, models/module.py:999-1038):
+ *   prev_depth == NULL : stage 1, linspace(depth_values[b,0], depth_values[b,Dv-1], D)
+ *   otherwise          : uncertainty-aware samples around prev_depth / prev_var ([B][hp][wp]),
+ *                        bilinearly upsampled to H x W, then trilinearly resampled to h x w.
+ * hyps: [B][D][h][w]. scale must be 1, 2 (refinement) or any value for stage 1. */
+int damvs_hypotheses(void* stream, int B, int D, int H, int W, int scale, const float* depth_values, int Dv,
+                     const float* prev_depth, const float* prev_var, int hp, int wp, float* hyps);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DAMVS_H */

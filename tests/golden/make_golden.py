@@ -1,0 +1,189 @@
+"""Generate the golden fixtures by importing the reference (build container only).
+
+Run from the repo root:  ``PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py``
+
+The reference (wsmtht520/DAMVSNet at /root/reference, read-only) is imported, never
+copied: its models are instantiated, loaded with this repo's seeded synthetic weights
+(``damvsnet_amd.weights.synthetic_state_dict``, matched by key with strict=True), BN
+running stats are calibrated with one train-mode pass (momentum=None), and the eval
+forward outputs are written as small ``.npz`` files next to this script. Inputs are
+regenerable from seeds (``damvsnet_amd.synth``) and each fixture records a checksum of them.
+
+``/root/reference`` does not exist on the GPU box; nothing there runs this script.
+The active model (models/cas_mvsnet.py) raises IndexError below 1019x576 (debug print at
+:275-285), so small-resolution fixtures use models/cas_mvsnet_origin0316.py, which is
+numerically identical.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from damvsnet_amd import synth  # noqa: E402
+from damvsnet_amd.weights import synthetic_state_dict, bn_stat_keys  # noqa: E402
+
+REF = "/root/reference"
+SEED = 0
+
+
+def import_reference():
+    tv = types.ModuleType("torchvision")
+    tvu = types.ModuleType("torchvision.utils")
+    tv.utils = tvu
+    sys.modules.setdefault("torchvision", tv)
+    sys.modules.setdefault("torchvision.utils", tvu)
+    sys.path.insert(0, REF)
+    import models.module as mod  # noqa
+    import models.cas_mvsnet as active  # noqa
+    import models.cas_mvsnet_origin0316 as origin  # noqa
+    return mod, active, origin
+
+
+def calibrate(model, run):
+    """One train-mode pass with cumulative BN stats, then eval."""
+    for m in model.modules():
+        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+            m.reset_running_stats()
+            m.momentum = None
+    model.train()
+    with torch.no_grad():
+        run()
+    model.eval()
+
+
+def checksum(*arrs):
+    return np.array([float(np.float64(np.asarray(a, dtype=np.float64).sum())) for a in arrs])
+
+
+def to_np(t):
+    return t.detach().cpu().numpy().astype(np.float32)
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, "%.1f KB" % (os.path.getsize(path) / 1024))
+
+
+def bn_stats(model, prefix=""):
+    sd = model.state_dict()
+    return {("bn::" + prefix + k): sd[k].numpy() for k in bn_stat_keys(sd)}
+
+
+def fixture_homo_warping(mod):
+    """homo_warping at small shapes with DTU-like cameras, per-pixel hypotheses."""
+    B, C, H, W, D = 1, 4, 12, 16, 5
+    proj, _, _ = synth.cameras(B, 3, 4 * H, 4 * W)  # stage1 of a 4x input => (H, W)
+    P = torch.from_numpy(proj["stage1"])
+    src = torch.from_numpy(synth.features(B, 3, C, H, W, seed=SEED)[2])
+    hyps = torch.from_numpy(synth.stage_hypotheses(B, D, H, W, seed=SEED))
+
+    def comp(p):
+        o = p[:, 0].clone()
+        o[:, :3, :4] = torch.matmul(p[:, 1, :3, :3], p[:, 0, :3, :4])
+        return o
+    out = mod.homo_warping(src, comp(P[:, 2]), comp(P[:, 0]), hyps)
+    save("homo_warping", out=to_np(out), chk=checksum(src, hyps, P))
+
+
+def fixture_costreg(mod):
+    """CostRegNet per stage channel count at a reduced volume, calibrated BN."""
+    arrays = {}
+    for s, C in enumerate((32, 16, 8)):
+        net = mod.CostRegNet(in_channels=C, base_channels=8)
+        sd = synthetic_state_dict(net.state_dict(), seed=SEED + s)
+        net.load_state_dict(sd, strict=True)
+        x = torch.from_numpy(synth.features(1, 1, C * 8, 16, 24, seed=SEED + 10 + s)[0].reshape(1, C, 8, 16, 24))
+        calibrate(net, lambda: net(x))
+        with torch.no_grad():
+            y = net(x)
+        arrays["logits%d" % s] = to_np(y)
+        arrays["chk%d" % s] = checksum(x)
+        for k, v in bn_stats(net).items():
+            arrays["s%d::%s" % (s, k)] = v
+    save("costreg", **arrays)
+
+
+def fixture_depthnet(active, mode, tag, B=1, N=3, H=256, W=320, D=8, stage_idx=2):
+    """cfgA: stage-3 DepthNet at 320x256, ref + 2 src, 8 hypotheses (BASELINE.json configs[0])."""
+    net = active.CascadeMVSNet(ndepths=[48, 32, 8], agg_mode=mode)
+    sd = synthetic_state_dict(net.state_dict(), seed=SEED)
+    net.load_state_dict(sd, strict=True)
+    C = net.feature.out_channels[stage_idx]
+    scale = 4 // (2 ** stage_idx)
+    proj, _, _ = synth.cameras(B, N, H * scale, W * scale)
+    P = torch.from_numpy(proj["stage%d" % (stage_idx + 1)])
+    f = synth.features(B, N, C, H, W, seed=SEED)
+    feats = [torch.from_numpy(f[v]) for v in range(N)]
+    hyps = torch.from_numpy(synth.stage_hypotheses(B, D, H, W, seed=SEED))
+    cr = net.cost_regularization[stage_idx]
+
+    def run():
+        return net.DepthNet(stage_idx, feats, P, hyps, D, cr)
+    calibrate(net, run)
+    with torch.no_grad():
+        out = run()
+    save("depthnet_" + tag, depth=to_np(out["depth"]), conf=to_np(out["photometric_confidence"]),
+         var=to_np(out["variance"]), prob=to_np(out["prob_volume"]), chk=checksum(f, hyps, P),
+         **bn_stats(net))
+
+
+def fixture_forward(origin, tag, B, N, H, W, ndepths, mode="adaptive", keep_prob=False):
+    """Full CascadeMVSNet forward (origin0316 class: identical numerics, no debug prints)."""
+    net = origin.CascadeMVSNet(ndepths=list(ndepths), agg_mode=mode)
+    sd = synthetic_state_dict(net.state_dict(), seed=SEED)
+    net.load_state_dict(sd, strict=True)
+    proj, ins, dv = synth.cameras(B, N, H, W)
+    imgs = synth.images(B, N, H, W, seed=SEED)
+    args = (torch.from_numpy(imgs), {k: torch.from_numpy(v) for k, v in proj.items()}, torch.from_numpy(dv),
+            {k: torch.from_numpy(v) for k, v in ins.items()})
+    calibrate(net, lambda: net(*args))
+    with torch.no_grad():
+        out = net(*args)
+    arrays = {"chk": checksum(imgs, dv, *proj.values())}
+    for s in (1, 2, 3):
+        o = out["stage%d" % s]
+        arrays["s%d_depth" % s] = to_np(o["depth"])
+        arrays["s%d_conf" % s] = to_np(o["photometric_confidence"])
+        arrays["s%d_var" % s] = to_np(o["variance"])
+    arrays.update(bn_stats(net))
+    save("forward_" + tag, **arrays)
+
+
+def fixture_state_dict_keys(active):
+    """Key -> shape of the reference CascadeMVSNet state_dict (fpn and unet arch modes)."""
+    import json
+    out = {}
+    for arch in ("fpn", "unet"):
+        net = active.CascadeMVSNet(arch_mode=arch)
+        out[arch] = {k: list(v.shape) for k, v in net.state_dict().items()}
+    path = os.path.join(HERE, "state_dict_keys.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=0, sort_keys=False)
+    print("wrote", path)
+
+
+def main():
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    mod, active, origin = import_reference()
+    fixture_state_dict_keys(active)
+    fixture_homo_warping(mod)
+    fixture_costreg(mod)
+    fixture_depthnet(active, "adaptive", "cfgA_adaptive")
+    fixture_depthnet(active, "variance", "cfgA_variance")
+    fixture_forward(origin, "160x128_48_32_8", 1, 5, 128, 160, (48, 32, 8))
+    fixture_forward(origin, "160x128_64_32_8_variance", 1, 3, 128, 160, (64, 32, 8), mode="variance")
+    fixture_forward(origin, "cfgB_640x512", 1, 5, 512, 640, (48, 32, 8))
+
+
+if __name__ == "__main__":
+    main()
