@@ -18,9 +18,15 @@ def reference_keys(arch="fpn"):
         return json.load(f)[arch]
 
 
-def model_state(golden_name=None, arch="fpn"):
-    """Synthetic reference-keyed state_dict, with calibrated BN stats from a fixture."""
-    tmpl = {k: tuple(v) for k, v in reference_keys(arch).items()}
+def model_state(golden_name=None, arch="fpn", mode=None):
+    """Synthetic reference-keyed state_dict, with calibrated BN stats from a fixture.
+
+    ``mode='variance'`` drops DepthNet.weight_net.* (the reference builds it only for 'adaptive').
+    """
+    if mode is None:
+        mode = "variance" if golden_name and "variance" in golden_name else "adaptive"
+    tmpl = {k: tuple(v) for k, v in reference_keys(arch).items()
+            if mode == "adaptive" or not k.startswith("DepthNet.weight_net.")}
     sd = synthetic_state_dict(tmpl, SEED)
     if golden_name:
         sd = apply_bn_stats(sd, bn_from_golden(golden(golden_name)))
