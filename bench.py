@@ -80,31 +80,36 @@ class StageTimer:
         return out
 
 
-def warp_roofline(net, imgs, proj, dv, ins, stage, dtype, iters=20):
-    """Time the fused warp+aggregation kernel of one stage alone (HIP events on its stream).
+def warp_roofline(net, imgs, proj, dv, stage, dtype, iters=20):
+    """Time the product-path fused warp+aggregation kernel of one stage alone (HIP events on the
+    stream it is launched on): channel-blocked features and cameras prepared outside the loop.
 
-    Algorithmic bytes per launch: e * (N*C*h*w [features, read once]
-    + C*D*h*w [volume write]) + 4*D*h*w [fp32 hypotheses] + 4*B*(N-1)*12 [cameras].
+    Algorithmic bytes per launch: e * (N*C*h*w [features, read
+    once] + C*D*h*w [volume write]) + 4*D*h*w [fp32 hypotheses] + 4*B*(N-1)*12 [cameras].
     """
+    from damvsnet_amd import _capi
     from damvsnet_amd.depthnet import to_nhwc
-    from damvsnet_amd.engine import hypotheses
+    from damvsnet_amd.engine import hypotheses, proj_prepare, block_channels
     name = "stage%d" % (stage + 1)
     B, N, _, H, W = imgs.shape
     scale = (4, 2, 1)[stage]
     with torch.no_grad():
         feats = net.extract_features(imgs)
         fs = [to_nhwc(f[name], dtype) for f in feats]
+        blocked = fs[0].shape[-1] * fs[0].element_size() > 16
+        fb = block_channels(fs) if blocked else fs
+        layout = _capi.DAMVS_LAYOUT_CBLOCK if blocked else _capi.DAMVS_LAYOUT_NHWC
         hyps = hypotheses(dv, net.ndepths[stage], H, W, scale)
+        rt = proj_prepare(proj[name])
         eng = net.DepthNet.engine(stage, net.cost_regularization[stage], imgs.device)
-        eng.warp_aggregate(fs, proj[name], hyps)
+        eng.warp_aggregate(fb, None, hyps, rt=rt, layout=layout)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(iters):
-            eng.warp_aggregate(fs, proj[name], hyps)
+            eng.warp_aggregate(fb, None, hyps, rt=rt, layout=layout)
         e1.record()
         torch.cuda.synchronize()
-    # eng.warp_aggregate also runs proj_prepare (one tiny launch); measured with it.
     ms = e0.elapsed_time(e1) / iters
     D = net.ndepths[stage]
     h, w, C = fs[0].shape[1], fs[0].shape[2], fs[0].shape[3]
@@ -113,11 +118,25 @@ def warp_roofline(net, imgs, proj, dv, ins, stage, dtype, iters=20):
     return ms, alg
 
 
+def pmc_traffic(config, kernel_substr="warp_aggregate"):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC summary
+    (profiles/<round>/pmc_*.json, produced by tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE,
+    the gfx950 correction of MI355X_MICROARCH.md), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_%s_%s.json" % (kernel_substr, config))))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return {"bytes": int(d["hbm_bytes_per_launch"]), "source": os.path.relpath(files[-1], REPO)}
+
+
 def cpu_baseline(cfg, budget_s=60.0):
     """The oracle (PyTorch CPU restatement of the reference forward, fp32) on this host's cores."""
     from oracle import mvs_oracle as O
     H, W, N, nd, _, _ = CONFIGS[cfg]
-    cores = len(os.sched_getaffinity(0))
+    # the GPU box's CPU share is what OMP_NUM_THREADS says (affinity shows the whole machine)
+    cores = int(os.environ.get("OMP_NUM_THREADS") or min(16, len(os.sched_getaffinity(0))))
     torch.set_num_threads(cores)
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.weights import synthetic_state_dict, apply_bn_stats
@@ -182,17 +201,16 @@ def main():
         barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], device=device)
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    elapsed = float(t.item())
+    from damvsnet_amd.dist import max_over_ranks
+    elapsed = max_over_ranks(elapsed, device=device)
     maps = args.steps * args.batch * world
     phases = {k: round(statistics.mean(v), 3) for k, v in timer.per_phase_ms().items()}
 
     result = None
     if rank == 0:
-        ms, alg = warp_roofline(net, imgs, proj, dv, ins, 1, dtype)
+        ms, alg = warp_roofline(net, imgs, proj, dv, 1, dtype)
         achieved = alg / (ms * 1e-3) / 1e9
+        tr = pmc_traffic(args.config)
         result = {
             "metric": "depth maps/sec (full CascadeMVSNet forward)",
             "value": round(maps / elapsed, 4),
@@ -212,7 +230,8 @@ def main():
             "ms_per_stage": phases,
             "roofline": {"kernel": "warp_aggregate stage2 (fused homography warp + adaptive aggregation)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr["bytes"] if tr else None,
+                         "traffic_source": tr["source"] if tr else None,
                          "ms_per_launch": round(ms, 4), "algorithmic_bytes": int(alg)},
         }
         if world == 1 and not args.no_cpu_baseline:

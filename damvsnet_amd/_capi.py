@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(_HERE, "libdamvs.so")
 
 DAMVS_F32, DAMVS_BF16 = 0, 1
 DAMVS_AGG_ADAPTIVE, DAMVS_AGG_VARIANCE = 0, 1
+DAMVS_LAYOUT_NHWC, DAMVS_LAYOUT_CBLOCK = 0, 1
 ERRORS = {-1: "DAMVS_E_ARG", -2: "DAMVS_E_SHAPE", -3: "DAMVS_E_DTYPE", -4: "DAMVS_E_HIP", -5: "DAMVS_E_NOMEM",
           -6: "DAMVS_E_WORKSPACE"}
 
@@ -52,7 +53,9 @@ SIGNATURES = (
     ("damvs_homo_warp", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                 c_void_p)),
     ("damvs_warp_aggregate", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_void_p),
-                                     c_void_p, c_void_p, c_void_p)),
+                                     c_int, c_void_p, c_void_p, c_void_p)),
+    ("damvs_block_channels", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_void_p),
+                                     ctypes.POINTER(c_void_p))),
     ("damvs_costreg_logits", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t,
                                      c_void_p)),
     ("damvs_regress", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -7,15 +7,14 @@ plus the last stage's keys at top level). Two extra keyword arguments select pre
 
 * ``compute_dtype``  storage of features / cost volumes in the HIP path: torch.float32 (parity
   path, exact-f32 MFMA) or torch.bfloat16 (bf16 MFMA, fp32 accumulate, fp32 regression).
-* ``frontend_dtype`` autocast dtype of the 2D front-end (FeatureNet, GeoFeatureFusion), which runs
-  on PyTorch-ROCm in channels-last memory (SURVEY.md section 8(f) row f1 — next to be moved to HIP).
+* ``frontend_dtype`` dtype of the 2D front-end (FeatureNet, GeoFeatureFusion), which runs on
+  PyTorch-ROCm (MIOpen) as BN-folded channels-last copies (SURVEY.md section 8(f) row f1 — next to be
+  moved to HIP). The originals keep the reference parameters/state_dict.
 
 Per stage: hypotheses (HIP) -> [GeoFeatureFusion, stages 2/3] -> DepthNet (HIP). The reference's
 host syncs (depth_values .cpu(), :191-193; stage-3 debug prints, :275-285) are not reproduced.
 """
 from __future__ import annotations
-
-import contextlib
 
 import torch
 import torch.nn as nn
@@ -24,6 +23,7 @@ import torch.nn.functional as F
 from .depthnet import DepthNet
 from .engine import hypotheses
 from .frontend import FeatureNet, GeoFeatureFusion, ConvBNReLU2d
+from .frontend_fold import fold_frontend
 from .layers import CostRegNet
 
 STAGE_SCALE = {"stage1": 4, "stage2": 2, "stage3": 1}
@@ -69,29 +69,30 @@ class CascadeMVSNet(nn.Module):
         if refine:
             self.refine_network = RefineNet()
         self.DepthNet = DepthNet(agg_mode, self.feature.out_channels, compute_dtype=compute_dtype)
-        self._channels_last = False
+        self._folded_key = None
 
-    def _frontend_ctx(self, device):
-        if self.frontend_dtype is None or self.frontend_dtype == torch.float32:
-            return contextlib.nullcontext()
-        return torch.autocast(device_type="cuda", dtype=self.frontend_dtype)
-
-    def _prepare_frontend(self):
-        if not self._channels_last:
-            self.feature.to(memory_format=torch.channels_last)
-            self.GeoFeatureFusionNet.to(memory_format=torch.channels_last)
-            self._channels_last = True
+    def _frontend(self):
+        """BN-folded, channels-last, ``frontend_dtype`` copies of FeatureNet / GeoFeatureFusion,
+        rebuilt whenever their parameters change (load_state_dict bumps tensor versions)."""
+        fd = self.frontend_dtype or torch.float32
+        mods = (self.feature, self.GeoFeatureFusionNet)
+        ver = tuple(t._version for m in mods for t in list(m.parameters()) + list(m.buffers()))
+        key = (ver, fd, str(next(self.feature.parameters()).device))
+        if getattr(self, "_folded_key", None) != key:
+            self._folded = tuple(fold_frontend(m, fd) for m in mods)
+            self._folded_key = key
+        return self._folded
 
     def _apply(self, fn, *a, **k):
-        self._channels_last = False
+        self._folded_key = None
         return super()._apply(fn, *a, **k)
 
     def extract_features(self, imgs):
         """FeatureNet over all views in one batched call (BN in eval is per-sample)."""
+        feat, _ = self._frontend()
         B, N = imgs.shape[:2]
         x = imgs.reshape(B * N, *imgs.shape[2:]).contiguous(memory_format=torch.channels_last)
-        with self._frontend_ctx(imgs.device):
-            f = self.feature(x)
+        f = feat(x)
         return [{k: v.reshape(B, N, *v.shape[1:])[:, i] for k, v in f.items()} for i in range(N)]
 
     def forward(self, imgs, proj_matrices, depth_values, intrinsics_matrices=None, stage_hook=None):
@@ -101,7 +102,6 @@ class CascadeMVSNet(nn.Module):
         if not imgs.is_cuda:
             raise ValueError("damvsnet_amd is a GPU engine: move the model and inputs to a HIP device")
         hook = stage_hook or (lambda name: None)
-        self._prepare_frontend()
         B, N, _, H, W = imgs.shape
         hook("features")
         features = self.extract_features(imgs)
@@ -113,14 +113,13 @@ class CascadeMVSNet(nn.Module):
             fs = [f[name] for f in features]
             if s >= 1:
                 hook(name + ".geofusion")
-                with self._frontend_ctx(imgs.device):
-                    ref_img = F.interpolate(imgs[:, 0], scale_factor=1.0 / 2 ** (2 - s), mode="bilinear",
-                                            align_corners=False)
-                    dl = F.interpolate(depth.unsqueeze(1), scale_factor=2, mode="bilinear", align_corners=False)
-                    cl = F.interpolate(conf.unsqueeze(1), scale_factor=2, mode="bilinear", align_corners=False)
-                    fs[0] = self.GeoFeatureFusionNet(ref_img.contiguous(memory_format=torch.channels_last), dl, cl,
-                                                     depth_values, s, fs[0],
-                                                     None if intrinsics_matrices is None else intrinsics_matrices[name])
+                _, geo = self._frontend()
+                ref_img = F.interpolate(imgs[:, 0], scale_factor=1.0 / 2 ** (2 - s), mode="bilinear",
+                                        align_corners=False)
+                dl = F.interpolate(depth.unsqueeze(1), scale_factor=2, mode="bilinear", align_corners=False)
+                cl = F.interpolate(conf.unsqueeze(1), scale_factor=2, mode="bilinear", align_corners=False)
+                fs[0] = geo(ref_img.contiguous(memory_format=torch.channels_last), dl, cl, depth_values, s, fs[0],
+                            None if intrinsics_matrices is None else intrinsics_matrices[name])
             hook(name + ".hypotheses")
             hyps = hypotheses(depth_values, self.ndepths[s], H, W, scale, depth, exp_var)
             hook(name + ".depthnet")

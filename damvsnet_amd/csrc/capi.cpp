@@ -173,10 +173,12 @@ Shapes level_shapes(int D, int h, int w) {
 }
 
 struct Workspace {
-  size_t rt, vol, c[7], logits, total;
+  size_t rt, feat, vol, c[7], logits, total;
 };
 
 // c[i] holds conv_i's output for i = 0..6 (conv7/9/11 accumulate in place into c4/c2/c0).
+bool feat_needs_blocking(const damvs_stage* st) { return st->C * (st->dtype == DAMVS_BF16 ? 2 : 4) > 16; }
+
 Workspace plan_ws(const damvs_stage* st, int B, int N, int D, int h, int w) {
   const size_t es = st->dtype == DAMVS_BF16 ? 2 : 4;
   const size_t V = (size_t)B * D * h * w;
@@ -187,6 +189,8 @@ Workspace plan_ws(const damvs_stage* st, int B, int N, int D, int h, int w) {
   size_t o = 0;
   ws.rt = o;
   o += align_up((size_t)B * (N > 1 ? N - 1 : 1) * 12 * 4);
+  ws.feat = o;  // channel-blocked copies of the N feature maps (only when C spans several 16-B chunks)
+  if (feat_needs_blocking(st)) o += (size_t)N * align_up((size_t)B * h * w * st->C * es);
   ws.vol = o;
   o += align_up(V * st->C * es);
   for (int i = 0; i < 7; ++i) {
@@ -238,12 +242,13 @@ ConvArgs conv_args(const damvs_stage* st, int li, int B, const Shapes& S, int li
   return a;
 }
 
-int run_costreg(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, const void* vol, char* ws,
-                const Workspace& W, float* logits, const float* prob_init) {
+// U-Net through conv11 (+conv0 skip): the prob conv input ends in c[0].
+int run_unet(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, const void* vol, char* ws,
+             const Workspace& W) {
   const Shapes S = level_shapes(D, h, w);
   void* c[7];
   for (int i = 0; i < 7; ++i) c[i] = ws + W.c[i];
-  // encoder: (layer, in level, out level, input, output)
+  // (layer, in level, out level, input, output, skip)
   struct Step { int li, lin, lout; const void* in; void* out; const void* res; };
   const Step steps[10] = {
       {0, 0, 0, vol, c[0], nullptr},  {1, 0, 1, c[0], c[1], nullptr}, {2, 1, 1, c[1], c[2], nullptr},
@@ -254,8 +259,6 @@ int run_costreg(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w
     ConvArgs a = conv_args(st, k.li, B, S, k.lin, k.lout, k.in, k.out, k.res);
     DAMVS_TRY(hip_check(launch_conv3d(s, st->dtype, a), "conv3d launch"));
   }
-  DAMVS_TRY(hip_check(launch_prob_conv(s, st->dtype, B, st->base, D, h, w, c[0], st->prob_w, prob_init, logits),
-                      "prob conv launch"));
   return DAMVS_OK;
 }
 
@@ -403,10 +406,32 @@ int damvs_stage_forward(const damvs_stage* st, void* stream, int B, int N, int D
   char* ws = reinterpret_cast<char*>(workspace);
   float* rt = reinterpret_cast<float*>(ws + W.rt);
   DAMVS_TRY(hip_check(launch_proj_prepare(s, B, N, proj, rt), "proj_prepare launch"));
-  WarpArgs wa = warp_args(st, B, N, st->C, D, h, w, feats, rt, hyps, ws + W.vol);
-  DAMVS_TRY(hip_check(launch_warp_aggregate(s, st->dtype, st->mode, wa), "warp_aggregate launch"));
+  const bool blk = feat_needs_blocking(st);
+  const void* fv[kMaxViews];
+  for (int v = 0; v < N; ++v) fv[v] = feats[v];
+  if (blk) {  // repack to [B][C/E][h][w][E]: halves the cache lines each gather instruction touches
+    FeatPtrs src, dst;
+    const size_t per = align_up((size_t)B * h * w * st->C * (st->dtype == DAMVS_BF16 ? 2 : 4));
+    for (int v = 0; v < N; ++v) {
+      src.p[v] = feats[v];
+      dst.p[v] = ws + W.feat + v * per;
+      fv[v] = dst.p[v];
+    }
+    DAMVS_TRY(hip_check(launch_block_channels(s, st->dtype, src, dst, N, B, h * w, st->C), "block_channels launch"));
+  }
+  WarpArgs wa = warp_args(st, B, N, st->C, D, h, w, fv, rt, hyps, ws + W.vol);
+  DAMVS_TRY(hip_check(launch_warp_aggregate(s, st->dtype, st->mode, wa, blk), "warp_aggregate launch"));
+  DAMVS_TRY(run_unet(st, s, B, D, h, w, ws + W.vol, ws, W));
+  const void* feat = ws + W.c[0];
+  if (prob_regress_smem_bytes(st->dtype, st->base, D) <= 160 * 1024) {  // fused: logits stay in LDS
+    DAMVS_TRY(hip_check(launch_prob_regress(s, st->dtype, B, st->base, D, h, w, feat, st->prob_w, prob_init, hyps,
+                                            depth, conf, var, prob),
+                        "prob_regress launch"));
+    return DAMVS_OK;
+  }
   float* logits = reinterpret_cast<float*>(ws + W.logits);
-  DAMVS_TRY(run_costreg(st, s, B, D, h, w, ws + W.vol, ws, W, logits, prob_init));
+  DAMVS_TRY(hip_check(launch_prob_conv(s, st->dtype, B, st->base, D, h, w, feat, st->prob_w, prob_init, logits),
+                      "prob conv launch"));
   DAMVS_TRY(hip_check(launch_regress(s, B, D, h, w, logits, hyps, depth, conf, var, prob), "regress launch"));
   return DAMVS_OK;
 }
@@ -425,17 +450,36 @@ int damvs_homo_warp(void* stream, int dtype, int B, int C, int D, int h, int w, 
   if (B < 1 || D < 1 || h < 2 || w < 2) return fail(DAMVS_E_SHAPE, "bad shape");
   const void* feats[2] = {src, src};
   WarpArgs a = warp_args(nullptr, B, 2, C, D, h, w, feats, rt, hyps, out);
-  return hip_check(launch_warp_aggregate(reinterpret_cast<hipStream_t>(stream), dtype, AGG_WARP_ONLY, a),
+  return hip_check(launch_warp_aggregate(reinterpret_cast<hipStream_t>(stream), dtype, AGG_WARP_ONLY, a, false),
                    "homo_warp launch");
 }
 
 int damvs_warp_aggregate(const damvs_stage* st, void* stream, int B, int N, int D, int h, int w,
-                         const void* const* feats, const float* rt, const float* hyps, void* volume) {
+                         const void* const* feats, int layout, const float* rt, const float* hyps, void* volume) {
   if (!st || !feats || !rt || !hyps || !volume) return fail(DAMVS_E_ARG, "null argument");
   if (B < 1 || N < 2 || N > kMaxViews || D < 1 || h < 2 || w < 2) return fail(DAMVS_E_SHAPE, "bad shape");
+  if (layout != DAMVS_LAYOUT_NHWC && layout != DAMVS_LAYOUT_CBLOCK) return fail(DAMVS_E_ARG, "layout %d", layout);
   WarpArgs a = warp_args(st, B, N, st->C, D, h, w, feats, rt, hyps, volume);
-  return hip_check(launch_warp_aggregate(reinterpret_cast<hipStream_t>(stream), st->dtype, st->mode, a),
+  return hip_check(launch_warp_aggregate(reinterpret_cast<hipStream_t>(stream), st->dtype, st->mode, a,
+                                         layout == DAMVS_LAYOUT_CBLOCK),
                    "warp_aggregate launch");
+}
+
+int damvs_block_channels(void* stream, int dtype, int N, int B, int h, int w, int C, const void* const* src,
+                         void* const* dst) {
+  if (!src || !dst) return fail(DAMVS_E_ARG, "null argument");
+  if (dtype != DAMVS_F32 && dtype != DAMVS_BF16) return fail(DAMVS_E_DTYPE, "dtype %d unsupported", dtype);
+  const int E = dtype == DAMVS_BF16 ? 8 : 4;
+  if (N < 1 || N > kMaxViews || B < 1 || h < 1 || w < 1 || C < E || C % E)
+    return fail(DAMVS_E_SHAPE, "bad shape (C must be a multiple of %d)", E);
+  FeatPtrs s, d;
+  for (int v = 0; v < N; ++v) {
+    if (!src[v] || !dst[v]) return fail(DAMVS_E_ARG, "null feature pointer for map %d", v);
+    s.p[v] = src[v];
+    d.p[v] = dst[v];
+  }
+  return hip_check(launch_block_channels(reinterpret_cast<hipStream_t>(stream), dtype, s, d, N, B, h * w, C),
+                   "block_channels launch");
 }
 
 int damvs_costreg_logits(const damvs_stage* st, void* stream, int B, int D, int h, int w, const void* volume,
@@ -444,8 +488,11 @@ int damvs_costreg_logits(const damvs_stage* st, void* stream, int B, int D, int 
   DAMVS_TRY(check_stage_shape(st, B, 2, D, h, w));
   const Workspace W = plan_ws(st, B, 2, D, h, w);
   if (workspace_bytes < W.total) return fail(DAMVS_E_WORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, W.total);
-  return run_costreg(st, reinterpret_cast<hipStream_t>(stream), B, D, h, w, volume,
-                     reinterpret_cast<char*>(workspace), W, logits, nullptr);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  char* ws = reinterpret_cast<char*>(workspace);
+  DAMVS_TRY(run_unet(st, s, B, D, h, w, volume, ws, W));
+  return hip_check(launch_prob_conv(s, st->dtype, B, st->base, D, h, w, ws + W.c[0], st->prob_w, nullptr, logits),
+                   "prob conv launch");
 }
 
 int damvs_regress(void* stream, int B, int D, int h, int w, const float* logits, const float* hyps,

@@ -65,10 +65,21 @@ hipError_t launch_proj_prepare(hipStream_t s, int B, int N, const float* proj, f
 hipError_t launch_hyp_linear(hipStream_t s, int B, int D, int h, int w, const float* dv, int Dv, float* out);
 hipError_t launch_hyp_refine(hipStream_t s, int B, int D, int H, int W, int scale, const float* pd,
                              const float* pv, int hp, int wp, float* out);
-hipError_t launch_warp_aggregate(hipStream_t s, int store, int mode, const WarpArgs& a);
+struct FeatPtrs {
+  const void* p[kMaxViews];
+};
+// blocked = features in channel-blocked layout [B][C/E][h][w][E] (E = 16 bytes of channels)
+hipError_t launch_warp_aggregate(hipStream_t s, int store, int mode, const WarpArgs& a, bool blocked);
+hipError_t launch_block_channels(hipStream_t s, int store, const FeatPtrs& src, const FeatPtrs& dst, int N, int B,
+                                 int hw, int C);
 hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a);
+bool conv_lds_disabled();  // DAMVS_CONV_NO_LDS=1 selects the global-gather conv kernel (A/B testing)
 hipError_t launch_prob_conv(hipStream_t s, int store, int B, int Cb, int D, int h, int w, const void* feat,
                             const float* wprob, const float* prob_init, float* logits);
+hipError_t launch_prob_regress(hipStream_t s, int store, int B, int Cb, int D, int h, int w, const void* feat,
+                               const float* wprob, const float* prob_init, const float* hyps, float* depth,
+                               float* conf, float* var, float* prob);
+size_t prob_regress_smem_bytes(int store, int Cb, int D);
 hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float* logits, const float* hyps,
                           float* depth, float* conf, float* var, float* prob);
 

@@ -17,6 +17,8 @@
 // ConvTranspose3d(k3, s2, p1, op1) runs as 8 output-parity phases, each a dense sub-convolution
 // with 1..8 taps (sub-pixel decomposition): no MFMA work on the structural zeros a
 // zero-inserted transposed conv would carry.
+#include <cstdlib>
+
 #include "damvs_device.h"
 
 namespace damvs {
@@ -73,11 +75,18 @@ __device__ __forceinline__ void load4<bf16_t>(const bf16_t* p, float* r) {
 constexpr int kGroups = 4;  // 16-voxel column groups per wave (64 output voxels per wave)
 
 template <typename T, int MT>
-__global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a) {
+__global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int nqblk) {
   typedef typename Frag<T>::raw raw;
   constexpr int E = Stor<T>::E;  // input channels per lane per K-chunk
   constexpr int KC = 4 * E;      // K per chunk (4 lane groups)
-  const ConvPhase& ph = a.ph[blockIdx.y];
+  // Logical block = (q-block, phase) with the phase fastest, dealt XCD-contiguously: the 8 output
+  // parities of one deconv q-range run together on one XCD, so their interleaved half-line writes
+  // (and the skip tensor's reads) merge in that L2.
+  const int nblk = nqblk * a.nphase;
+  const int bid = blockIdx.x, q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int qblk = L / a.nphase;
+  const ConvPhase& ph = a.ph[L - qblk * a.nphase];
   __shared__ int s_tap[32];
   if (threadIdx.x < 27) {
     const signed char* t = ph.tap[threadIdx.x];
@@ -88,7 +97,7 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
   const long long Qtot = (long long)a.B * a.Dq * a.Hq * a.Wq;
-  const long long base = ((long long)blockIdx.x * 4 + wave) * (kGroups * 16);
+  const long long base = ((long long)qblk * 4 + wave) * (kGroups * 16);
   if (base >= Qtot) return;
 
   int vb[kGroups], vz[kGroups], vy[kGroups], vx[kGroups];
@@ -169,15 +178,152 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// LDS-staged variant for stride-1 k3 convs (conv0/2/4/6): a block owns a 4 x 8 x 16 output tile
+// (512 voxels, 8 sixteen-voxel groups per wave). Its (4+2) x (8+2) x (16+2) x Cin halo is read from
+// HBM/L2 once (16-byte loads, zero padding) into LDS; every K-chunk's B fragment is then a
+// conflict-light ds_read_b128 instead of an L1 gather, cutting the L1/TA traffic that bounds the
+// global-gather kernel by ~27x (each input voxel feeds 27 taps). Blocks are dealt so that
+// consecutive tiles along x land on one XCD (bijective remap): neighbours' halos hit that L2.
+constexpr int LTD = 4, LTH = 8, LTW = 16;
+constexpr int LHD = LTD + 2, LHH = LTH + 2, LHW = LTW + 2;
+constexpr int kLdsGroups = 8;  // per wave: 4 waves x 8 groups x 16 voxels = 512 = LTD*LTH*LTW
+
+template <typename T, int CIN>
+constexpr size_t lds_tile_bytes() { return (size_t)LHD * LHH * LHW * CIN * sizeof(T); }
+
+template <typename T, int CIN, int MT>
+__global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int tiles_x, int tiles_y, int tiles_z,
+                                                         int ntiles) {
+  typedef typename Frag<T>::raw raw;
+  constexpr int E = Stor<T>::E;
+  constexpr int KC = 4 * E;
+  constexpr int CH = CIN / E;                              // 16-byte chunks per voxel
+  constexpr int KCHUNKS = (27 * CIN + KC - 1) / KC;
+  constexpr int TILE_CHUNKS = LHD * LHH * LHW * CH;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  raw* tile = reinterpret_cast<raw*>(smem);
+
+  // XCD-aware bijective remap: blocks b and b+8 share an XCD; give each XCD a contiguous tile range.
+  const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  int tt = t;
+  const int tx = tt % tiles_x; tt /= tiles_x;
+  const int ty = tt % tiles_y; tt /= tiles_y;
+  const int tz = tt % tiles_z;
+  const int b = tt / tiles_z;
+  const int z0 = tz * LTD, y0 = ty * LTH, x0 = tx * LTW;
+
+  const T* __restrict__ in = reinterpret_cast<const T*>(a.in) + (size_t)b * a.Di * a.Hi * a.Wi * CIN;
+  for (int c = threadIdx.x; c < TILE_CHUNKS; c += 256) {
+    const int vox = c / CH, part = c - vox * CH;
+    const int hx = vox % LHW, hy = (vox / LHW) % LHH, hz = vox / (LHW * LHH);
+    const int iz = z0 - 1 + hz, iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+    const bool ok = (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+    const size_t off = ok ? (((size_t)iz * a.Hi + iy) * a.Wi + ix) * CIN + part * E : 0;
+    const raw v = *reinterpret_cast<const raw*>(in + off);
+    tile[c] = ok ? v : Frag<T>::zero();
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  f32x4_t acc[kLdsGroups][MT];
+#pragma unroll
+  for (int j = 0; j < kLdsGroups; ++j)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + lane;
+#pragma unroll 2
+  for (int s = 0; s < KCHUNKS; ++s) {
+    const int k0 = s * KC + g * E;
+    const int tap = k0 / CIN, ci = k0 - tap * CIN;
+    const bool tv = tap < 27;
+    const int dz = tap / 9, dy = (tap / 3) % 3, dx = tap % 3;
+    raw wf[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * MT + m) * 64];
+    // group j of this wave = output row (z, y) = (j2 / LTH, j2 % LTH), voxel x = n
+    const int base = ((dz * LHH + dy) * LHW + n + dx) * CH + ci / E;
+#pragma unroll
+    for (int j = 0; j < kLdsGroups; ++j) {
+      const int j2 = wave * kLdsGroups + j;
+      const int zz = j2 / LTH, yy = j2 % LTH;
+      raw xf = tile[base + (zz * LHH + yy) * LHW * CH];
+      if (!tv) xf = Frag<T>::zero();
+#pragma unroll
+      for (int m = 0; m < MT; ++m) Frag<T>::mma(wf[m], xf, acc[j][m]);
+    }
+  }
+
+  T* __restrict__ out = reinterpret_cast<T*>(a.out);
+  const T* __restrict__ res = reinterpret_cast<const T*>(a.resid);
+#pragma unroll
+  for (int j = 0; j < kLdsGroups; ++j) {
+    const int j2 = wave * kLdsGroups + j;
+    const int oz = z0 + j2 / LTH, oy = y0 + j2 % LTH, ox = x0 + n;
+    if (oz >= a.Do || oy >= a.Ho || ox >= a.Wo) continue;
+    const size_t ob = ((((size_t)b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * a.Cout;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int co = m * 16 + g * 4;
+      if (co >= a.Cout) continue;
+      float r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        r[i] = acc[j][m][i] + a.bias[co + i];
+        if (a.relu) r[i] = fmaxf(r[i], 0.f);
+      }
+      if (res) {
+        float q[4];
+        load4<T>(res + ob + co, q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] += q[i];
+      }
+      store4<T>(out + ob + co, r);
+    }
+  }
+}
+
+template <typename T, int CIN, int MT>
+hipError_t launch_lds_t(hipStream_t s, const ConvArgs& a) {
+  const size_t smem = lds_tile_bytes<T, CIN>();
+  auto k = conv3d_lds_kernel<T, CIN, MT>;
+  if (smem > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)smem);
+    if (e != hipSuccess) return e;
+  }
+  const int tx = (a.Wo + LTW - 1) / LTW, ty = (a.Ho + LTH - 1) / LTH, tz = (a.Do + LTD - 1) / LTD;
+  const long long nt = (long long)tx * ty * tz * a.B;
+  hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, tz, (int)nt);
+  return hipGetLastError();
+}
+
+// Returns hipErrorNotSupported when no LDS variant fits this layer (caller falls back).
+template <typename T>
+hipError_t launch_lds(hipStream_t s, const ConvArgs& a) {
+  if (a.nphase != 1 || a.in_stride != 1 || a.out_stride != 1 || a.ph[0].ntaps != 27) return hipErrorNotSupported;
+  const int MT = a.MT;
+  if (a.Cin == 8 && MT == 1) return launch_lds_t<T, 8, 1>(s, a);
+  if (a.Cin == 16 && MT == 1) return launch_lds_t<T, 16, 1>(s, a);
+  if (a.Cin == 32 && MT == 1) return launch_lds_t<T, 32, 1>(s, a);
+  if (a.Cin == 32 && MT == 2) return launch_lds_t<T, 32, 2>(s, a);
+  if (a.Cin == 64 && MT == 4 && lds_tile_bytes<T, 64>() <= 160 * 1024) return launch_lds_t<T, 64, 4>(s, a);
+  return hipErrorNotSupported;
+}
+
 template <typename T>
 hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
   long long Qtot = (long long)a.B * a.Dq * a.Hq * a.Wq;
   long long per_block = 4LL * kGroups * 16;
-  dim3 grid((unsigned)((Qtot + per_block - 1) / per_block), a.nphase);
+  const int nq = (int)((Qtot + per_block - 1) / per_block);
+  dim3 grid((unsigned)(nq * a.nphase));
   switch (a.MT) {
-    case 1: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1>), grid, dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 2>), grid, dim3(256), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 4>), grid, dim3(256), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1>), grid, dim3(256), 0, s, a, nq); break;
+    case 2: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 2>), grid, dim3(256), 0, s, a, nq); break;
+    case 4: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 4>), grid, dim3(256), 0, s, a, nq); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -186,7 +332,19 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
 }  // namespace
 
 hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a) {
+  if (!conv_lds_disabled()) {
+    hipError_t e = store == ST_BF16 ? launch_lds<bf16_t>(s, a) : launch_lds<float>(s, a);
+    if (e != hipErrorNotSupported) return e;
+  }
   return store == ST_BF16 ? launch_t<bf16_t>(s, a) : launch_t<float>(s, a);
+}
+
+bool conv_lds_disabled() {
+  static const bool off = [] {
+    const char* v = getenv("DAMVS_CONV_NO_LDS");
+    return v && v[0] == '1';
+  }();
+  return off;
 }
 
 }  // namespace damvs

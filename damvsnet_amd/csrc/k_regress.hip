@@ -9,6 +9,8 @@
 //              confidence = sum of p over [i*-1, i*+2] at i* = clamp(long(sum p*i), 0, D-1)
 //              (:113-118, the 4*avg_pool3d of the padded volume), exp-variance
 //              3*sqrt(sum (d - depth)^2 p) (:121-124); optional prob volume write.
+#include <type_traits>
+
 #include "damvs_device.h"
 
 namespace damvs {
@@ -20,9 +22,7 @@ __global__ __launch_bounds__(256) void prob_conv_kernel(int B, int D, int h, int
                                                         const float* __restrict__ wprob,
                                                         const float* __restrict__ prob_init,
                                                         float* __restrict__ logits) {
-  __shared__ float sw[27 * CB];  // [kd][kh][kw][c]
-  for (int i = threadIdx.x; i < 27 * CB; i += blockDim.x) sw[i] = wprob[i];
-  __syncthreads();
+  const float* sw = wprob;  // [kd][kh][kw][c], wave-uniform -> scalar loads
   const int hw = h * w;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
@@ -41,9 +41,10 @@ __global__ __launch_bounds__(256) void prob_conv_kernel(int B, int D, int h, int
         if (xx < 0 || xx >= w) continue;
         float v[CB];
         load_vec<T, CB>(feat + ((((size_t)b * D + pl) * h + yy) * w + xx) * CB, v);
-        const float* w0 = sw + ((0 * 3 + ky) * 3 + kx) * CB;
-        const float* w1 = sw + ((1 * 3 + ky) * 3 + kx) * CB;
-        const float* w2 = sw + ((2 * 3 + ky) * 3 + kx) * CB;
+        // wave-uniform weights through the scalar cache (SGPR operands of v_fmac)
+        const float* w0 = wprob + ((0 * 3 + ky) * 3 + kx) * CB;
+        const float* w1 = wprob + ((1 * 3 + ky) * 3 + kx) * CB;
+        const float* w2 = wprob + ((2 * 3 + ky) * 3 + kx) * CB;
 #pragma unroll
         for (int c = 0; c < CB; ++c) {
           c0 += w0[c] * v[c];
@@ -100,6 +101,167 @@ __global__ __launch_bounds__(256) void regress_kernel(int B, int D, int hw, cons
   var[(size_t)b * hw + p] = 3.f * sqrtf(vs);
 }
 
+// Fused prob conv + regression. One 256-thread block owns an 8 x 32 pixel tile for all D planes:
+// each input plane's (8+2) x (32+2) x Cb halo tile is staged once in LDS (double-buffered, one
+// barrier per plane, next plane's global loads issued before this plane's FMAs), every thread slides
+// its 3x3x3 window over the planes keeping the two open logits in registers, completed logits go to
+// an LDS column [D][256] and the regression runs from there. Logits never reach HBM.
+constexpr int kTY = 8, kTX = 32, kHY = kTY + 2, kHX = kTX + 2;
+
+template <typename T, int CB>
+__global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, int w, const T* __restrict__ feat,
+                                                           const float* __restrict__ wprob,
+                                                           const float* __restrict__ prob_init,
+                                                           const float* __restrict__ hyps, float* __restrict__ depth,
+                                                           float* __restrict__ conf, float* __restrict__ var,
+                                                           float* __restrict__ prob) {
+  constexpr int E = Stor<T>::E;
+  constexpr int CH = CB / E;                 // 16-byte chunks per voxel
+  constexpr int TILE_CHUNKS = kHY * kHX * CH;
+  constexpr int PER_T = (TILE_CHUNKS + 255) / 256;
+  typedef typename std::conditional<sizeof(T) == 4, float4, uint4>::type raw;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  raw* tile = reinterpret_cast<raw*>(smem);                      // 2 x TILE_CHUNKS (double buffer)
+  float* lg = reinterpret_cast<float*>(tile + 2 * TILE_CHUNKS);  // [D][256] logits, column per thread
+
+  const int tid = threadIdx.x;
+  const int ty = tid / kTX, tx = tid % kTX;
+  const int y0 = blockIdx.y * kTY, x0 = blockIdx.x * kTX;
+  const int b = blockIdx.z;
+  const T* fb = feat + (size_t)b * D * h * w * CB;
+  raw regs[PER_T];
+  auto gload = [&](int pl) {
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k) {
+      const int c = tid + k * 256;
+      raw v;
+      if constexpr (sizeof(T) == 4) v = make_float4(0.f, 0.f, 0.f, 0.f); else v = make_uint4(0u, 0u, 0u, 0u);
+      if (c < TILE_CHUNKS) {
+        const int vox = c / CH, part = c % CH;
+        const int yy = y0 - 1 + vox / kHX, xx = x0 - 1 + vox % kHX;
+        if (yy >= 0 && yy < h && xx >= 0 && xx < w)
+          v = *reinterpret_cast<const raw*>(fb + (((size_t)pl * h + yy) * w + xx) * CB + part * E);
+      }
+      regs[k] = v;
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k) {
+      const int c = tid + k * 256;
+      if (c < TILE_CHUNKS) tile[buf * TILE_CHUNKS + c] = regs[k];
+    }
+  };
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  float am1 = 0.f, a0 = 0.f;
+  for (int pl = 0; pl < D; ++pl) {
+    if (pl + 1 < D) gload(pl + 1);
+    const raw* tb = tile + (pl & 1) * TILE_CHUNKS;
+    float c0 = 0.f, c1 = 0.f, c2 = 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        float v[CB];
+        const raw* src = tb + ((ty + ky) * kHX + tx + kx) * CH;
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+          raw r = src[q];
+          if constexpr (sizeof(T) == 4) {
+            v[q * 4 + 0] = r.x; v[q * 4 + 1] = r.y; v[q * 4 + 2] = r.z; v[q * 4 + 3] = r.w;
+          } else {
+            const uint32_t u[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              v[q * 8 + 2 * i] = __uint_as_float(u[i] << 16);
+              v[q * 8 + 2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+            }
+          }
+        }
+        // wave-uniform weights through the scalar cache (SGPR operands of v_fmac)
+        const float* w0 = wprob + ((0 * 3 + ky) * 3 + kx) * CB;
+        const float* w1 = wprob + ((1 * 3 + ky) * 3 + kx) * CB;
+        const float* w2 = wprob + ((2 * 3 + ky) * 3 + kx) * CB;
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+          c0 += w0[c] * v[c];
+          c1 += w1[c] * v[c];
+          c2 += w2[c] * v[c];
+        }
+      }
+    if (pl >= 1) lg[(pl - 1) * 256 + tid] = am1 + c2;
+    am1 = a0 + c1;
+    a0 = c0;
+    if (pl + 1 < D) lstore((pl + 1) & 1);
+    __syncthreads();
+  }
+  lg[(D - 1) * 256 + tid] = am1;
+
+  const int y = y0 + ty, x = x0 + tx;
+  if (y >= h || x >= w) return;
+  const size_t hw = (size_t)h * w, pix = (size_t)y * w + x;
+  const float* hy = hyps + (size_t)b * D * hw + pix;
+  const float* pin = prob_init ? prob_init + (size_t)b * D * hw + pix : nullptr;
+  float* lcol = lg + tid;
+  if (pin)
+    for (int d = 0; d < D; ++d) lcol[d * 256] += pin[(size_t)d * hw];
+  float mx = -INFINITY;
+  for (int d = 0; d < D; ++d) mx = fmaxf(mx, lcol[d * 256]);
+  float sum = 0.f;
+  for (int d = 0; d < D; ++d) {
+    const float e = expf(lcol[d * 256] - mx);
+    lcol[d * 256] = e;
+    sum += e;
+  }
+  float dep = 0.f, idx = 0.f;
+  for (int d = 0; d < D; ++d) {
+    const float pr = lcol[d * 256] / sum;
+    lcol[d * 256] = pr;
+    dep += pr * hy[(size_t)d * hw];
+    idx += pr * (float)d;
+  }
+  int ii = (int)idx;
+  ii = ii < 0 ? 0 : (ii > D - 1 ? D - 1 : ii);
+  float c = 0.f, vs = 0.f;
+  float* po = prob ? prob + (size_t)b * D * hw + pix : nullptr;
+  for (int d = 0; d < D; ++d) {
+    const float pr = lcol[d * 256];
+    const float df = hy[(size_t)d * hw] - dep;
+    vs += df * df * pr;
+    if (d >= ii - 1 && d <= ii + 2) c += pr;
+    if (po) po[(size_t)d * hw] = pr;
+  }
+  depth[(size_t)b * hw + pix] = dep;
+  conf[(size_t)b * hw + pix] = c;
+  var[(size_t)b * hw + pix] = 3.f * sqrtf(vs);
+}
+
+template <typename T, int CB>
+size_t prob_regress_smem(int D) {
+  constexpr int CH = CB / Stor<T>::E;
+  return 2 * (size_t)kHY * kHX * CH * 16 + (size_t)D * 256 * 4;
+}
+
+template <typename T, int CB>
+hipError_t launch_pr_t(hipStream_t s, int B, int D, int h, int w, const void* feat, const float* wprob,
+                       const float* prob_init, const float* hyps, float* depth, float* conf, float* var, float* prob) {
+  const size_t smem = prob_regress_smem<T, CB>(D);
+  if (smem > 160 * 1024) return hipErrorInvalidValue;
+  auto k = prob_regress_kernel<T, CB>;
+  if (smem > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)smem);
+    if (e != hipSuccess) return e;
+  }
+  dim3 grid((w + kTX - 1) / kTX, (h + kTY - 1) / kTY, B);
+  hipLaunchKernelGGL(k, grid, dim3(256), smem, s, B, D, h, w, reinterpret_cast<const T*>(feat), wprob, prob_init, hyps,
+                     depth, conf, var, prob);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_pc(hipStream_t s, int B, int Cb, int D, int h, int w, const void* feat, const float* wprob,
                      const float* prob_init, float* logits) {
@@ -119,6 +281,23 @@ hipError_t launch_prob_conv(hipStream_t s, int store, int B, int Cb, int D, int 
                             const float* wprob, const float* prob_init, float* logits) {
   return store == ST_BF16 ? launch_pc<bf16_t>(s, B, Cb, D, h, w, feat, wprob, prob_init, logits)
                           : launch_pc<float>(s, B, Cb, D, h, w, feat, wprob, prob_init, logits);
+}
+
+hipError_t launch_prob_regress(hipStream_t s, int store, int B, int Cb, int D, int h, int w, const void* feat,
+                               const float* wprob, const float* prob_init, const float* hyps, float* depth,
+                               float* conf, float* var, float* prob) {
+  if (Cb == 8)
+    return store == ST_BF16 ? launch_pr_t<bf16_t, 8>(s, B, D, h, w, feat, wprob, prob_init, hyps, depth, conf, var, prob)
+                            : launch_pr_t<float, 8>(s, B, D, h, w, feat, wprob, prob_init, hyps, depth, conf, var, prob);
+  if (Cb == 16)
+    return store == ST_BF16 ? launch_pr_t<bf16_t, 16>(s, B, D, h, w, feat, wprob, prob_init, hyps, depth, conf, var, prob)
+                            : launch_pr_t<float, 16>(s, B, D, h, w, feat, wprob, prob_init, hyps, depth, conf, var, prob);
+  return hipErrorInvalidValue;
+}
+
+size_t prob_regress_smem_bytes(int store, int Cb, int D) {
+  if (Cb == 8) return store == ST_BF16 ? prob_regress_smem<bf16_t, 8>(D) : prob_regress_smem<float, 8>(D);
+  return store == ST_BF16 ? prob_regress_smem<bf16_t, 16>(D) : prob_regress_smem<float, 16>(D);
 }
 
 hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float* logits, const float* hyps,

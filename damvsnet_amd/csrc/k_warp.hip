@@ -19,127 +19,196 @@ namespace damvs {
 
 namespace {
 
-template <typename T, int C>
+// Bilinear sample of C channels at (ix, iy), zero padding. Branch-free: invalid taps load from a
+// clamped in-bounds address with weight 0 (all four loads issue back to back). BLK selects the
+// channel-blocked layout [C/E][h][w][E] (one contiguous 16-byte plane per chunk: a wave's gather
+// touches half the cache lines of plain NHWC for C > E).
+template <typename T, int C, bool BLK>
 __device__ __forceinline__ void sample_bilinear(const T* __restrict__ src, int h, int w, float ix, float iy, float* s) {
-#pragma unroll
-  for (int c = 0; c < C; ++c) s[c] = 0.f;
-  // Non-finite or far-away coordinates sample nothing (all four taps out of bounds).
-  if (!(ix > -2.f && ix < (float)w + 1.f && iy > -2.f && iy < (float)h + 1.f)) return;
-  const float x0f = floorf(ix), y0f = floorf(iy);
+  constexpr int E = Stor<T>::E;
+  const bool inside = ix > -2.f && ix < (float)w + 1.f && iy > -2.f && iy < (float)h + 1.f;  // false for NaN
+  const float cx = inside ? ix : -4.f, cy = inside ? iy : -4.f;
+  const float x0f = floorf(cx), y0f = floorf(cy);
   const int x0 = (int)x0f, y0 = (int)y0f;
-  const float wx1 = ix - x0f, wx0 = (x0f + 1.f) - ix;
-  const float wy1 = iy - y0f, wy0 = (y0f + 1.f) - iy;
-  const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};  // nw, ne, sw, se
+  const float wx1 = cx - x0f, wx0 = (x0f + 1.f) - cx;
+  const float wy1 = cy - y0f, wy0 = (y0f + 1.f) - cy;
+  float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};  // nw, ne, sw, se
+  int idx[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int xx = x0 + (k & 1), yy = y0 + (k >> 1);
-    if (xx < 0 || xx >= w || yy < 0 || yy >= h) continue;
-    float v[C];
-    load_vec<T, C>(src + ((size_t)yy * w + xx) * C, v);
+    const bool ok = xx >= 0 && xx < w && yy >= 0 && yy < h;
+    idx[k] = ok ? yy * w + xx : 0;
+    wt[k] = ok ? wt[k] : 0.f;
+  }
+  const size_t plane = (size_t)h * w * E;
 #pragma unroll
-    for (int c = 0; c < C; ++c) s[c] += v[c] * wt[k];
+  for (int q = 0; q < C / E; ++q) {
+    float v[4][E];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      Stor<T>::load16(BLK ? src + q * plane + (size_t)idx[k] * E : src + (size_t)idx[k] * C + q * E, v[k]);
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      s[q * E + e] = ((v[0][e] * wt[0] + v[1][e] * wt[1]) + v[2][e] * wt[2]) + v[3][e] * wt[3];
   }
 }
 
-template <typename T, int C, int MODE>
-__global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a) {
+// Work decomposition (locality): a block owns 256 consecutive pixels of one image row band and a
+// chunk of `dchunk` consecutive depth planes, and each thread walks its pixel through those planes.
+// Consecutive hypotheses of one pixel sample along one epipolar segment, so a block's gathers stay
+// inside a narrow band of each source image; blocks are dealt so that each XCD gets a contiguous
+// range of (pixel-chunk, depth-chunk) work and its L2 holds that band (the naive (pixels, D) grid
+// spreads every depth slice over all 8 XCDs and serves the gathers from the Infinity Cache).
+template <typename T, int C, int MODE, bool BLK>
+__global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, int npix_blocks, int dchunk,
+                                                             int ndchunks) {
   const int hw = a.h * a.w;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  const int d = blockIdx.y, b = blockIdx.z;
+  const int nblk = npix_blocks * ndchunks * a.B;
+  const int bid = blockIdx.x, q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;  // bijective XCD remap
+  const int dc = L % ndchunks; L /= ndchunks;
+  const int pb = L % npix_blocks;
+  const int b = L / npix_blocks;
+  const int p = pb * 256 + threadIdx.x;
   if (p >= hw) return;
   const int y = p / a.w, x = p - y * a.w;
-  const size_t vox = ((size_t)b * a.D + d) * hw + p;
-  const float hyp = a.hyps[vox];
   const float fx = (float)x, fy = (float)y;
   const float nx = (float)(a.w - 1) * 0.5f, ny = (float)(a.h - 1) * 0.5f;
 
-  float ref[C], acc[C], sq[C];
+  float ref[C];
   if (MODE != AGG_WARP_ONLY) {
-    load_vec<T, C>(reinterpret_cast<const T*>(a.feats[0]) + ((size_t)b * hw + p) * C, ref);
-  }
+    const T* f0 = reinterpret_cast<const T*>(a.feats[0]) + (size_t)b * hw * C;
+    constexpr int E = Stor<T>::E;
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    acc[c] = (MODE == AGG_VARIANCE) ? ref[c] : 0.f;
-    sq[c] = (MODE == AGG_VARIANCE) ? ref[c] * ref[c] : 0.f;
-  }
-
-  for (int v = 1; v < a.N; ++v) {
-    const float* m = a.rt + ((size_t)b * (a.N - 1) + (v - 1)) * 12;
-    const float rx = m[0] * fx + m[1] * fy + m[2];
-    const float ry = m[3] * fx + m[4] * fy + m[5];
-    const float rz = m[6] * fx + m[7] * fy + m[8];
-    const float qx = rx * hyp + m[9], qy = ry * hyp + m[10], qz = rz * hyp + m[11];
-    const float gx = (qx / qz) / nx - 1.f, gy = (qy / qz) / ny - 1.f;
-    const float ix = ((gx + 1.f) * (float)a.w - 1.f) * 0.5f;
-    const float iy = ((gy + 1.f) * (float)a.h - 1.f) * 0.5f;
-    float s[C];
-    sample_bilinear<T, C>(reinterpret_cast<const T*>(a.feats[v]) + (size_t)b * hw * C, a.h, a.w, ix, iy, s);
-    if (MODE == AGG_WARP_ONLY) {
-#pragma unroll
-      for (int c = 0; c < C; ++c) acc[c] = s[c];
-    } else if (MODE == AGG_VARIANCE) {
-#pragma unroll
-      for (int c = 0; c < C; ++c) { acc[c] += s[c]; sq[c] += s[c] * s[c]; }
-    } else {
-      float dot = 0.f;
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const float df = ref[c] - s[c];
-        s[c] = df * df;
-        dot += a.k1[c] * s[c];
-      }
-      const float a1 = fmaxf(dot * a.s1 + a.t1, 0.f);
-      const float wt = fmaxf(a1 * a.s2 + a.t2, 0.f) + 1.f;
-#pragma unroll
-      for (int c = 0; c < C; ++c) acc[c] += wt * s[c];
-    }
+    for (int q = 0; q < C / E; ++q)
+      Stor<T>::load16(BLK ? f0 + ((size_t)q * hw + p) * E : f0 + (size_t)p * C + q * E, ref + q * E);
   }
 
-  float o[C];
-  if (MODE == AGG_VARIANCE) {
-    const float n = (float)a.N;
+  const int d0 = dc * dchunk, d1 = min(a.D, d0 + dchunk);
+  for (int d = d0; d < d1; ++d) {
+    const size_t vox = ((size_t)b * a.D + d) * hw + p;
+    const float hyp = a.hyps[vox];
+    float acc[C], sq[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      const float mean = acc[c] / n;
-      o[c] = sq[c] / n - mean * mean;
+      acc[c] = (MODE == AGG_VARIANCE) ? ref[c] : 0.f;
+      sq[c] = (MODE == AGG_VARIANCE) ? ref[c] * ref[c] : 0.f;
     }
-  } else if (MODE == AGG_ADAPTIVE) {
-    const float n1 = (float)(a.N - 1);
+    for (int v = 1; v < a.N; ++v) {
+      const float* m = a.rt + ((size_t)b * (a.N - 1) + (v - 1)) * 12;
+      const float rx = m[0] * fx + m[1] * fy + m[2];
+      const float ry = m[3] * fx + m[4] * fy + m[5];
+      const float rz = m[6] * fx + m[7] * fy + m[8];
+      const float qx = rx * hyp + m[9], qy = ry * hyp + m[10], qz = rz * hyp + m[11];
+      const float gx = (qx / qz) / nx - 1.f, gy = (qy / qz) / ny - 1.f;
+      const float ix = ((gx + 1.f) * (float)a.w - 1.f) * 0.5f;
+      const float iy = ((gy + 1.f) * (float)a.h - 1.f) * 0.5f;
+      float s[C];
+      sample_bilinear<T, C, BLK>(reinterpret_cast<const T*>(a.feats[v]) + (size_t)b * hw * C, a.h, a.w, ix, iy, s);
+      if (MODE == AGG_WARP_ONLY) {
 #pragma unroll
-    for (int c = 0; c < C; ++c) o[c] = acc[c] / n1;
-  } else {
+        for (int c = 0; c < C; ++c) acc[c] = s[c];
+      } else if (MODE == AGG_VARIANCE) {
 #pragma unroll
-    for (int c = 0; c < C; ++c) o[c] = acc[c];
+        for (int c = 0; c < C; ++c) { acc[c] += s[c]; sq[c] += s[c] * s[c]; }
+      } else {
+        float dot = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const float df = ref[c] - s[c];
+          s[c] = df * df;
+          dot += a.k1[c] * s[c];
+        }
+        const float a1 = fmaxf(dot * a.s1 + a.t1, 0.f);
+        const float wt = fmaxf(a1 * a.s2 + a.t2, 0.f) + 1.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] += wt * s[c];
+      }
+    }
+    float o[C];
+    if (MODE == AGG_VARIANCE) {
+      const float n = (float)a.N;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float mean = acc[c] / n;
+        o[c] = sq[c] / n - mean * mean;
+      }
+    } else if (MODE == AGG_ADAPTIVE) {
+      const float n1 = (float)(a.N - 1);
+#pragma unroll
+      for (int c = 0; c < C; ++c) o[c] = acc[c] / n1;
+    } else {
+#pragma unroll
+      for (int c = 0; c < C; ++c) o[c] = acc[c];
+    }
+    store_vec<T, C>(reinterpret_cast<T*>(a.out) + vox * C, o);
   }
-  store_vec<T, C>(reinterpret_cast<T*>(a.out) + vox * C, o);
 }
 
-template <typename T, int MODE>
+template <typename T, int MODE, bool BLK>
 hipError_t launch_c(hipStream_t s, const WarpArgs& a) {
-  dim3 grid((a.h * a.w + 255) / 256, a.D, a.B);
+  const int npb = (a.h * a.w + 255) / 256;
+  // depth chunk: as long as possible (locality) while keeping >= ~4 blocks per CU in flight
+  int dchunk = a.D;
+  while (dchunk > 2 && (long long)npb * a.B * ((a.D + dchunk - 1) / dchunk) < 2048) dchunk = (dchunk + 1) / 2;
+  const int ndc = (a.D + dchunk - 1) / dchunk;
+  dim3 grid((unsigned)(npb * ndc * a.B));
   switch (a.C) {
-    case 8: hipLaunchKernelGGL((warp_aggregate_kernel<T, 8, MODE>), grid, dim3(256), 0, s, a); break;
-    case 16: hipLaunchKernelGGL((warp_aggregate_kernel<T, 16, MODE>), grid, dim3(256), 0, s, a); break;
-    case 32: hipLaunchKernelGGL((warp_aggregate_kernel<T, 32, MODE>), grid, dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((warp_aggregate_kernel<T, 8, MODE, BLK>), grid, dim3(256), 0, s, a, npb, dchunk, ndc); break;
+    case 16: hipLaunchKernelGGL((warp_aggregate_kernel<T, 16, MODE, BLK>), grid, dim3(256), 0, s, a, npb, dchunk, ndc); break;
+    case 32: hipLaunchKernelGGL((warp_aggregate_kernel<T, 32, MODE, BLK>), grid, dim3(256), 0, s, a, npb, dchunk, ndc); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-template <typename T>
+template <typename T, bool BLK>
 hipError_t launch_t(hipStream_t s, int mode, const WarpArgs& a) {
   switch (mode) {
-    case AGG_ADAPTIVE: return launch_c<T, AGG_ADAPTIVE>(s, a);
-    case AGG_VARIANCE: return launch_c<T, AGG_VARIANCE>(s, a);
-    case AGG_WARP_ONLY: return launch_c<T, AGG_WARP_ONLY>(s, a);
+    case AGG_ADAPTIVE: return launch_c<T, AGG_ADAPTIVE, BLK>(s, a);
+    case AGG_VARIANCE: return launch_c<T, AGG_VARIANCE, BLK>(s, a);
+    case AGG_WARP_ONLY: return launch_c<T, AGG_WARP_ONLY, BLK>(s, a);
   }
   return hipErrorInvalidValue;
 }
 
+// [N views][B][h][w][C] -> [B][C/E][h][w][E] per view; one thread per (view, b, pixel, chunk).
+template <typename T>
+__global__ __launch_bounds__(256) void block_channels_kernel(const FeatPtrs src, FeatPtrs dst, int B, int hw, int C,
+                                                             int N) {
+  constexpr int E = Stor<T>::E;
+  const int CH = C / E;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long per_view = (long long)B * hw * CH;
+  if (i >= per_view * N) return;
+  const int v = (int)(i / per_view);
+  long long r = i - v * per_view;
+  const int p = (int)(r % hw);
+  r /= hw;
+  const int q = (int)(r % CH);
+  const int b = (int)(r / CH);
+  const T* sp = reinterpret_cast<const T*>(src.p[v]) + ((size_t)b * hw + p) * C + q * E;
+  T* dp = const_cast<T*>(reinterpret_cast<const T*>(dst.p[v])) + (((size_t)b * CH + q) * hw + p) * E;
+  *reinterpret_cast<uint4*>(dp) = *reinterpret_cast<const uint4*>(sp);
+}
+
 }  // namespace
 
-hipError_t launch_warp_aggregate(hipStream_t s, int store, int mode, const WarpArgs& a) {
-  return store == ST_BF16 ? launch_t<bf16_t>(s, mode, a) : launch_t<float>(s, mode, a);
+hipError_t launch_warp_aggregate(hipStream_t s, int store, int mode, const WarpArgs& a, bool blocked) {
+  if (blocked) return store == ST_BF16 ? launch_t<bf16_t, true>(s, mode, a) : launch_t<float, true>(s, mode, a);
+  return store == ST_BF16 ? launch_t<bf16_t, false>(s, mode, a) : launch_t<float, false>(s, mode, a);
+}
+
+hipError_t launch_block_channels(hipStream_t s, int store, const FeatPtrs& src, const FeatPtrs& dst, int N, int B,
+                                 int hw, int C) {
+  const long long n = (long long)N * B * hw * (C / (store == ST_BF16 ? 8 : 4));
+  dim3 grid((unsigned)((n + 255) / 256));
+  if (store == ST_BF16)
+    hipLaunchKernelGGL(block_channels_kernel<bf16_t>, grid, dim3(256), 0, s, src, dst, B, hw, C, N);
+  else
+    hipLaunchKernelGGL(block_channels_kernel<float>, grid, dim3(256), 0, s, src, dst, B, hw, C, N);
+  return hipGetLastError();
 }
 
 }  // namespace damvs

@@ -96,15 +96,18 @@ class StageEngine:
         return depth, conf, var, prob
 
     # ---- split entry points (parity tests / sharded execution)
-    def warp_aggregate(self, feats_nhwc, proj, hyps):
-        N = len(feats_nhwc)
-        B, h, w, C = feats_nhwc[0].shape
-        D = hyps.shape[1]
-        rt = proj_prepare(proj)
+    def warp_aggregate(self, feats, proj, hyps, rt=None, layout=_capi.DAMVS_LAYOUT_NHWC):
+        """feats: N NHWC (B,h,w,C) tensors, or channel-blocked ones (see block_channels) with
+        layout=DAMVS_LAYOUT_CBLOCK; rt from proj_prepare (computed from proj when None)."""
+        N = len(feats)
+        B, D, h, w = hyps.shape
+        C = self.C
+        if rt is None:
+            rt = proj_prepare(proj)
         vol = torch.empty(B, D, h, w, C, device=self.device, dtype=self.dtype)
-        fptrs = (ctypes.c_void_p * N)(*[f.data_ptr() for f in feats_nhwc])
-        check(self._lib.damvs_warp_aggregate(self.handle, _capi.stream_ptr(self.device), B, N, D, h, w, fptrs, ptr(rt),
-                                             ptr(hyps), ptr(vol)))
+        fptrs = (ctypes.c_void_p * N)(*[f.data_ptr() for f in feats])
+        check(self._lib.damvs_warp_aggregate(self.handle, _capi.stream_ptr(self.device), B, N, D, h, w, fptrs, layout,
+                                             ptr(rt), ptr(hyps), ptr(vol)))
         return vol
 
     def costreg_logits(self, vol):
@@ -131,6 +134,20 @@ def proj_prepare(proj):
     rt = torch.empty(B, N - 1, 12, device=proj.device, dtype=torch.float32)
     check(lib.damvs_proj_prepare(_capi.stream_ptr(proj.device), B, N, ptr(proj), ptr(rt)))
     return rt
+
+
+def block_channels(feats_nhwc):
+    """N NHWC (B,h,w,C) maps -> channel-blocked copies [B][C/E][h][w][E] (E = 16 bytes)."""
+    lib = _capi.load_library()
+    N = len(feats_nhwc)
+    B, h, w, C = feats_nhwc[0].shape
+    dt = feats_nhwc[0].dtype
+    E = 16 // feats_nhwc[0].element_size()
+    outs = [torch.empty(B, C // E, h, w, E, device=f.device, dtype=dt) for f in feats_nhwc]
+    src = (ctypes.c_void_p * N)(*[f.data_ptr() for f in feats_nhwc])
+    dst = (ctypes.c_void_p * N)(*[o.data_ptr() for o in outs])
+    check(lib.damvs_block_channels(_capi.stream_ptr(feats_nhwc[0].device), DTYPES[dt], N, B, h, w, C, src, dst))
+    return outs
 
 
 def regress(logits, hyps, want_prob=True):

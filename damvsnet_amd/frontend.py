@@ -94,7 +94,7 @@ class FeatureNet(nn.Module):
                 self.out_channels.append(b)
 
     def forward(self, x):
-        c0 = self.conv0(x)
+        c0 = self.conv0(x.to(self.out1.weight.dtype))
         c1 = self.conv1(c0)
         c2 = self.conv2(c1)
         out = {"stage1": self.out1(c2)}
@@ -199,6 +199,9 @@ class GeoFeatureFusion(nn.Module):
         d2, m2 = sparse_pool_close(d, vm)
         d3, m3 = sparse_pool_close(d2, m2)
         d4, _ = sparse_pool_close(d3, m3)
+        wd = self.rgb_conv_init[0].weight.dtype  # geometry in fp32, convs in the module's dtype
+        rgb, d, d2, d3, d4 = (t.to(wd) for t in (rgb, d, d2, d3, d4))
+        origin_feat = origin_feat.to(wd)
 
         r0 = self.rgb_conv_init(torch.cat((rgb, d), 1))
         r1 = self.rgb_encoder_layer1(r0, d, d2)

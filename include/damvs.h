@@ -112,9 +112,18 @@ int damvs_proj_prepare(void* stream, int B, int N, const float* proj, float* rt)
 int damvs_homo_warp(void* stream, int dtype, int B, int C, int D, int h, int w, const void* src, const float* rt,
                     const float* hyps, void* out);
 
-/* Aggregated cost volume (models/cas_mvsnet.py:26-87): volume [B][D][h][w][C]. */
+/* Feature layouts accepted by damvs_warp_aggregate. */
+enum { DAMVS_LAYOUT_NHWC = 0, DAMVS_LAYOUT_CBLOCK = 1 /* [B][C/E][h][w][E], E = 16 bytes of channels */ };
+
+/* Aggregated cost volume (models/cas_mvsnet.py:26-87): volume [B][D][h][w][C]. `layout` gives the
+ * feature layout (damvs_stage_forward repacks NHWC to DAMVS_LAYOUT_CBLOCK internally when C spans
+ * several 16-byte chunks: each gather instruction then touches half the cache lines). */
 int damvs_warp_aggregate(const damvs_stage* st, void* stream, int B, int N, int D, int h, int w,
-                         const void* const* feats, const float* rt, const float* hyps, void* volume);
+                         const void* const* feats, int layout, const float* rt, const float* hyps, void* volume);
+
+/* NHWC [B][h][w][C] -> DAMVS_LAYOUT_CBLOCK for N maps (src[v] -> dst[v], device buffers). */
+int damvs_block_channels(void* stream, int dtype, int N, int B, int h, int w, int C, const void* const* src,
+                         void* const* dst);
 
 /* CostRegNet forward incl. the final prob conv (models/module.py:532-541): logits [B][D][h][w]. */
 int damvs_costreg_logits(const damvs_stage* st, void* stream, int B, int D, int h, int w, const void* volume,

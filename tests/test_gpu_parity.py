@@ -111,6 +111,24 @@ def test_warp_aggregate_vs_oracle(mode, C, N):
     assert rel_max(np_(vol.permute(0, 4, 1, 2, 3)), ref.numpy()) < 5e-5
 
 
+@pytest.mark.parametrize("C,dtype", [(32, torch.bfloat16), (16, torch.bfloat16), (16, torch.float32),
+                                     (8, torch.float32)])
+def test_warp_aggregate_channel_blocked_layout(C, dtype):
+    """The channel-blocked feature layout (used inside the stage forward) gives the NHWC result."""
+    from damvsnet_amd import _capi
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine, block_channels
+    s = {32: 0, 16: 1, 8: 2}[C]
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    feats, P, hyps = depthnet_inputs(B=2, N=4, H=24, W=40, D=8, stage_idx=s, C=C)
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", dtype, torch.device(DEV))
+    nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(dtype)) for f in feats]
+    a = eng.warp_aggregate(nhwc, cuda(P), cuda(hyps))
+    b = eng.warp_aggregate(block_channels(nhwc), cuda(P), cuda(hyps), layout=_capi.DAMVS_LAYOUT_CBLOCK)
+    assert torch.equal(a, b)
+
+
 # ----------------------------------------------------------------------------- CostRegNet (A6)
 
 @pytest.mark.parametrize("s", [0, 1, 2])

@@ -1,0 +1,19 @@
+"""Per-launch durations of the damvs kernels in the last timed step of a rocprofv3 kernel trace."""
+import csv
+import sys
+
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+key = "prob_regress_kernel" if any("prob_regress_kernel" in r["Kernel_Name"] for r in rows) else "regress_kernel"
+reg = [i for i, r in enumerate(rows) if key in r["Kernel_Name"]]
+ends = reg[2::3]
+step = int(sys.argv[2]) if len(sys.argv) > 2 else len(ends) - 1
+sel = rows[ends[step - 1] + 1:ends[step] + 1]
+tot = 0.0
+for r in sel:
+    n = r["Kernel_Name"]
+    if "damvs" in n:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        tot += d
+        print("%8.1f us  grid %9s x %2s  vgpr %3s lds %6s  %s" % (d, r["Grid_Size_X"], r["Grid_Size_Y"], r["VGPR_Count"],
+                                                               r["LDS_Block_Size"], n.split("(")[0].split("::")[-1][:60]))
+print("damvs total %.1f us" % tot)
