@@ -36,11 +36,11 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
-def build_model(ndepths, dtype, device):
+def build_model(ndepths, dtype, device, frontend="hip"):
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.weights import synthetic_state_dict, apply_bn_stats
     net = CascadeMVSNet(ndepths=list(ndepths), compute_dtype=dtype,
-                        frontend_dtype=torch.bfloat16 if dtype == torch.bfloat16 else None)
+                        frontend_dtype=torch.bfloat16 if dtype == torch.bfloat16 else None, frontend_impl=frontend)
     sd = synthetic_state_dict(net.state_dict(), 0)
     g = np.load(os.path.join(REPO, "tests", "golden", "forward_cfgB_640x512.npz"))
     sd = apply_bn_stats(sd, {k[4:]: g[k] for k in g.files if k.startswith("bn::")})
@@ -95,7 +95,8 @@ def warp_roofline(net, imgs, proj, dv, stage, dtype, iters=20):
     scale = (4, 2, 1)[stage]
     with torch.no_grad():
         feats = net.extract_features(imgs)
-        fs = [to_nhwc(f[name], dtype) for f in feats]
+        fs = [f[name].to(dtype).contiguous() if net.frontend_impl == "hip" else to_nhwc(f[name], dtype)
+              for f in feats]
         blocked = fs[0].shape[-1] * fs[0].element_size() > 16
         fb = block_channels(fs) if blocked else fs
         layout = _capi.DAMVS_LAYOUT_CBLOCK if blocked else _capi.DAMVS_LAYOUT_NHWC
@@ -167,6 +168,7 @@ def main():
     ap.add_argument("--config", default="cfgC", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=1, help="depth maps (reference views) per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--frontend", default="hip", choices=["hip", "torch"], help="2D front-end implementation")
     ap.add_argument("--cpu-budget", type=float, default=60.0)
     args = ap.parse_args()
 
@@ -180,7 +182,7 @@ def main():
     torch.cuda.set_device(device)
 
     H, W, N, nd, dtype, desc = CONFIGS[args.config]
-    net, _ = build_model(nd, dtype, device)
+    net, _ = build_model(nd, dtype, device, args.frontend)
     imgs, proj, dv, ins = make_inputs(args.batch, N, H, W, device, seed=rank)
 
     def barrier():
@@ -225,6 +227,7 @@ def main():
             "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
             "data": "synthetic (seeded DTU-like images/cameras, synthetic weights with calibrated BN stats)",
             "config": {"workload": "%s: %s" % (args.config, desc), "batch_per_gpu": args.batch,
+                       "frontend": args.frontend,
                        "global_batch": args.batch * world, "height": H, "width": W, "views": N,
                        "ndepths": list(nd), "parallelism": "replicas x%d (reference views sharded over ranks)" % world},
             "ms_per_stage": phases,

@@ -38,6 +38,12 @@ class DamvsAggweightParams(ctypes.Structure):
     _fields_ = [("in_channels", c_int), ("w1", c_void_p), ("bn1", DamvsBN), ("w2", c_void_p), ("bn2", DamvsBN)]
 
 
+class DamvsConv2dDesc(ctypes.Structure):
+    _fields_ = [("transposed", c_int), ("kernel", c_int), ("stride", c_int), ("padding", c_int),
+                ("output_padding", c_int), ("cin", c_int), ("cout", c_int), ("c0", c_int), ("c0_at", c_int),
+                ("c1", c_int), ("c1_at", c_int), ("ngeo", c_int), ("geo_at", c_int * 4), ("relu", c_int)]
+
+
 # (name, restype, argtypes) — the full exported surface of include/damvs.h
 SIGNATURES = (
     ("damvs_abi_version", c_int, ()),
@@ -62,6 +68,14 @@ SIGNATURES = (
                               c_void_p, c_void_p)),
     ("damvs_hypotheses", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                  c_int, c_int, c_void_p)),
+    ("damvs_conv2d_create", c_int, (ctypes.POINTER(DamvsConv2dDesc), c_void_p, c_void_p, c_int,
+                                    ctypes.POINTER(c_void_p))),
+    ("damvs_conv2d_destroy", c_int, (c_void_p,)),
+    ("damvs_conv2d_out_size", c_int, (c_void_p, c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                                      ctypes.POINTER(c_int))),
+    ("damvs_conv2d_forward", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                     ctypes.POINTER(c_void_p), ctypes.POINTER(ctypes.c_longlong), c_void_p, c_void_p,
+                                     c_int, c_void_p)),
 )
 
 _lib = None

@@ -7,9 +7,10 @@ plus the last stage's keys at top level). Two extra keyword arguments select pre
 
 * ``compute_dtype``  storage of features / cost volumes in the HIP path: torch.float32 (parity
   path, exact-f32 MFMA) or torch.bfloat16 (bf16 MFMA, fp32 accumulate, fp32 regression).
-* ``frontend_dtype`` dtype of the 2D front-end (FeatureNet, GeoFeatureFusion), which runs on
-  PyTorch-ROCm (MIOpen) as BN-folded channels-last copies (SURVEY.md section 8(f) row f1 — next to be
-  moved to HIP). The originals keep the reference parameters/state_dict.
+* ``frontend_dtype`` storage dtype of the 2D front-end (FeatureNet, GeoFeatureFusion; default
+  float32), and ``frontend_impl``: "hip" (default) runs it on libdamvs's fused NHWC conv2d kernels
+  (frontend_hip.py), "torch" on PyTorch-ROCm/MIOpen as BN-folded channels-last copies (A/B only).
+  The reference-keyed modules keep the parameters/state_dict either way.
 
 Per stage: hypotheses (HIP) -> [GeoFeatureFusion, stages 2/3] -> DepthNet (HIP). The reference's
 host syncs (depth_values .cpu(), :191-193; stage-3 debug prints, :275-285) are not reproduced.
@@ -43,7 +44,7 @@ class RefineNet(nn.Module):
 class CascadeMVSNet(nn.Module):
     def __init__(self, refine=False, ndepths=[64, 32, 8], depth_interals_ratio=[4, 2, 1], share_cr=False,
                  grad_method="detach", arch_mode="fpn", cr_base_chs=[8, 8, 8], agg_mode="adaptive",
-                 compute_dtype=torch.float32, frontend_dtype=None):
+                 compute_dtype=torch.float32, frontend_dtype=None, frontend_impl="hip"):
         super().__init__()
         assert len(ndepths) == len(depth_interals_ratio)
         if len(ndepths) != 3:
@@ -55,6 +56,9 @@ class CascadeMVSNet(nn.Module):
         self.stage_infos = {k: {"scale": float(v)} for k, v in STAGE_SCALE.items()}
         self.compute_dtype = compute_dtype
         self.frontend_dtype = frontend_dtype
+        if frontend_impl not in ("hip", "torch"):
+            raise ValueError("frontend_impl must be 'hip' or 'torch'")
+        self.frontend_impl = frontend_impl
 
         self.feature = FeatureNet(base_channels=8, stride=4, num_stage=self.num_stage, arch_mode=arch_mode)
         self.GeoFeatureFusionNet = GeoFeatureFusion(convolutional_layer_encoding="z", mask_type="basic",
@@ -72,14 +76,20 @@ class CascadeMVSNet(nn.Module):
         self._folded_key = None
 
     def _frontend(self):
-        """BN-folded, channels-last, ``frontend_dtype`` copies of FeatureNet / GeoFeatureFusion,
-        rebuilt whenever their parameters change (load_state_dict bumps tensor versions)."""
+        """Front-end executors, rebuilt whenever FeatureNet / GeoFeatureFusion parameters change
+        (load_state_dict bumps tensor versions): BN-folded copies, then either fused HIP conv2d layer
+        chains ("hip") or channels-last ``frontend_dtype`` module copies ("torch")."""
         fd = self.frontend_dtype or torch.float32
         mods = (self.feature, self.GeoFeatureFusionNet)
         ver = tuple(t._version for m in mods for t in list(m.parameters()) + list(m.buffers()))
-        key = (ver, fd, str(next(self.feature.parameters()).device))
+        key = (ver, fd, self.frontend_impl, str(next(self.feature.parameters()).device))
         if getattr(self, "_folded_key", None) != key:
-            self._folded = tuple(fold_frontend(m, fd) for m in mods)
+            if self.frontend_impl == "hip":
+                from .frontend_hip import HipFeatureNet, HipGeoFeatureFusion
+                f32 = tuple(fold_frontend(m, torch.float32) for m in mods)
+                self._folded = (HipFeatureNet(f32[0], fd), HipGeoFeatureFusion(f32[1], fd))
+            else:
+                self._folded = tuple(fold_frontend(m, fd) for m in mods)
             self._folded_key = key
         return self._folded
 
@@ -88,9 +98,14 @@ class CascadeMVSNet(nn.Module):
         return super()._apply(fn, *a, **k)
 
     def extract_features(self, imgs):
-        """FeatureNet over all views in one batched call (BN in eval is per-sample)."""
+        """FeatureNet over all views in one batched call (BN in eval is per-sample). Returns per view a
+        dict of stage features: NHWC (B,h,w,C) for the HIP front-end, NCHW views for "torch"."""
         feat, _ = self._frontend()
         B, N = imgs.shape[:2]
+        if self.frontend_impl == "hip":
+            x = imgs.transpose(0, 1).reshape(N * B, *imgs.shape[2:])  # view-major: view v = rows v*B..
+            f = feat(x)
+            return [{k: v[i * B:(i + 1) * B] for k, v in f.items()} for i in range(N)]
         x = imgs.reshape(B * N, *imgs.shape[2:]).contiguous(memory_format=torch.channels_last)
         f = feat(x)
         return [{k: v.reshape(B, N, *v.shape[1:])[:, i] for k, v in f.items()} for i in range(N)]
@@ -118,13 +133,19 @@ class CascadeMVSNet(nn.Module):
                                         align_corners=False)
                 dl = F.interpolate(depth.unsqueeze(1), scale_factor=2, mode="bilinear", align_corners=False)
                 cl = F.interpolate(conf.unsqueeze(1), scale_factor=2, mode="bilinear", align_corners=False)
-                fs[0] = geo(ref_img.contiguous(memory_format=torch.channels_last), dl, cl, depth_values, s, fs[0],
-                            None if intrinsics_matrices is None else intrinsics_matrices[name])
+                if self.frontend_impl == "hip":
+                    fs[0] = geo(ref_img, dl, cl, depth_values, s, fs[0])
+                else:
+                    fs[0] = geo(ref_img.contiguous(memory_format=torch.channels_last), dl, cl, depth_values, s,
+                                fs[0], None if intrinsics_matrices is None else intrinsics_matrices[name])
             hook(name + ".hypotheses")
             hyps = hypotheses(depth_values, self.ndepths[s], H, W, scale, depth, exp_var)
             hook(name + ".depthnet")
             cr = self.cost_regularization if self.share_cr else self.cost_regularization[s]
-            out = self.DepthNet(s, fs, proj_matrices[name], hyps, self.ndepths[s], cr)
+            if self.frontend_impl == "hip":
+                out = self.DepthNet.forward_nhwc(s, fs, proj_matrices[name], hyps, cr)
+            else:
+                out = self.DepthNet(s, fs, proj_matrices[name], hyps, self.ndepths[s], cr)
             depth, conf, exp_var = out["depth"], out["photometric_confidence"], out["variance"]
             outputs[name] = out
             outputs.update(out)

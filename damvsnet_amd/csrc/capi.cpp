@@ -521,3 +521,229 @@ int damvs_hypotheses(void* stream, int B, int D, int H, int W, int scale, const 
 }
 
 }  // extern "C"
+
+// ============================================================================ 2D convolutions
+struct damvs_conv2d {
+  damvs_conv2d_desc d;
+  int dtype = 0, cout_pad = 0, cout_store = 0, MTtot = 0, nphase = 0, kchunk_k = 0;
+  Conv2dPhase ph[4];
+  void* wpack = nullptr;
+  float* wgeo = nullptr;
+  float* bias = nullptr;
+};
+
+namespace {
+
+// Tap lists. Conv: input = q*s + (k - p), one phase. Transposed conv of stride s: output parity r
+// per dim takes the kernel taps k with (r + p - k) % s == 0 at input offset (r + p - k) / s.
+int build_phases_2d(damvs_conv2d* L) {
+  const damvs_conv2d_desc& d = L->d;
+  const int K = d.kernel, s = d.stride, p = d.padding;
+  const int ctot = d.c0 + d.c1;
+  std::memset(L->ph, 0, sizeof(L->ph));
+  std::vector<int> offs[2], ks[2];  // per parity r
+  if (!d.transposed) {
+    L->nphase = 1;
+    for (int k = 0; k < K; ++k) { offs[0].push_back(k - p); ks[0].push_back(k); }
+  } else {
+    if (s != 1 && s != 2) return fail(DAMVS_E_SHAPE, "transposed stride %d unsupported", s);
+    L->nphase = s * s;
+    for (int r = 0; r < s; ++r)
+      for (int k = 0; k < K; ++k)
+        if (((r + p - k) % s + s) % s == 0) { offs[r].push_back((r + p - k) / s); ks[r].push_back(k); }
+  }
+  int w_off = 0, g_off = 0;
+  for (int ph = 0; ph < L->nphase; ++ph) {
+    Conv2dPhase& P = L->ph[ph];
+    const int ry = d.transposed ? ph / s : 0, rx = d.transposed ? ph % s : 0;
+    P.py = ry;
+    P.px = rx;
+    int t = 0;
+    for (size_t a = 0; a < offs[ry].size(); ++a)
+      for (size_t b = 0; b < offs[rx].size(); ++b) {
+        if (t >= 25) return fail(DAMVS_E_SHAPE, "more than 25 taps per phase");
+        P.tap[t][0] = (signed char)offs[ry][a];
+        P.tap[t][1] = (signed char)offs[rx][b];
+        P.wtap[t] = (signed char)(ks[ry][a] * K + ks[rx][b]);
+        ++t;
+      }
+    P.ntaps = t;
+    P.kchunks = ctot > 0 ? (t * ctot + L->kchunk_k - 1) / L->kchunk_k : 0;
+    P.w_off = w_off;
+    P.g_off = g_off;
+    w_off += P.kchunks;
+    g_off += t * d.ngeo;
+  }
+  return DAMVS_OK;
+}
+
+float wget(const damvs_conv2d_desc& d, const float* W, int co, int wc, int wt) {
+  const int KK = d.kernel * d.kernel;
+  return d.transposed ? W[((size_t)wc * d.cout + co) * KK + wt] : W[((size_t)co * d.cin + wc) * KK + wt];
+}
+
+template <typename S>
+void pack_2d(const damvs_conv2d* L, const float* W, std::vector<S>& out, S (*cvt)(float)) {
+  const damvs_conv2d_desc& d = L->d;
+  const int E = L->kchunk_k / 4, ctot = d.c0 + d.c1;
+  for (int ph = 0; ph < L->nphase; ++ph) {
+    const Conv2dPhase& P = L->ph[ph];
+    for (int s = 0; s < P.kchunks; ++s)
+      for (int m = 0; m < L->MTtot; ++m)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e = 0; e < E; ++e) {
+            const int co = m * 16 + (lane & 15);
+            const int k = s * L->kchunk_k + (lane >> 4) * E + e;
+            const int t = k / ctot, ci = k % ctot;
+            float v = 0.f;
+            if (co < d.cout && t < P.ntaps) {
+              const int wc = ci < d.c0 ? d.c0_at + ci : d.c1_at + (ci - d.c0);
+              v = wget(d, W, co, wc, (unsigned char)P.wtap[t]);
+            }
+            out.push_back(cvt(v));
+          }
+  }
+}
+
+void conv2d_out(const damvs_conv2d* L, int Hi, int Wi, int* Ho, int* Wo) {
+  const damvs_conv2d_desc& d = L->d;
+  if (d.transposed) {
+    *Ho = (Hi - 1) * d.stride - 2 * d.padding + d.kernel + d.output_padding;
+    *Wo = (Wi - 1) * d.stride - 2 * d.padding + d.kernel + d.output_padding;
+  } else {
+    *Ho = (Hi + 2 * d.padding - d.kernel) / d.stride + 1;
+    *Wo = (Wi + 2 * d.padding - d.kernel) / d.stride + 1;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int damvs_conv2d_create(const damvs_conv2d_desc* desc, const float* weight, const float* bias, int dtype,
+                        damvs_conv2d** out) {
+  if (!desc || !weight || !out) return fail(DAMVS_E_ARG, "null argument");
+  if (dtype != DAMVS_F32 && dtype != DAMVS_BF16) return fail(DAMVS_E_DTYPE, "dtype %d unsupported", dtype);
+  const damvs_conv2d_desc& d = *desc;
+  const int E = dtype == DAMVS_BF16 ? 8 : 4;
+  if (d.kernel < 1 || d.kernel > 5 || d.stride < 1 || d.stride > 2 || d.cout < 1 || d.cin < 1)
+    return fail(DAMVS_E_SHAPE, "kernel %d stride %d cout %d cin %d unsupported", d.kernel, d.stride, d.cout, d.cin);
+  if (d.c0 % E || d.c1 % E || d.c0 < 0 || d.c1 < 0 || (d.c0 == 0 && d.c1 > 0))
+    return fail(DAMVS_E_SHAPE, "tensor input channels must be multiples of %d", E);
+  if (d.ngeo < 0 || d.ngeo > 4 || d.c0 + d.c1 + d.ngeo != d.cin)
+    return fail(DAMVS_E_SHAPE, "c0 + c1 + ngeo (%d) != cin (%d)", d.c0 + d.c1 + d.ngeo, d.cin);
+  damvs_conv2d* L = new damvs_conv2d();
+  L->d = d;
+  L->dtype = dtype;
+  L->kchunk_k = 4 * E;
+  L->MTtot = (d.cout + 15) / 16;
+  L->cout_pad = L->MTtot * 16;
+  L->cout_store = (d.cout + 3) / 4 * 4;
+  int rc = build_phases_2d(L);
+  if (rc == DAMVS_OK && d.c0 + d.c1 > 0) {
+    if (dtype == DAMVS_BF16) {
+      std::vector<uint16_t> pk;
+      pack_2d<uint16_t>(L, weight, pk, cvt_bf16);
+      rc = upload(pk.data(), pk.size() * 2, &L->wpack);
+    } else {
+      std::vector<float> pk;
+      pack_2d<float>(L, weight, pk, cvt_f32);
+      rc = upload(pk.data(), pk.size() * 4, &L->wpack);
+    }
+  }
+  if (rc == DAMVS_OK && d.ngeo > 0) {
+    std::vector<float> wg;
+    for (int ph = 0; ph < L->nphase; ++ph)
+      for (int t = 0; t < L->ph[ph].ntaps; ++t)
+        for (int g = 0; g < d.ngeo; ++g)
+          for (int co = 0; co < L->cout_pad; ++co)
+            wg.push_back(co < d.cout ? wget(d, weight, co, d.geo_at[g], (unsigned char)L->ph[ph].wtap[t]) : 0.f);
+    rc = upload(wg.data(), wg.size() * 4, reinterpret_cast<void**>(&L->wgeo));
+  }
+  if (rc == DAMVS_OK) {
+    std::vector<float> b(L->cout_pad, 0.f);
+    if (bias)
+      for (int i = 0; i < d.cout; ++i) b[i] = bias[i];
+    rc = upload(b.data(), b.size() * 4, reinterpret_cast<void**>(&L->bias));
+  }
+  if (rc != DAMVS_OK) {
+    damvs_conv2d_destroy(L);
+    return rc;
+  }
+  *out = L;
+  return DAMVS_OK;
+}
+
+int damvs_conv2d_destroy(damvs_conv2d* L) {
+  if (!L) return DAMVS_OK;
+  if (L->wpack) (void)hipFree(L->wpack);
+  if (L->wgeo) (void)hipFree(L->wgeo);
+  if (L->bias) (void)hipFree(L->bias);
+  delete L;
+  return DAMVS_OK;
+}
+
+int damvs_conv2d_out_size(const damvs_conv2d* L, int Hi, int Wi, int* Ho, int* Wo, int* cout_stored) {
+  if (!L || !Ho || !Wo) return fail(DAMVS_E_ARG, "null argument");
+  conv2d_out(L, Hi, Wi, Ho, Wo);
+  if (cout_stored) *cout_stored = L->cout_store;
+  return DAMVS_OK;
+}
+
+int damvs_conv2d_forward(const damvs_conv2d* L, void* stream, int B, int Hi, int Wi, const void* in0,
+                         const void* in1, const float* const* geo, const long long* geo_batch_stride, const void* res_pre,
+                         const void* res_post, int post_up, void* out) {
+  if (!L || !out) return fail(DAMVS_E_ARG, "null argument");
+  const damvs_conv2d_desc& d = L->d;
+  if ((d.c0 > 0 && !in0) || (d.c1 > 0 && !in1)) return fail(DAMVS_E_ARG, "missing tensor input");
+  if (d.ngeo > 0 && (!geo || !geo_batch_stride)) return fail(DAMVS_E_ARG, "missing geometry planes");
+  if (B < 1 || Hi < 1 || Wi < 1) return fail(DAMVS_E_SHAPE, "bad shape");
+  if (res_post && post_up != 1 && post_up != 2) return fail(DAMVS_E_ARG, "post_up must be 1 or 2");
+  Conv2dArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.in0 = in0;
+  a.in1 = in1;
+  a.c0 = d.c0;
+  a.c1 = d.c1;
+  a.ngeo = d.ngeo;
+  for (int g = 0; g < d.ngeo; ++g) {
+    if (!geo[g]) return fail(DAMVS_E_ARG, "null geometry plane %d", g);
+    a.geo[g] = geo[g];
+    a.geo_bstride[g] = geo_batch_stride[g];
+  }
+  a.wpack = L->wpack;
+  a.wgeo = L->wgeo;
+  a.bias = L->bias;
+  a.res_pre = res_pre;
+  a.res_post = res_post;
+  a.post_up = res_post ? post_up : 1;
+  a.out = out;
+  a.cout = L->cout_store;
+  a.cout_pad = L->cout_pad;
+  a.MTtot = L->MTtot;
+  a.B = B;
+  a.Hi = Hi;
+  a.Wi = Wi;
+  conv2d_out(L, Hi, Wi, &a.Ho, &a.Wo);
+  if (a.Ho < 1 || a.Wo < 1) return fail(DAMVS_E_SHAPE, "empty output");
+  if (d.transposed) {
+    if (a.Ho != d.stride * Hi || a.Wo != d.stride * Wi)
+      return fail(DAMVS_E_SHAPE, "transposed conv must produce stride x input size");
+    a.Hq = Hi;
+    a.Wq = Wi;
+    a.in_stride = 1;
+    a.out_stride = d.stride;
+  } else {
+    a.Hq = a.Ho;
+    a.Wq = a.Wo;
+    a.in_stride = d.stride;
+    a.out_stride = 1;
+  }
+  if (res_post && (a.Ho % a.post_up || a.Wo % a.post_up)) return fail(DAMVS_E_SHAPE, "bad upsample shape");
+  a.relu = d.relu;
+  a.nphase = L->nphase;
+  std::memcpy(a.ph, L->ph, sizeof(a.ph));
+  return hip_check(launch_conv2d(reinterpret_cast<hipStream_t>(stream), L->dtype, a), "conv2d launch");
+}
+
+}  // extern "C"

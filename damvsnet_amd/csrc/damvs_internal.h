@@ -60,6 +60,36 @@ struct ConvArgs {
   ConvPhase ph[kMaxPhases];
 };
 
+// ---------------------------------------------------------------- 2D front-end convolutions
+// One phase of a 2D conv / transposed conv: input = q * in_stride + tap offset, output =
+// q * out_stride + (py, px). Weights for the tensor inputs are packed like the 3D kernel's
+// (A-fragment order, K = taps x (c0 + c1)); geometry-plane weights are fp32 [tap][g][cout_pad].
+struct Conv2dPhase {
+  int ntaps, kchunks, w_off, g_off, py, px;
+  signed char tap[25][2];  // dy, dx (up to 5 x 5)
+  signed char wtap[25];    // weight tap index ky*k + kx
+  signed char pad_[3];
+};
+
+struct Conv2dArgs {
+  const void* in0;
+  const void* in1;
+  int c0, c1;
+  const float* geo[4];      // planar fp32 [B][Hi][Wi] planes at the input resolution
+  long long geo_bstride[4]; // elements between batches of each geo plane
+  int ngeo;
+  const void* wpack;
+  const float* wgeo;
+  const float* bias;        // [cout_pad]
+  const void* res_pre;      // added before ReLU, [B][Ho][Wo][cout]
+  const void* res_post;     // added after ReLU, [B][Ho/up][Wo/up][cout]
+  int post_up;
+  void* out;                // [B][Ho][Wo][cout]
+  int cout, cout_pad, MTtot;
+  int B, Hi, Wi, Hq, Wq, Ho, Wo, in_stride, out_stride, relu, nphase;
+  Conv2dPhase ph[4];
+};
+
 // ---------------------------------------------------------------- launchers (return hipError_t)
 hipError_t launch_proj_prepare(hipStream_t s, int B, int N, const float* proj, float* rt);
 hipError_t launch_hyp_linear(hipStream_t s, int B, int D, int h, int w, const float* dv, int Dv, float* out);
@@ -73,6 +103,7 @@ hipError_t launch_warp_aggregate(hipStream_t s, int store, int mode, const WarpA
 hipError_t launch_block_channels(hipStream_t s, int store, const FeatPtrs& src, const FeatPtrs& dst, int N, int B,
                                  int hw, int C);
 hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a);
+hipError_t launch_conv2d(hipStream_t s, int store, const Conv2dArgs& a);
 bool conv_lds_disabled();  // DAMVS_CONV_NO_LDS=1 selects the global-gather conv kernel (A/B testing)
 hipError_t launch_prob_conv(hipStream_t s, int store, int B, int Cb, int D, int h, int w, const void* feat,
                             const float* wprob, const float* prob_init, float* logits);

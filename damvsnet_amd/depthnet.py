@@ -70,9 +70,17 @@ class DepthNet(nn.Module):
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()) and self.training:
             raise NotImplementedError("damvsnet_amd is an inference engine; wrap the call in torch.no_grad()")
         _require_gpu(depth_values, proj_matrices, *features)
+        feats = [to_nhwc(f, self.compute_dtype) for f in features]
+        return self.forward_nhwc(stage_idx, feats, proj_matrices, depth_values, cost_regularization,
+                                 prob_volume_init, return_prob_volume)
+
+    def forward_nhwc(self, stage_idx, feats_nhwc, proj_matrices, depth_values, cost_regularization,
+                     prob_volume_init=None, return_prob_volume=True):
+        """Same as forward() with features already NHWC (B,h,w,C) — the HIP front-end's output."""
         dev = depth_values.device
         eng = self.engine(stage_idx, cost_regularization, dev)
-        feats = [to_nhwc(f, self.compute_dtype) for f in features]
+        feats = [f if f.dtype == self.compute_dtype and f.is_contiguous() else f.to(self.compute_dtype).contiguous()
+                 for f in feats_nhwc]
         hyps = depth_values.float().contiguous()
         pinit = prob_volume_init.float().contiguous() if prob_volume_init is not None else None
         depth, conf, var, prob = eng.forward(feats, proj_matrices.float().contiguous(), hyps, pinit,

@@ -1,0 +1,234 @@
+"""The 2D front-end on libdamvs: FeatureNet and GeoFeatureFusion
+as chains of fused HIP conv2d layers (damvs_conv2d_*), NHWC end to end.
+
+Each reference op sequence maps to one launch: conv + BN + ReLU (+ the residual add that follows,
+before or after the ReLU), with the reference's torch.cat of feature maps and 1-channel depth
+planes folded into the conv's inputs. Weights come from the BN-folded copies
+(``frontend_fold.fold_frontend``); the reference-keyed modules stay the parameter owners.
+
+Reference forwards mirrored: FeatureNet.forward models/module.py:417-462 (fpn and unet),
+GeoFeatureFusion.forward models/geometry.py:87-277, BasicBlockGeo.forward geometry.py:410-433,
+SparseDownSampleClose geometry.py:443-455.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn as nn
+
+from . import _capi
+from ._capi import check, ptr
+from .engine import DTYPES
+from .frontend import ConvBNReLU2d, DeconvBNReLU2d, GeoBlock, sparse_pool_close
+
+
+class HipConv2d:
+    """One fused conv2d / conv-transpose2d layer resident on the GPU (damvs_conv2d handle)."""
+
+    def __init__(self, conv, dtype, relu, c0=0, c0_at=0, c1=0, c1_at=0, geo_at=()):
+        lib = _capi.load_library()
+        self._lib = lib
+        tr = isinstance(conv, nn.ConvTranspose2d)
+        w = conv.weight.detach().to("cpu", torch.float32).contiguous()
+        b = conv.bias.detach().to("cpu", torch.float32).contiguous() if conv.bias is not None else None
+        cin = w.shape[0] if tr else w.shape[1]
+        cout = w.shape[1] if tr else w.shape[0]
+        d = _capi.DamvsConv2dDesc()
+        d.transposed = int(tr)
+        d.kernel, d.stride, d.padding = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        d.output_padding = conv.output_padding[0] if tr else 0
+        d.cin, d.cout = cin, cout
+        d.c0, d.c0_at, d.c1, d.c1_at = c0, c0_at, c1, c1_at
+        d.ngeo = len(geo_at)
+        for i, g in enumerate(geo_at):
+            d.geo_at[i] = g
+        d.relu = int(relu)
+        h = ctypes.c_void_p()
+        check(lib.damvs_conv2d_create(ctypes.byref(d), ptr(w), ptr(b), DTYPES[dtype], ctypes.byref(h)))
+        self.handle, self.dtype, self.ngeo = h, dtype, len(geo_at)
+        self.cout = cout
+        self.cout_store = (cout + 3) // 4 * 4
+
+    def __del__(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            try:
+                self._lib.damvs_conv2d_destroy(self.handle)
+            except Exception:
+                pass
+
+    def __call__(self, B, Hi, Wi, in0=None, in1=None, geo=(), res_pre=None, res_post=None, post_up=1):
+        ho, wo, cs = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(self._lib.damvs_conv2d_out_size(self.handle, Hi, Wi, ctypes.byref(ho), ctypes.byref(wo),
+                                              ctypes.byref(cs)))
+        dev = (in0 if in0 is not None else geo[0][0]).device
+        out = torch.empty(B, ho.value, wo.value, cs.value, device=dev, dtype=self.dtype)
+        gp = gs = None
+        if self.ngeo:
+            assert len(geo) == self.ngeo, (len(geo), self.ngeo)
+            gp = (ctypes.c_void_p * 4)(*([g.data_ptr() for g, _ in geo] + [0] * (4 - len(geo))))
+            gs = (ctypes.c_longlong * 4)(*([st for _, st in geo] + [0] * (4 - len(geo))))
+        check(self._lib.damvs_conv2d_forward(self.handle, _capi.stream_ptr(dev), B, Hi, Wi, ptr(in0), ptr(in1), gp,
+                                             gs, ptr(res_pre), ptr(res_post), post_up, ptr(out)))
+        return out
+
+
+def planes(t):
+    """(B, C, H, W) fp32 tensor -> list of C (plane view, batch stride) for the geo inputs."""
+    t = t.float().contiguous()
+    B, C, H, W = t.shape
+    return [(t[:, c], C * H * W) for c in range(C)]
+
+
+class HipFeatureNet:
+    """FeatureNet (fpn or unet) on libdamvs. Input imgs (B, 3, H, W) fp32; outputs NHWC."""
+
+    def __init__(self, fnet, dtype):
+        self.arch, self.num_stage = fnet.arch_mode, fnet.num_stage
+        L = lambda m, relu, **k: HipConv2d(m, dtype, relu, **k)
+        c00, c01 = fnet.conv0[0], fnet.conv0[1]
+        self.c0 = [L(c00.conv, True, geo_at=(0, 1, 2)), L(c01.conv, True, c0=c01.conv.in_channels)]
+        self.c1 = [L(m.conv, True, c0=m.conv.in_channels) for m in fnet.conv1]
+        self.c2 = [L(m.conv, True, c0=m.conv.in_channels) for m in fnet.conv2]
+        self.out1 = L(fnet.out1, False, c0=fnet.out1.in_channels)
+        if self.arch == "fpn":
+            self.inner1 = L(fnet.inner1, False, c0=fnet.inner1.in_channels)
+            self.out2 = L(fnet.out2, False, c0=fnet.out2.in_channels)
+            if self.num_stage == 3:
+                self.inner2 = L(fnet.inner2, False, c0=fnet.inner2.in_channels)
+                self.out3 = L(fnet.out3, False, c0=fnet.out3.in_channels)
+        else:
+            self.up = []
+            for fu in [fnet.deconv1] + ([fnet.deconv2] if self.num_stage == 3 else []):
+                co = fu.deconv.conv.out_channels
+                self.up.append((L(fu.deconv.conv, True, c0=fu.deconv.conv.in_channels),
+                                L(fu.conv.conv, True, c0=co, c0_at=0, c1=co, c1_at=co)))
+            self.out2 = L(fnet.out2, False, c0=fnet.out2.in_channels)
+            if self.num_stage == 3:
+                self.out3 = L(fnet.out3, False, c0=fnet.out3.in_channels)
+
+    def __call__(self, x):
+        B, _, H, W = x.shape
+        t = self.c0[0](B, H, W, geo=planes(x))
+        c0 = self.c0[1](B, H, W, t)
+        h, w = c0.shape[1:3]
+        t = c0
+        for L in self.c1:
+            t = L(B, t.shape[1], t.shape[2], t)
+        c1 = t
+        for L in self.c2:
+            t = L(B, t.shape[1], t.shape[2], t)
+        c2 = t
+        out = {"stage1": self.out1(B, c2.shape[1], c2.shape[2], c2)}
+        if self.arch == "fpn":
+            f = self.inner1(B, c1.shape[1], c1.shape[2], c1, res_post=c2, post_up=2)
+            out["stage2"] = self.out2(B, f.shape[1], f.shape[2], f)
+            if self.num_stage == 3:
+                f = self.inner2(B, c0.shape[1], c0.shape[2], c0, res_post=f, post_up=2)
+                out["stage3"] = self.out3(B, f.shape[1], f.shape[2], f)
+            return out
+        f = c2
+        for i, (dec, conv) in enumerate(self.up):
+            skip = c1 if i == 0 else c0
+            y = dec(B, f.shape[1], f.shape[2], f)
+            f = conv(B, y.shape[1], y.shape[2], y, skip)
+            key = "stage%d" % (i + 2)
+            L = self.out2 if i == 0 else self.out3
+            out[key] = L(B, f.shape[1], f.shape[2], f)
+        return out
+
+
+class _HipGeoBlock:
+    """BasicBlockGeo: conv1(cat(x, g1)) -> ReLU -> conv2(cat(g2, .)) + downsample(cat(x, g1)) -> ReLU."""
+
+    def __init__(self, blk: GeoBlock, dtype, split=None):
+        cin = blk.conv1.in_channels - 1
+        if split is None:
+            x_in = dict(c0=cin)
+        else:  # x is torch.cat([a, b]) of two tensors
+            x_in = dict(c0=split[0], c0_at=0, c1=split[1], c1_at=split[0])
+        self.conv1 = HipConv2d(blk.conv1, dtype, True, geo_at=(cin,), **x_in)
+        cout = blk.conv2.out_channels
+        self.conv2 = HipConv2d(blk.conv2, dtype, True, c0=cout, c0_at=1, geo_at=(0,))
+        self.ds = HipConv2d(blk.downsample[0], dtype, False, geo_at=(cin,), **x_in) if blk.downsample is not None \
+            else None
+        self.split = split
+
+    def __call__(self, x, g1, g2, post=None):
+        xa, xb = x if isinstance(x, tuple) else (x, None)
+        B, H, W = xa.shape[:3]
+        y = self.conv1(B, H, W, xa, xb, geo=g1)
+        idt = self.ds(B, H, W, xa, xb, geo=g1) if self.ds is not None else xa
+        return self.conv2(B, y.shape[1], y.shape[2], y, geo=g2, res_pre=idt, res_post=post)
+
+
+class HipGeoFeatureFusion:
+    """GeoFeatureFusion ('z' encoding, 'basic' mask) on libdamvs; stage_idx 1 or 2."""
+
+    def __init__(self, geo, dtype):
+        self.mask_type = geo.mask_type
+        self.add_origin = geo.add_origin_feat_flag
+        D = lambda seq, relu=True: HipConv2d(seq[0], dtype, relu, c0=seq[0].in_channels)
+        G = lambda b, split=None: _HipGeoBlock(b, dtype, split)
+        self.rgb_init = HipConv2d(geo.rgb_conv_init[0], dtype, True, geo_at=(0, 1, 2, 3))
+        self.rgb_enc = [G(getattr(geo, "rgb_encoder_layer%d" % i)) for i in range(1, 6)]
+        self.rgb_dec4, self.rgb_dec2 = D(geo.rgb_decoder_layer4), D(geo.rgb_decoder_layer2)
+        self.rgb_dec0, self.rgb_dec = D(geo.rgb_decoder_layer0), D(geo.rgb_decoder_layer)
+        self.rgb_out = D(geo.rgb_decoder_output)
+        self.depth_init = HipConv2d(geo.depth_conv_init[0], dtype, True, geo_at=(0, 1))
+        self.dl1, self.dl2 = G(geo.depth_layer1), G(geo.depth_layer2)
+        self.dl3 = G(geo.depth_layer3, split=(32, 32))
+        self.dl4 = G(geo.depth_layer4)
+        self.dl5 = G(geo.depth_layer5, split=(128, 128))
+        self.dec = {i: D(getattr(geo, "decoder_layer%d" % i)) for i in range(3, 8)}
+        self.rgbdepth = {1: D(geo.rgbdepth_decoder_stage2), 2: D(geo.rgbdepth_decoder_stage3)}
+        self.final = {1: D(geo.final_decoder_stage2), 2: D(geo.final_decoder_stage3)}
+
+    def __call__(self, rgb, depth, confidence, depth_values, stage_idx, origin_feat):
+        """rgb (B,3,h,w), depth/confidence (B,1,h,w) fp32; origin_feat NHWC (B,h,w,C). Returns NHWC."""
+        dmin = depth_values[:, 0, None, None, None]
+        dmax = depth_values[:, -1, None, None, None]
+        d = ((depth - dmin) / (dmax - dmin)).float()
+        if self.mask_type == "basic":
+            vm = (d > 0).float()
+        else:
+            vm = torch.logical_and(d > 0, confidence > confidence.mean()).float()
+        d2, m2 = sparse_pool_close(d, vm)
+        d3, m3 = sparse_pool_close(d2, m2)
+        d4, _ = sparse_pool_close(d3, m3)
+        P = {k: planes(v) for k, v in (("d", d), ("d2", d2), ("d3", d3), ("d4", d4))}
+        B, _, h, w = rgb.shape
+        r0 = self.rgb_init(B, h, w, geo=planes(rgb) + P["d"])
+        e = self.rgb_enc
+        r1 = e[0](r0, P["d"], P["d2"])
+        r2 = e[1](r1, P["d2"], P["d2"])
+        r3 = e[2](r2, P["d2"], P["d3"])
+        r4 = e[3](r3, P["d3"], P["d3"])
+        r5 = e[4](r4, P["d3"], P["d4"])
+        run = lambda L, x, **k: L(B, x.shape[1], x.shape[2], x, **k)
+        r4p = run(self.rgb_dec4, r5, res_post=r4)
+        r2p = run(self.rgb_dec2, r4p, res_post=r2)
+        r0p = run(self.rgb_dec0, r2p, res_post=r1)
+        rp = run(self.rgb_dec, r0p, res_post=r0)
+        rgb_out = run(self.rgb_out, rp)
+        rgb_depth = rgb_out[..., 0].float().contiguous()  # (B, h, w) plane
+        s0 = self.depth_init(B, h, w, geo=P["d"] + [(rgb_depth, h * w)])
+        s1 = self.dl1(s0, P["d"], P["d2"])
+        s2 = self.dl2(s1, P["d2"], P["d2"])
+        s3 = self.dl3((r2p, s2), P["d2"], P["d3"])
+        s4 = self.dl4(s3, P["d3"], P["d3"])
+        fusion3 = self.dl5((r4p, s4), P["d3"], P["d4"], post=r5)        # r5 + s5
+        fusion4 = run(self.dec[3], fusion3, res_post=s4)                # s4 + dec3
+        dec4 = run(self.dec[4], fusion4)
+        dec5 = run(self.dec[5], dec4)
+        post_origin = origin_feat if self.add_origin else None
+        if stage_idx == 1:
+            fusion6 = run(self.dec[6], dec5, res_post=s1)               # s1 + dec6
+            f = run(self.rgbdepth[1], fusion6, res_post=post_origin)
+            return run(self.final[1], f)
+        if stage_idx == 2:
+            dec6 = run(self.dec[6], dec5)
+            fusion7 = run(self.dec[7], dec6, res_post=s0)               # s0 + dec7
+            f = run(self.rgbdepth[2], fusion7, res_post=post_origin)
+            return run(self.final[2], f)
+        raise ValueError("GeoFeatureFusion runs at stage_idx 1 or 2, got %r" % (stage_idx,))

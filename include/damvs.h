@@ -142,6 +142,38 @@ int damvs_regress(void* stream, int B, int D, int h, int w, const float* logits,
 int damvs_hypotheses(void* stream, int B, int D, int H, int W, int scale, const float* depth_values, int Dv,
                      const float* prev_depth, const float* prev_var, int hp, int wp, float* hyps);
 
+/* ---- 2D front-end convolutions (FeatureNet models/module.py:355-462,
+ * GeoFeatureFusion models/geometry.py:14-277). One layer = Conv2d or ConvTranspose2d with BN already
+ * folded into weight/bias by the caller, optional ReLU, fused concat of up to two NHWC tensors and up
+ * to four fp32 planar inputs (the reference's torch.cat of feature maps and depth planes), and fused
+ * residual adds before / after the ReLU. */
+typedef struct {
+  int transposed;        /* 0: Conv2d weight [cout][cin][k][k]; 1: ConvTranspose2d weight [cin][cout][k][k] */
+  int kernel, stride, padding, output_padding;
+  int cin, cout;         /* channels of the weight */
+  int c0, c0_at;         /* NHWC tensor input 0: channel count, first weight input channel it feeds */
+  int c1, c1_at;         /* NHWC tensor input 1 (c1 = 0: none) */
+  int ngeo;              /* fp32 planar inputs (<= 4), each one weight input channel: */
+  int geo_at[4];
+  int relu;
+} damvs_conv2d_desc;
+
+typedef struct damvs_conv2d damvs_conv2d;
+
+/* weight / bias: host fp32 (bias may be NULL). c0, c1 must be multiples of 8 (bf16) / 4 (f32);
+ * the output is stored with cout rounded up to a multiple of 4 (extra channels are 0 + ReLU). */
+int damvs_conv2d_create(const damvs_conv2d_desc* desc, const float* weight, const float* bias, int dtype,
+                        damvs_conv2d** out);
+int damvs_conv2d_destroy(damvs_conv2d* layer);
+/* Output spatial size for an Hi x Wi input. */
+int damvs_conv2d_out_size(const damvs_conv2d* layer, int Hi, int Wi, int* Ho, int* Wo, int* cout_stored);
+/* in0/in1: [B][Hi][Wi][c0/c1]; geo[g]: fp32 [Hi][Wi] planes, batch b at geo[g] + b*geo_batch_stride[g];
+ * res_pre / res_post: [B][Ho][Wo][cout_stored] (res_post at (Ho/post_up, Wo/post_up), nearest);
+ * out: [B][Ho][Wo][cout_stored]. */
+int damvs_conv2d_forward(const damvs_conv2d* layer, void* stream, int B, int Hi, int Wi, const void* in0,
+                         const void* in1, const float* const* geo, const long long* geo_batch_stride, const void* res_pre,
+                         const void* res_post, int post_up, void* out);
+
 #ifdef __cplusplus
 }
 #endif

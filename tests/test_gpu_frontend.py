@@ -1,0 +1,150 @@
+"""GPU: the HIP 2D front-end (damvs_conv2d_*) against plain PyTorch fp32 references and the oracle.
+
+Layer level: every form the front-end uses (conv k1/k3/k5 s1/s2, transposed k3 s1 / k5 s2, two
+concatenated tensor inputs, fp32 planar inputs at any weight channel, residual before / after ReLU,
+nearest-x2 upsampled residual, channel padding of cout=2) vs F.conv2d / F.conv_transpose2d on the
+explicitly concatenated input. Network level: FeatureNet and GeoFeatureFusion vs the oracle.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from conftest import rel_max
+from common import model_state, forward_inputs
+from oracle import mvs_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from damvsnet_amd import build, _capi
+    build.build()
+    _capi.load_library()
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+# (transposed, k, s, p, op, c0, c1, geo positions, cout, relu, pre, post_up)
+CASES = [
+    (False, 3, 1, 1, 0, 16, 0, (), 32, True, False, 0),
+    (False, 5, 2, 2, 0, 8, 0, (), 16, True, False, 0),
+    (False, 1, 2, 0, 0, 16, 0, (16,), 32, False, False, 0),          # GeoBlock downsample
+    (False, 3, 2, 1, 0, 32, 32, (64,), 64, True, False, 0),         # cat([a, b], g1) conv1
+    (False, 3, 1, 1, 0, 16, 0, (0,), 16, True, True, 0),            # cat(g2, y) conv2 + identity
+    (False, 5, 1, 2, 0, 0, 0, (0, 1, 2, 3), 8, True, False, 0),      # rgb_conv_init (4 planes)
+    (False, 1, 1, 0, 0, 16, 0, (), 32, False, False, 2),            # FPN inner conv + up2 residual
+    (True, 5, 2, 2, 1, 64, 0, (), 32, True, False, 1),              # decoder deconv + skip
+    (True, 3, 1, 1, 0, 16, 0, (), 8, True, False, 1),
+    (True, 3, 1, 1, 0, 8, 0, (), 2, True, False, 0),                # rgb_decoder_output (cout 2)
+    (False, 3, 1, 1, 0, 256, 0, (), 256, True, False, 0),           # wide layer (cout tiling)
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[str(i) for i in range(len(CASES))])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv2d_layer_vs_torch(case, dtype):
+    from damvsnet_amd.frontend_hip import HipConv2d, planes
+    tr, k, s, p, op, c0, c1, geo, cout, relu, pre, post_up = case
+    g = torch.Generator().manual_seed(hash(case) % 1000)
+    B, H, W = 2, 20, 24
+    cin = c0 + c1 + len(geo)
+    conv = (nn.ConvTranspose2d(cin, cout, k, stride=s, padding=p, output_padding=op) if tr
+            else nn.Conv2d(cin, cout, k, stride=s, padding=p))
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.2)
+        conv.bias.copy_(torch.randn(conv.bias.shape, generator=g) * 0.1)
+    a = torch.randn(B, c0, H, W, generator=g) if c0 else None
+    b = torch.randn(B, c1, H, W, generator=g) if c1 else None
+    gp = torch.randn(B, len(geo), H, W, generator=g) if geo else None
+    # assemble the reference input in weight-channel order
+    full = torch.zeros(B, cin, H, W)
+    tensor_at = [c for c in range(cin) if c not in geo]
+    if c0:
+        full[:, tensor_at[:c0]] = a
+    if c1:
+        full[:, tensor_at[c0:]] = b
+    for i, gc in enumerate(geo):
+        full[:, gc] = gp[:, i]
+    if dtype == torch.bfloat16:  # tensor inputs are stored in bf16
+        full[:, tensor_at] = full[:, tensor_at].to(dtype).float()
+    ref = conv(full)
+    res_pre = torch.randn(ref.shape, generator=g) if pre else None
+    post = None
+    if post_up:
+        post = torch.randn(B, cout, ref.shape[2] // post_up, ref.shape[3] // post_up, generator=g)
+    if dtype == torch.bfloat16:
+        res_pre = res_pre.to(dtype).float() if res_pre is not None else None
+        post = post.to(dtype).float() if post is not None else None
+    y = ref + (res_pre if res_pre is not None else 0)
+    y = F.relu(y) if relu else y
+    if post is not None:
+        y = y + F.interpolate(post, scale_factor=post_up, mode="nearest")
+    at = dict(c0=c0, c1=c1, c1_at=0)
+    if c0 and c1:
+        at = dict(c0=c0, c0_at=tensor_at[0], c1=c1, c1_at=tensor_at[c0])
+    elif c0:
+        at = dict(c0=c0, c0_at=tensor_at[0])
+    L = HipConv2d(conv, dtype, relu, geo_at=geo, **at)
+    cs = L.cout_store
+    padc = lambda t: F.pad(t, (0, 0, 0, 0, 0, cs - cout)) if t is not None and cs != cout else t
+    out = L(B, H, W, nhwc(a).to(DEV, dtype) if c0 else None, nhwc(b).to(DEV, dtype) if c1 else None,
+            geo=planes(gp.to(DEV)) if geo else (),
+            res_pre=nhwc(padc(res_pre)).to(DEV, dtype) if pre else None,
+            res_post=nhwc(padc(post)).to(DEV, dtype) if post_up else None, post_up=max(post_up, 1))
+    got = out.float().cpu()[..., :cout].permute(0, 3, 1, 2)
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    assert got.shape == y.shape
+    assert rel_max(got.numpy(), y.detach().numpy()) < tol
+
+
+def _folded(sd, dtype):
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.frontend_fold import fold_frontend
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(sd)
+    return (fold_frontend(net.feature, torch.float32).to(DEV), fold_frontend(net.GeoFeatureFusionNet, torch.float32).to(DEV))
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 5e-2)])
+def test_featurenet_hip_vs_oracle(dtype, tol):
+    from damvsnet_amd.frontend_hip import HipFeatureNet
+    sd = model_state("forward_160x128_48_32_8")
+    fnet, _ = _folded(sd, dtype)
+    imgs, _, _, _ = forward_inputs(1, 5, 128, 160)
+    x = imgs[0]  # 5 views as a batch
+    ref = O.feature_net(x, sd)
+    got = HipFeatureNet(fnet, dtype)(x.to(DEV))
+    for k in ("stage1", "stage2", "stage3"):
+        err = rel_max(got[k].float().cpu().permute(0, 3, 1, 2).numpy(), ref[k].numpy())
+        assert err < tol, (k, err)
+
+
+@pytest.mark.parametrize("stage_idx", [1, 2])
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 8e-2)])
+def test_geofusion_hip_vs_oracle(stage_idx, dtype, tol):
+    from damvsnet_amd.frontend_hip import HipGeoFeatureFusion
+    sd = model_state("forward_160x128_48_32_8")
+    _, geo = _folded(sd, dtype)
+    imgs, _, dv, _ = forward_inputs(2, 5, 128, 160)
+    g = torch.Generator().manual_seed(stage_idx)
+    scale = 2 ** (2 - stage_idx)
+    h, w = 128 // scale, 160 // scale
+    C = (32, 16, 8)[stage_idx]
+    rgb = F.interpolate(imgs[:, 0], size=(h, w), mode="bilinear", align_corners=False)
+    depth = 425 + 500 * torch.rand(2, 1, h, w, generator=g)
+    depth[:, :, :4] = 300.0  # invalid (d <= 0) rows exercise the sparse-pool mask
+    conf = torch.rand(2, 1, h, w, generator=g)
+    origin = torch.randn(2, C, h, w, generator=g)
+    ref = O.geo_feature_fusion(rgb, depth, conf, dv, stage_idx, origin, sd)
+    got = HipGeoFeatureFusion(geo, dtype)(rgb.to(DEV), depth.to(DEV), conf.to(DEV), dv.to(DEV), stage_idx,
+                                           nhwc(origin).to(DEV, dtype))
+    err = rel_max(got.float().cpu().permute(0, 3, 1, 2).numpy(), ref.numpy())
+    assert err < tol, err
