@@ -61,6 +61,9 @@ __device__ __forceinline__ void st4<bf16_t>(bf16_t* p, const float* r) {
 
 constexpr int kG2 = 4;  // 16-pixel groups per wave
 
+template <typename T>
+__device__ __forceinline__ void tail4(const Conv2dArgs& a, int b, int oy, int ox, int co, float* r);
+
 // Epilogue shared by the MFMA and the VALU-only kernels: geometry planes, bias, residuals, ReLU.
 template <typename T>
 __device__ __forceinline__ void epilogue4(const Conv2dArgs& a, const Conv2dPhase& ph, int b, int qy, int qx, int co,
@@ -78,9 +81,15 @@ __device__ __forceinline__ void epilogue4(const Conv2dArgs& a, const Conv2dPhase
       }
     }
   }
-  const size_t ob = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.cout + co;
 #pragma unroll
   for (int i = 0; i < 4; ++i) r[i] += a.bias[co + i];
+  tail4<T>(a, b, oy, ox, co, r);
+}
+
+// Residual before ReLU, ReLU, (upsampled) residual after ReLU, store of 4 channels.
+template <typename T>
+__device__ __forceinline__ void tail4(const Conv2dArgs& a, int b, int oy, int ox, int co, float* r) {
+  const size_t ob = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.cout + co;
   if (a.res_pre) {
     float q[4];
     ld4<T>(reinterpret_cast<const T*>(a.res_pre) + ob, q);
@@ -189,6 +198,113 @@ __global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, in
   }
 }
 
+// Direct conv for layers whose only inputs are fp32 planes (c0 = c1 = 0: FeatureNet's RGB conv
+// 3x3 3->8, GeoFeatureFusion's RGB+depth 5x5 4->8 and depth+depth 5x5 2->8 init convs). The MFMA
+// kernel would run these in its epilogue with half the lanes idle and one dependent load chain per
+// tap. Here (stride 1, padding K/2) one thread computes 2 vertically adjacent output pixels x all
+// COUT channels: the K+1 input rows they need are loaded row by row (K*NG branch-free coalesced
+// loads in flight per row, each row feeding both pixels); weights sit in LDS as wave-uniform
+// broadcast reads.
+template <typename T, int COUT, int K, int NG>
+__global__ __launch_bounds__(256) void conv2d_planes_kernel(const Conv2dArgs a) {
+  constexpr int P = K / 2, RW = K * NG * COUT / 4;  // float4s per kernel row
+  // [K + 2][kx][g][COUT]: kernel rows -1 and K are zero, so the two pixels' accumulations need no
+  // row-validity branches (row r feeds pixel 0 with kernel row r and pixel 1 with kernel row r-1).
+  __shared__ float4 s_w[(K + 2) * RW];
+  for (int i = threadIdx.x; i < (K + 2) * RW; i += blockDim.x) {
+    const int row = i / RW - 1, j = i % RW;
+    const int c4 = j % (COUT / 4), tg = row * K * NG + j / (COUT / 4);
+    s_w[i] = (row < 0 || row >= K) ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                   : *reinterpret_cast<const float4*>(a.wgeo + (size_t)tg * a.cout_pad + c4 * 4);
+  }
+  __syncthreads();
+  const int Hp = (a.Ho + 1) / 2;
+  const int Qtot = a.B * Hp * a.Wo;  // host checks it fits in int
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Qtot) return;
+  const int ox = q % a.Wo;
+  const int oy0 = (q / a.Wo) % Hp * 2;
+  const int b = q / (a.Wo * Hp);
+  float acc0[COUT], acc1[COUT];
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) acc0[c] = acc1[c] = a.bias[c];
+  const float* gp[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) gp[g] = a.geo[g] + (size_t)b * a.geo_bstride[g];
+#pragma unroll 1
+  for (int r = 0; r <= K; ++r) {
+    const int iy = oy0 - P + r;
+    const bool oky = (unsigned)iy < (unsigned)a.Hi;
+    const int rowoff = (oky ? iy : 0) * a.Wi;
+    float v[K][NG];
+#pragma unroll
+    for (int kx = 0; kx < K; ++kx) {
+      const int ix = ox - P + kx;
+      const bool ok = oky && (unsigned)ix < (unsigned)a.Wi;
+      const int off = rowoff + (ok ? ix : 0);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const float x = gp[g][off];  // clamped address, unconditional load
+        v[kx][g] = ok ? x : 0.f;
+      }
+    }
+    const float4* w0 = s_w + (r + 1) * RW;  // kernel row r for pixel 0
+    const float4* w1 = s_w + r * RW;        // kernel row r-1 for pixel 1
+#pragma unroll
+    for (int kx = 0; kx < K; ++kx)
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int c4 = 0; c4 < COUT / 4; ++c4) {
+          const float4 u = w0[(kx * NG + g) * (COUT / 4) + c4];
+          const float4 z = w1[(kx * NG + g) * (COUT / 4) + c4];
+          const float x = v[kx][g];
+          acc0[c4 * 4 + 0] += u.x * x; acc0[c4 * 4 + 1] += u.y * x;
+          acc0[c4 * 4 + 2] += u.z * x; acc0[c4 * 4 + 3] += u.w * x;
+          acc1[c4 * 4 + 0] += z.x * x; acc1[c4 * 4 + 1] += z.y * x;
+          acc1[c4 * 4 + 2] += z.z * x; acc1[c4 * 4 + 3] += z.w * x;
+        }
+  }
+  const bool two = oy0 + 1 < a.Ho;
+#pragma unroll
+  for (int c0 = 0; c0 < COUT; c0 += 4) {
+    if (c0 >= a.cout) break;
+    tail4<T>(a, b, oy0, ox, c0, acc0 + c0);
+    if (two) tail4<T>(a, b, oy0 + 1, ox, c0, acc1 + c0);
+  }
+}
+
+// True when the layer is a plain (non-transposed) KxK conv with padding K/2 and dense row-major taps.
+bool planes_fast_ok(const Conv2dArgs& a, int K) {
+  if (a.nphase != 1 || a.out_stride != 1 || a.in_stride != 1 || (long long)a.B * a.Ho * a.Wo >= (1LL << 31) || a.ph[0].ntaps != K * K || a.ph[0].g_off != 0) return false;
+  for (int t = 0; t < K * K; ++t)
+    if (a.ph[0].tap[t][0] != t / K - K / 2 || a.ph[0].tap[t][1] != t % K - K / 2) return false;
+  return true;
+}
+
+template <typename T, int COUT, int K>
+hipError_t launch_planes_k(hipStream_t st, const Conv2dArgs& a) {
+  const long long Qtot = (long long)a.B * ((a.Ho + 1) / 2) * a.Wo;
+  dim3 grid((unsigned)((Qtot + 255) / 256));
+  switch (a.ngeo) {
+    case 1: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 1>), grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 2>), grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 3>), grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 4>), grid, dim3(256), 0, st, a); break;
+  }
+  return hipGetLastError();
+}
+
+// Returns hipErrorNotSupported when the layer is not of the fast form (caller uses the MFMA kernel).
+template <typename T>
+hipError_t launch_planes(hipStream_t st, const Conv2dArgs& a) {
+  const int K = a.ph[0].ntaps == 9 ? 3 : a.ph[0].ntaps == 25 ? 5 : 0;
+  if (K == 0 || a.ngeo < 1 || a.ngeo > 4 || a.cout > 16 || a.cout_pad < 16 || !planes_fast_ok(a, K))
+    return hipErrorNotSupported;
+  if (a.cout <= 8) return K == 3 ? launch_planes_k<T, 8, 3>(st, a) : launch_planes_k<T, 8, 5>(st, a);
+  return K == 3 ? launch_planes_k<T, 16, 3>(st, a) : launch_planes_k<T, 16, 5>(st, a);
+}
+
 template <typename T, int MT>
 hipError_t launch_mt(hipStream_t s, const Conv2dArgs& a) {
   const long long Qtot = (long long)a.B * a.Hq * a.Wq;
@@ -200,6 +316,10 @@ hipError_t launch_mt(hipStream_t s, const Conv2dArgs& a) {
 
 template <typename T>
 hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
+  if (a.c0 + a.c1 == 0) {
+    const hipError_t e = launch_planes<T>(s, a);
+    if (e != hipErrorNotSupported) return e;
+  }
   if (a.MTtot >= 4 && a.MTtot % 4 == 0) return launch_mt<T, 4>(s, a);
   if (a.MTtot >= 2 && a.MTtot % 2 == 0) return launch_mt<T, 2>(s, a);
   return launch_mt<T, 1>(s, a);

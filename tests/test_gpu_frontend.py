@@ -40,6 +40,8 @@ CASES = [
     (False, 3, 2, 1, 0, 32, 32, (64,), 64, True, False, 0),         # cat([a, b], g1) conv1
     (False, 3, 1, 1, 0, 16, 0, (0,), 16, True, True, 0),            # cat(g2, y) conv2 + identity
     (False, 5, 1, 2, 0, 0, 0, (0, 1, 2, 3), 8, True, False, 0),      # rgb_conv_init (4 planes)
+    (False, 3, 1, 1, 0, 0, 0, (0, 1, 2), 12, False, True, 2),        # planes-only, cout 12, both residuals
+    (False, 3, 2, 1, 0, 0, 0, (0, 1), 2, True, False, 0),            # planes-only, stride 2, cout 2
     (False, 1, 1, 0, 0, 16, 0, (), 32, False, False, 2),            # FPN inner conv + up2 residual
     (True, 5, 2, 2, 1, 64, 0, (), 32, True, False, 1),              # decoder deconv + skip
     (True, 3, 1, 1, 0, 16, 0, (), 8, True, False, 1),
