@@ -569,9 +569,10 @@ int build_phases_2d(damvs_conv2d* L) {
       }
     P.ntaps = t;
     P.kchunks = ctot > 0 ? (t * ctot + L->kchunk_k - 1) / L->kchunk_k : 0;
+    P.gchunks = d.ngeo > 0 ? (t * d.ngeo + L->kchunk_k - 1) / L->kchunk_k : 0;
     P.w_off = w_off;
     P.g_off = g_off;
-    w_off += P.kchunks;
+    w_off += P.kchunks + P.gchunks;
     g_off += t * d.ngeo;
   }
   return DAMVS_OK;
@@ -588,16 +589,19 @@ void pack_2d(const damvs_conv2d* L, const float* W, std::vector<S>& out, S (*cvt
   const int E = L->kchunk_k / 4, ctot = d.c0 + d.c1;
   for (int ph = 0; ph < L->nphase; ++ph) {
     const Conv2dPhase& P = L->ph[ph];
-    for (int s = 0; s < P.kchunks; ++s)
+    // tensor-input chunks (K = tap x concatenated channel), then plane chunks (K = tap x plane)
+    for (int s = 0; s < P.kchunks + P.gchunks; ++s)
       for (int m = 0; m < L->MTtot; ++m)
         for (int lane = 0; lane < 64; ++lane)
           for (int e = 0; e < E; ++e) {
             const int co = m * 16 + (lane & 15);
-            const int k = s * L->kchunk_k + (lane >> 4) * E + e;
-            const int t = k / ctot, ci = k % ctot;
+            const bool plane = s >= P.kchunks;
+            const int k = (plane ? s - P.kchunks : s) * L->kchunk_k + (lane >> 4) * E + e;
+            const int per = plane ? d.ngeo : ctot;
+            const int t = k / per, ci = k % per;
             float v = 0.f;
             if (co < d.cout && t < P.ntaps) {
-              const int wc = ci < d.c0 ? d.c0_at + ci : d.c1_at + (ci - d.c0);
+              const int wc = plane ? d.geo_at[ci] : ci < d.c0 ? d.c0_at + ci : d.c1_at + (ci - d.c0);
               v = wget(d, W, co, wc, (unsigned char)P.wtap[t]);
             }
             out.push_back(cvt(v));
@@ -640,7 +644,7 @@ int damvs_conv2d_create(const damvs_conv2d_desc* desc, const float* weight, cons
   L->cout_pad = L->MTtot * 16;
   L->cout_store = (d.cout + 3) / 4 * 4;
   int rc = build_phases_2d(L);
-  if (rc == DAMVS_OK && d.c0 + d.c1 > 0) {
+  if (rc == DAMVS_OK && d.c0 + d.c1 + d.ngeo > 0) {
     if (dtype == DAMVS_BF16) {
       std::vector<uint16_t> pk;
       pack_2d<uint16_t>(L, weight, pk, cvt_bf16);

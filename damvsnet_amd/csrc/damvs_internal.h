@@ -65,7 +65,7 @@ struct ConvArgs {
 // q * out_stride + (py, px). Weights for the tensor inputs are packed like the 3D kernel's
 // (A-fragment order, K = taps x (c0 + c1)); geometry-plane weights are fp32 [tap][g][cout_pad].
 struct Conv2dPhase {
-  int ntaps, kchunks, w_off, g_off, py, px;
+  int ntaps, kchunks, gchunks, w_off, g_off, py, px;  // kchunks: tensor-input K chunks; gchunks: plane K chunks
   signed char tap[25][2];  // dy, dx (up to 5 x 5)
   signed char wtap[25];    // weight tap index ky*k + kx
   signed char pad_[3];

@@ -2,8 +2,9 @@
 // models/geometry.py:14-277) as NHWC implicit GEMM on MFMA, with the glue the reference runs as
 // separate ops fused in:
 //   * channel concat of two feature tensors (torch.cat([r2p, s2]) etc.): K runs over in0 then in1;
-//   * up to 4 fp32 planar "geometry" inputs (the 1-channel depth planes BasicBlockGeo concatenates,
-//     or the RGB/depth planes of the 2-4 channel init convs) added by VALU in the epilogue;
+//   * up to 4 fp32 planar "geometry" inputs (the 1-channel depth planes BasicBlockGeo concatenates)
+//     as extra K rows (tap x plane) after the tensor-input chunks; layers whose only inputs are
+//     planes (the RGB/depth init convs) run on a direct VALU kernel instead;
 //   * bias (BN folded host side), residual before ReLU (BasicBlockGeo identity/downsample),
 //     ReLU, residual after ReLU (decoder skips, FPN's nearest-x2 upsampled top-down path).
 // Conv and ConvTranspose share one kernel: a transposed conv of stride s is s^2 output-parity
@@ -61,26 +62,21 @@ __device__ __forceinline__ void st4<bf16_t>(bf16_t* p, const float* r) {
 
 constexpr int kG2 = 4;  // 16-pixel groups per wave
 
+template <typename T> __device__ __forceinline__ typename Frag2<T>::raw pack_vals(const float* v);
+template <> __device__ __forceinline__ float4 pack_vals<float>(const float* v) { return make_float4(v[0], v[1], v[2], v[3]); }
+template <> __device__ __forceinline__ uint4 pack_vals<bf16_t>(const float* v) {
+  return make_uint4((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16), (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16),
+                    (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16), (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16));
+}
+
 template <typename T>
 __device__ __forceinline__ void tail4(const Conv2dArgs& a, int b, int oy, int ox, int co, float* r);
 
-// Epilogue shared by the MFMA and the VALU-only kernels: geometry planes, bias, residuals, ReLU.
+// MFMA epilogue: bias, then residuals / ReLU / store.
 template <typename T>
 __device__ __forceinline__ void epilogue4(const Conv2dArgs& a, const Conv2dPhase& ph, int b, int qy, int qx, int co,
                                           float* r) {
   const int oy = qy * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
-  if (a.ngeo > 0) {
-    const float* wg = a.wgeo + (size_t)ph.g_off * a.cout_pad;  // [tap][g][cout_pad]
-    for (int t = 0; t < ph.ntaps; ++t) {
-      const int iy = qy * a.in_stride + ph.tap[t][0], ix = qx * a.in_stride + ph.tap[t][1];
-      if ((unsigned)iy >= (unsigned)a.Hi || (unsigned)ix >= (unsigned)a.Wi) continue;
-      for (int g = 0; g < a.ngeo; ++g) {
-        const float v = a.geo[g][(size_t)b * a.geo_bstride[g] + (size_t)iy * a.Wi + ix];
-        const float4 w = *reinterpret_cast<const float4*>(wg + ((size_t)t * a.ngeo + g) * a.cout_pad + co);
-        r[0] += w.x * v; r[1] += w.y * v; r[2] += w.z * v; r[3] += w.w * v;
-      }
-    }
-  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) r[i] += a.bias[co + i];
   tail4<T>(a, b, oy, ox, co, r);
@@ -177,6 +173,50 @@ __global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, in
         const size_t off = ok ? (((size_t)vb[j] * a.Hi + iy) * a.Wi + ix) * cs + ci : 0;
         const raw v = *reinterpret_cast<const raw*>((ok ? src : in0) + off);
         xf[j] = ok ? v : Frag2<T>::zero();
+      }
+#pragma unroll
+      for (int j = 0; j < kG2; ++j)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf[j], acc[j][m]);
+    }
+  }
+
+  // fp32 planes (BasicBlockGeo's concatenated depth planes, the init convs' RGB/depth) as extra K
+  // rows tap x plane, rounded to the compute type like the reference's torch.cat(...).to(dtype).
+  if (ph.gchunks > 0) {
+    const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) +
+                                 ((size_t)(ph.w_off + ph.kchunks) * a.MTtot + mt0) * 64 + lane;
+    for (int s = 0; s < ph.gchunks; ++s) {
+      raw wf[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * a.MTtot + m) * 64];
+      int dy[E], dx[E];
+      const float* pl[E];
+      long long pbs[E];
+      bool tv[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int k = s * KC + g * E + e;
+        const int t = k / a.ngeo, gi = k - t * a.ngeo;
+        tv[e] = t < ph.ntaps;
+        const int code = s_tap[tv[e] ? t : 0];
+        dy[e] = (code & 0xff) - 8;
+        dx[e] = ((code >> 8) & 0xff) - 8;
+        pl[e] = gi == 0 ? a.geo[0] : gi == 1 ? a.geo[1] : gi == 2 ? a.geo[2] : a.geo[3];
+        pbs[e] = gi == 0 ? a.geo_bstride[0] : gi == 1 ? a.geo_bstride[1] : gi == 2 ? a.geo_bstride[2] : a.geo_bstride[3];
+      }
+      raw xf[kG2];
+#pragma unroll
+      for (int j = 0; j < kG2; ++j) {
+        float v[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int iy = vy[j] * a.in_stride + dy[e], ix = vx[j] * a.in_stride + dx[e];
+          const bool ok = valid[j] && tv[e] && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+          const float x = pl[e][ok ? (size_t)vb[j] * pbs[e] + (size_t)iy * a.Wi + ix : 0];
+          v[e] = ok ? x : 0.f;
+        }
+        xf[j] = pack_vals<T>(v);
       }
 #pragma unroll
       for (int j = 0; j < kG2; ++j)
