@@ -636,6 +636,10 @@ int damvs_conv2d_create(const damvs_conv2d_desc* desc, const float* weight, cons
     return fail(DAMVS_E_SHAPE, "tensor input channels must be multiples of %d", E);
   if (d.ngeo < 0 || d.ngeo > 4 || d.c0 + d.c1 + d.ngeo != d.cin)
     return fail(DAMVS_E_SHAPE, "c0 + c1 + ngeo (%d) != cin (%d)", d.c0 + d.c1 + d.ngeo, d.cin);
+  if (d.c0 + d.c1 > 0 && d.ngeo > 1)
+    return fail(DAMVS_E_SHAPE, "at most one fp32 plane next to tensor inputs (got %d)", d.ngeo);
+  if (d.c0 + d.c1 == 0 && d.cout > 16)
+    return fail(DAMVS_E_SHAPE, "plane-only layers support cout <= 16 (got %d)", d.cout);
   damvs_conv2d* L = new damvs_conv2d();
   L->d = d;
   L->dtype = dtype;
@@ -746,6 +750,8 @@ int damvs_conv2d_forward(const damvs_conv2d* L, void* stream, int B, int Hi, int
   if (res_post && (a.Ho % a.post_up || a.Wo % a.post_up)) return fail(DAMVS_E_SHAPE, "bad upsample shape");
   a.relu = d.relu;
   a.nphase = L->nphase;
+  a.div_wq = make_fastdiv(a.Wq);
+  a.div_hq = make_fastdiv(a.Hq);
   std::memcpy(a.ph, L->ph, sizeof(a.ph));
   return hip_check(launch_conv2d(reinterpret_cast<hipStream_t>(stream), L->dtype, a), "conv2d launch");
 }

@@ -71,6 +71,26 @@ struct Conv2dPhase {
   signed char pad_[3];
 };
 
+// n / d for 0 <= n < 2^31 without a hardware divide: q = (umulhi(n, mul) + n) >> shift.
+struct FastDiv {
+  uint32_t mul, shift;
+  int d;
+};
+inline FastDiv make_fastdiv(int d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t sh = 0;
+  while (sh < 31 && (1u << sh) < (uint32_t)d) ++sh;
+  f.shift = sh;
+  f.mul = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << sh) - (uint64_t)d)) / (uint64_t)d + 1);
+  return f;
+}
+#ifdef __HIPCC__
+__device__ __forceinline__ int fdiv(const FastDiv& f, int n) {
+  return (int)((__umulhi((uint32_t)n, f.mul) + (uint32_t)n) >> f.shift);
+}
+#endif
+
 struct Conv2dArgs {
   const void* in0;
   const void* in1;
@@ -87,6 +107,7 @@ struct Conv2dArgs {
   void* out;                // [B][Ho][Wo][cout]
   int cout, cout_pad, MTtot;
   int B, Hi, Wi, Hq, Wq, Ho, Wo, in_stride, out_stride, relu, nphase;
+  FastDiv div_wq, div_hq;   // output-grid decomposition q -> (b, qy, qx)
   Conv2dPhase ph[4];
 };
 

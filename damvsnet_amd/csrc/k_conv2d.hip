@@ -9,6 +9,8 @@
 //     ReLU, residual after ReLU (decoder skips, FPN's nearest-x2 upsampled top-down path).
 // Conv and ConvTranspose share one kernel: a transposed conv of stride s is s^2 output-parity
 // phases, each a dense sub-convolution over the input grid (no structural zeros on MFMA).
+#include <cstdlib>
+
 #include "damvs_device.h"
 
 namespace damvs {
@@ -61,6 +63,8 @@ __device__ __forceinline__ void st4<bf16_t>(bf16_t* p, const float* r) {
 }
 
 constexpr int kG2 = 4;  // 16-pixel groups per wave
+typedef unsigned int v4u32_t __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u32_t __attribute__((ext_vector_type(2)));
 
 template <typename T> __device__ __forceinline__ typename Frag2<T>::raw pack_vals(const float* v);
 template <> __device__ __forceinline__ float4 pack_vals<float>(const float* v) { return make_float4(v[0], v[1], v[2], v[3]); }
@@ -69,23 +73,11 @@ template <> __device__ __forceinline__ uint4 pack_vals<bf16_t>(const float* v) {
                     (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16), (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16));
 }
 
-template <typename T>
-__device__ __forceinline__ void tail4(const Conv2dArgs& a, int b, int oy, int ox, int co, float* r);
-
-// MFMA epilogue: bias, then residuals / ReLU / store.
-template <typename T>
-__device__ __forceinline__ void epilogue4(const Conv2dArgs& a, const Conv2dPhase& ph, int b, int qy, int qx, int co,
-                                          float* r) {
-  const int oy = qy * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) r[i] += a.bias[co + i];
-  tail4<T>(a, b, oy, ox, co, r);
-}
-
-// Residual before ReLU, ReLU, (upsampled) residual after ReLU, store of 4 channels.
+// Residual before ReLU, ReLU, (upsampled) residual after ReLU, store of 4 channels (32-bit indices:
+// the launcher keeps every operand below 2^31 elements).
 template <typename T>
 __device__ __forceinline__ void tail4(const Conv2dArgs& a, int b, int oy, int ox, int co, float* r) {
-  const size_t ob = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.cout + co;
+  const uint32_t ob = (uint32_t)(((b * a.Ho + oy) * a.Wo + ox) * a.cout + co);
   if (a.res_pre) {
     float q[4];
     ld4<T>(reinterpret_cast<const T*>(a.res_pre) + ob, q);
@@ -98,7 +90,7 @@ __device__ __forceinline__ void tail4(const Conv2dArgs& a, int b, int oy, int ox
   }
   if (a.res_post) {
     const int up = a.post_up;  // 1, or 2 for a nearest-x2 upsampled source of half resolution
-    const size_t pb = (((size_t)b * (a.Ho / up) + oy / up) * (a.Wo / up) + ox / up) * a.cout + co;
+    const uint32_t pb = (uint32_t)(((b * (a.Ho / up) + oy / up) * (a.Wo / up) + ox / up) * a.cout + co);
     float q[4];
     ld4<T>(reinterpret_cast<const T*>(a.res_post) + pb, q);
 #pragma unroll
@@ -107,11 +99,65 @@ __device__ __forceinline__ void tail4(const Conv2dArgs& a, int b, int oy, int ox
   st4<T>(reinterpret_cast<T*>(a.out) + ob, r);
 }
 
-template <typename T, int MT>
+// Buffer loads/stores: 32-bit byte offsets against a descriptor whose range check returns 0 for an
+// offset past the end (and drops such a store), so padding taps and tail pixels need no branch.
+constexpr uint32_t kOOB = 0x80000000u;  // every operand is < 2 GiB (checked by the launcher)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+template <typename T> struct BufIO;
+template <> struct BufIO<float> {
+  typedef float4 raw;   // one MFMA K fragment (4 channels x 4 K-steps)
+  typedef float4 quad;  // 4 output channels
+  __device__ __forceinline__ static raw frag(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  }
+  __device__ __forceinline__ static raw merge(const raw& x, const raw& y) {
+    return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+  }
+  __device__ __forceinline__ static quad ldq(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  }
+  __device__ __forceinline__ static void addq(const quad& q, float* v) { v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w; }
+  __device__ __forceinline__ static void stq(__amdgpu_buffer_rsrc_t r, uint32_t off, const float* v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, make_float4(v[0], v[1], v[2], v[3])), r, off, 0, 0);
+  }
+};
+template <> struct BufIO<bf16_t> {
+  typedef uint4 raw;
+  typedef uint2 quad;
+  __device__ __forceinline__ static raw frag(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  }
+  __device__ __forceinline__ static raw merge(const raw& x, const raw& y) {
+    return make_uint4(x.x | y.x, x.y | y.y, x.z | y.z, x.w | y.w);
+  }
+  __device__ __forceinline__ static quad ldq(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+  }
+  __device__ __forceinline__ static void addq(const quad& q, float* v) {
+    v[0] += __uint_as_float(q.x << 16); v[1] += __uint_as_float(q.x & 0xffff0000u);
+    v[2] += __uint_as_float(q.y << 16); v[3] += __uint_as_float(q.y & 0xffff0000u);
+  }
+  __device__ __forceinline__ static void stq(__amdgpu_buffer_rsrc_t r, uint32_t off, const float* v) {
+    const uint2 w = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                               (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, w), r, off, 0, 0);
+  }
+};
+
+// Implicit-GEMM conv on MFMA. A wave owns 64 output pixels (kG2 groups of 16) x MT 16-channel
+// tiles. K runs over (tap, concatenated channel) in chunks of KC = 4E, then over (tap, plane) for
+// the fp32 planes. Index arithmetic is 32-bit and incremental (no divisions in the K loop): the
+// kernel is otherwise VALU-bound on address math for the thin full-resolution layers.
+template <typename T, int MT, bool TWO>
 __global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, int nqblk) {
-  typedef typename Frag2<T>::raw raw;
+  typedef BufIO<T> IO;
+  typedef typename IO::raw raw;
   constexpr int E = Stor<T>::E;
   constexpr int KC = 4 * E;
+  constexpr uint32_t ES = sizeof(T);
   // logical block = (q-block, phase), phase fastest, XCD-contiguous (see conv3d_mfma_kernel)
   const int nblk = nqblk * a.nphase;
   const int bid = blockIdx.x, q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
@@ -120,25 +166,32 @@ __global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, in
   const Conv2dPhase& ph = a.ph[L - qblk * a.nphase];
   const int mt0 = blockIdx.y * MT;  // first 16-channel output tile of this block
 
-  __shared__ int s_tap[32];
+  __shared__ int s_tap[32];  // packed (dy + 8) | (dx + 8) << 8
   if (threadIdx.x < 25) s_tap[threadIdx.x] = ((int)(ph.tap[threadIdx.x][0] + 8)) | ((int)(ph.tap[threadIdx.x][1] + 8) << 8);
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
-  const long long Qtot = (long long)a.B * a.Hq * a.Wq;
-  const long long base = ((long long)qblk * 4 + wave) * (kG2 * 16);
+  const int Qtot = a.B * a.Hq * a.Wq;
+  const int base = (qblk * 4 + wave) * (kG2 * 16);
   if (base >= Qtot) return;
-  int vb[kG2], vy[kG2], vx[kG2];
+  // per pixel group: input origin (y, x, flat pixel index), output flat pixel index
+  int ys[kG2], xs[kG2], pin[kG2], pout[kG2], ppost[kG2];
   bool valid[kG2];
 #pragma unroll
   for (int j = 0; j < kG2; ++j) {
-    long long q = base + j * 16 + n;
+    int q = base + j * 16 + n;
     valid[j] = q < Qtot;
-    if (!valid[j]) q = 0;
-    vx[j] = (int)(q % a.Wq); q /= a.Wq;
-    vy[j] = (int)(q % a.Hq);
-    vb[j] = (int)(q / a.Hq);
+    q = valid[j] ? q : 0;
+    const int r = fdiv(a.div_wq, q), qx = q - r * a.Wq;
+    const int b = fdiv(a.div_hq, r), qy = r - b * a.Hq;
+    ys[j] = qy * a.in_stride;
+    xs[j] = qx * a.in_stride;
+    pin[j] = (b * a.Hi + ys[j]) * a.Wi + xs[j];
+    const int oy = qy * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
+    pout[j] = (b * a.Ho + oy) * a.Wo + ox;
+    const int us = a.post_up >> 1;  // post_up is 1 or 2
+    ppost[j] = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
   }
   f32x4_t acc[kG2][MT];
 #pragma unroll
@@ -146,78 +199,82 @@ __global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, in
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
+  const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + ((size_t)ph.w_off * a.MTtot + mt0) * 64 + lane;
+  const int npix = a.B * a.Hi * a.Wi;
   const int ctot = a.c0 + a.c1;
-  if (ctot > 0) {
-    const T* __restrict__ in0 = reinterpret_cast<const T*>(a.in0);
-    const T* __restrict__ in1 = reinterpret_cast<const T*>(a.in1);
-    const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + ((size_t)ph.w_off * a.MTtot + mt0) * 64 + lane;
-    for (int s = 0; s < ph.kchunks; ++s) {
-      const int k0 = s * KC + g * E;
-      const int t = k0 / ctot;
-      int ci = k0 - t * ctot;
+  const int nk = ph.kchunks;
+  if (nk > 0) {
+    const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.in0, (long long)npix * a.c0 * ES);
+    const __amdgpu_buffer_rsrc_t r1 = make_rsrc(TWO ? a.in1 : a.in0, TWO ? (long long)npix * a.c1 * ES : 0);
+    int t = (g * E) / ctot, ci = g * E - t * ctot;  // this lane's (tap, channel) at k = s*KC + g*E
+    const int qt = KC / ctot, rc = KC - qt * ctot;
+    for (int s = 0; s < nk; ++s) {
+      raw wf[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * a.MTtot + m) * 64];
       const bool tv = t < ph.ntaps;
       const int code = s_tap[tv ? t : 0];
       const int dy = (code & 0xff) - 8, dx = ((code >> 8) & 0xff) - 8;
-      const bool second = ci >= a.c0;
-      const T* src = second ? in1 : in0;
-      const int cs = second ? a.c1 : a.c0;
-      ci = second ? ci - a.c0 : ci;
-      raw wf[MT];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * a.MTtot + m) * 64];
+      const int tapoff = dy * a.Wi + dx;
+      const bool second = TWO && ci >= a.c0;
+      const int cs = second ? a.c1 : a.c0, cl = second ? ci - a.c0 : ci;
       raw xf[kG2];
 #pragma unroll
       for (int j = 0; j < kG2; ++j) {
-        const int iy = vy[j] * a.in_stride + dy, ix = vx[j] * a.in_stride + dx;
+        const int iy = ys[j] + dy, ix = xs[j] + dx;
         const bool ok = valid[j] && tv && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
-        const size_t off = ok ? (((size_t)vb[j] * a.Hi + iy) * a.Wi + ix) * cs + ci : 0;
-        const raw v = *reinterpret_cast<const raw*>((ok ? src : in0) + off);
-        xf[j] = ok ? v : Frag2<T>::zero();
+        const uint32_t off = (uint32_t)((pin[j] + tapoff) * cs + cl) * ES;
+        if (TWO)
+          xf[j] = IO::merge(IO::frag(r0, ok && !second ? off : kOOB), IO::frag(r1, ok && second ? off : kOOB));
+        else
+          xf[j] = IO::frag(r0, ok ? off : kOOB);
       }
 #pragma unroll
       for (int j = 0; j < kG2; ++j)
 #pragma unroll
         for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf[j], acc[j][m]);
+      ci += rc;
+      t += qt;
+      if (ci >= ctot) { ci -= ctot; ++t; }
     }
   }
 
-  // fp32 planes (BasicBlockGeo's concatenated depth planes, the init convs' RGB/depth) as extra K
-  // rows tap x plane, rounded to the compute type like the reference's torch.cat(...).to(dtype).
+  // the fp32 plane (BasicBlockGeo's concatenated depth plane; host allows at most one next to
+  // tensor inputs) as extra K rows, one per tap, rounded to the compute type like the reference's
+  // torch.cat(...).to(dtype)
   if (ph.gchunks > 0) {
-    const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) +
-                                 ((size_t)(ph.w_off + ph.kchunks) * a.MTtot + mt0) * 64 + lane;
+    const raw* __restrict__ wg = wp + (size_t)nk * a.MTtot * 64;
+    const int plane = a.Hi * a.Wi;
+    const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.geo[0], ((long long)(a.B - 1) * a.geo_bstride[0] + plane) * 4);
+    int pg[kG2];  // plane offset of the pixel's tap-(0,0) input
+#pragma unroll
+    for (int j = 0; j < kG2; ++j) {  // batch of the pixel group: recover from its flat input index
+      const int b = fdiv(a.div_hq, fdiv(a.div_wq, valid[j] ? base + j * 16 + n : 0));
+      pg[j] = b * (int)a.geo_bstride[0] + (pin[j] - b * plane);
+    }
     for (int s = 0; s < ph.gchunks; ++s) {
       raw wf[MT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * a.MTtot + m) * 64];
-      int dy[E], dx[E];
-      const float* pl[E];
-      long long pbs[E];
-      bool tv[E];
+      for (int m = 0; m < MT; ++m) wf[m] = wg[(size_t)(s * a.MTtot + m) * 64];
+      float v[kG2][E];
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const int k = s * KC + g * E + e;
-        const int t = k / a.ngeo, gi = k - t * a.ngeo;
-        tv[e] = t < ph.ntaps;
-        const int code = s_tap[tv[e] ? t : 0];
-        dy[e] = (code & 0xff) - 8;
-        dx[e] = ((code >> 8) & 0xff) - 8;
-        pl[e] = gi == 0 ? a.geo[0] : gi == 1 ? a.geo[1] : gi == 2 ? a.geo[2] : a.geo[3];
-        pbs[e] = gi == 0 ? a.geo_bstride[0] : gi == 1 ? a.geo_bstride[1] : gi == 2 ? a.geo_bstride[2] : a.geo_bstride[3];
+        const int t = s * KC + g * E + e;
+        const bool tv = t < ph.ntaps;
+        const int code = s_tap[tv ? t : 0];
+        const int dy = (code & 0xff) - 8, dx = ((code >> 8) & 0xff) - 8;
+        const int tapoff = dy * a.Wi + dx;
+#pragma unroll
+        for (int j = 0; j < kG2; ++j) {
+          const int iy = ys[j] + dy, ix = xs[j] + dx;
+          const bool ok = valid[j] && tv && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+          v[j][e] = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(rg, ok ? (uint32_t)(pg[j] + tapoff) * 4u : kOOB, 0, 0));
+        }
       }
       raw xf[kG2];
 #pragma unroll
-      for (int j = 0; j < kG2; ++j) {
-        float v[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const int iy = vy[j] * a.in_stride + dy[e], ix = vx[j] * a.in_stride + dx[e];
-          const bool ok = valid[j] && tv[e] && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
-          const float x = pl[e][ok ? (size_t)vb[j] * pbs[e] + (size_t)iy * a.Wi + ix : 0];
-          v[e] = ok ? x : 0.f;
-        }
-        xf[j] = pack_vals<T>(v);
-      }
+      for (int j = 0; j < kG2; ++j) xf[j] = pack_vals<T>(v[j]);
 #pragma unroll
       for (int j = 0; j < kG2; ++j)
 #pragma unroll
@@ -225,15 +282,45 @@ __global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, in
     }
   }
 
+  // epilogue: residual loads first, then bias / residual / ReLU / store
+  typedef typename IO::quad quad;
+  const int up = a.post_up;
+  const long long nout = (long long)a.B * a.Ho * a.Wo * a.cout;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout * ES);
+  const __amdgpu_buffer_rsrc_t rpre = make_rsrc(a.res_pre ? a.res_pre : a.out, a.res_pre ? nout * ES : 0);
+  const __amdgpu_buffer_rsrc_t rpost = make_rsrc(a.res_post ? a.res_post : a.out, a.res_post ? nout / (up * up) * ES : 0);
+  float bias[MT][4];
+  bool cok[MT];
 #pragma unroll
-  for (int j = 0; j < kG2; ++j) {
-    if (!valid[j]) continue;
+  for (int m = 0; m < MT; ++m) {
+    const int co = (mt0 + m) * 16 + g * 4;
+    cok[m] = co < a.cout;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[m][i] = a.bias[co + i];  // padded to cout_pad
+  }
+#pragma unroll
+  for (int j = 0; j < kG2; ++j) {  // residual loads of one pixel group first, then the math
+    quad qpre[MT], qpost[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
+      const bool ok = valid[j] && cok[m];
       const int co = (mt0 + m) * 16 + g * 4;
-      if (co >= a.cout) continue;
-      float r[4] = {acc[j][m][0], acc[j][m][1], acc[j][m][2], acc[j][m][3]};
-      epilogue4<T>(a, ph, vb[j], vy[j], vx[j], co, r);
+      if (a.res_pre) qpre[m] = IO::ldq(rpre, ok ? (uint32_t)(pout[j] * a.cout + co) * ES : kOOB);
+      if (a.res_post) qpost[m] = IO::ldq(rpost, ok ? (uint32_t)(ppost[j] * a.cout + co) * ES : kOOB);
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      float r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = acc[j][m][i] + bias[m][i];
+      if (a.res_pre) IO::addq(qpre[m], r);
+      if (a.relu) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = fmaxf(r[i], 0.f);
+      }
+      if (a.res_post) IO::addq(qpost[m], r);
+      const uint32_t off = (uint32_t)(pout[j] * a.cout + (mt0 + m) * 16 + g * 4) * ES;
+      IO::stq(ro, valid[j] && cok[m] ? off : kOOB, r);
     }
   }
 }
@@ -314,6 +401,33 @@ __global__ __launch_bounds__(256) void conv2d_planes_kernel(const Conv2dArgs a) 
   }
 }
 
+// Any other plane-only layer (stride 2, transposed; no production layer): one thread per output
+// pixel of a phase, all (<= 16) output channels.
+template <typename T>
+__global__ __launch_bounds__(256) void conv2d_planes_generic_kernel(const Conv2dArgs a) {
+  const int Qtot = a.B * a.Hq * a.Wq;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const Conv2dPhase& ph = a.ph[blockIdx.y];
+  if (q >= Qtot) return;
+  const int qx = q % a.Wq, qy = (q / a.Wq) % a.Hq, b = q / (a.Wq * a.Hq);
+  float acc[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) acc[c] = a.bias[c];
+  const float* wg = a.wgeo + (size_t)ph.g_off * a.cout_pad;
+  for (int t = 0; t < ph.ntaps; ++t) {
+    const int iy = qy * a.in_stride + ph.tap[t][0], ix = qx * a.in_stride + ph.tap[t][1];
+    if ((unsigned)iy >= (unsigned)a.Hi || (unsigned)ix >= (unsigned)a.Wi) continue;
+    for (int g = 0; g < a.ngeo; ++g) {
+      const float v = a.geo[g][b * a.geo_bstride[g] + iy * a.Wi + ix];
+      const float* w = wg + (t * a.ngeo + g) * a.cout_pad;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) acc[c] += w[c] * v;
+    }
+  }
+  const int oy = qy * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
+  for (int c0 = 0; c0 < a.cout; c0 += 4) tail4<T>(a, b, oy, ox, c0, acc + c0);
+}
+
 // True when the layer is a plain (non-transposed) KxK conv with padding K/2 and dense row-major taps.
 bool planes_fast_ok(const Conv2dArgs& a, int K) {
   if (a.nphase != 1 || a.out_stride != 1 || a.in_stride != 1 || (long long)a.B * a.Ho * a.Wo >= (1LL << 31) || a.ph[0].ntaps != K * K || a.ph[0].g_off != 0) return false;
@@ -350,18 +464,38 @@ hipError_t launch_mt(hipStream_t s, const Conv2dArgs& a) {
   const long long Qtot = (long long)a.B * a.Hq * a.Wq;
   const int nq = (int)((Qtot + 4LL * kG2 * 16 - 1) / (4LL * kG2 * 16));
   dim3 grid((unsigned)(nq * a.nphase), (unsigned)((a.MTtot + MT - 1) / MT));
-  hipLaunchKernelGGL((conv2d_mfma_kernel<T, MT>), grid, dim3(256), 0, s, a, nq);
+  if (a.c1 > 0)
+    hipLaunchKernelGGL((conv2d_mfma_kernel<T, MT, true>), grid, dim3(256), 0, s, a, nq);
+  else
+    hipLaunchKernelGGL((conv2d_mfma_kernel<T, MT, false>), grid, dim3(256), 0, s, a, nq);
   return hipGetLastError();
 }
 
+template <typename T> struct T_is_bf16 { static constexpr bool value = false; };
+template <> struct T_is_bf16<bf16_t> { static constexpr bool value = true; };
+
 template <typename T>
 hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
+  // 32-bit indices / buffer offsets: every operand must stay below 2 GiB
+  const long long lim = 1LL << 31, es = sizeof(T);
+  const long long npix = (long long)a.B * a.Hi * a.Wi, nout = (long long)a.B * a.Ho * a.Wo * a.cout;
+  if (npix * (a.c0 > a.c1 ? a.c0 : a.c1) * es >= lim || nout * es >= lim || (long long)a.B * a.Hq * a.Wq >= lim)
+    return hipErrorInvalidValue;
+  for (int g = 0; g < a.ngeo; ++g)
+    if (((long long)(a.B - 1) * a.geo_bstride[g] + npix / a.B) * 4 >= lim) return hipErrorInvalidValue;
   if (a.c0 + a.c1 == 0) {
     const hipError_t e = launch_planes<T>(s, a);
     if (e != hipErrorNotSupported) return e;
+    if (a.cout > 16 || a.cout_pad < 16) return hipErrorInvalidValue;
+    dim3 grid((unsigned)((a.B * a.Hq * a.Wq + 255) / 256), a.nphase);
+    hipLaunchKernelGGL(conv2d_planes_generic_kernel<T>, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
   }
-  if (a.MTtot >= 4 && a.MTtot % 4 == 0) return launch_mt<T, 4>(s, a);
-  if (a.MTtot >= 2 && a.MTtot % 2 == 0) return launch_mt<T, 2>(s, a);
+  if (a.ngeo > 1) return hipErrorInvalidValue;  // the MFMA path takes at most one plane
+  // widest cout tile: each loaded input fragment feeds MT MFMAs
+  if (a.MTtot % 8 == 0 && T_is_bf16<T>::value) return launch_mt<T, 8>(s, a);
+  if (a.MTtot % 4 == 0) return launch_mt<T, 4>(s, a);
+  if (a.MTtot % 2 == 0) return launch_mt<T, 2>(s, a);
   return launch_mt<T, 1>(s, a);
 }
 

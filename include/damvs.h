@@ -153,7 +153,8 @@ typedef struct {
   int cin, cout;         /* channels of the weight */
   int c0, c0_at;         /* NHWC tensor input 0: channel count, first weight input channel it feeds */
   int c1, c1_at;         /* NHWC tensor input 1 (c1 = 0: none) */
-  int ngeo;              /* fp32 planar inputs (<= 4), each one weight input channel: */
+  int ngeo;              /* fp32 planar inputs, each one weight input channel: <= 4 when c0 = c1 = 0
+                            (then cout <= 16), else <= 1 (BasicBlockGeo's depth plane) */
   int geo_at[4];
   int relu;
 } damvs_conv2d_desc;
@@ -161,7 +162,8 @@ typedef struct {
 typedef struct damvs_conv2d damvs_conv2d;
 
 /* weight / bias: host fp32 (bias may be NULL). c0, c1 must be multiples of 8 (bf16) / 4 (f32);
- * the output is stored with cout rounded up to a multiple of 4 (extra channels are 0 + ReLU). */
+ * the output is stored with cout rounded up to a multiple of 4 (extra channels are 0 + ReLU).
+ * Every operand of a forward call must be smaller than 2 GiB (32-bit device offsets). */
 int damvs_conv2d_create(const damvs_conv2d_desc* desc, const float* weight, const float* bias, int dtype,
                         damvs_conv2d** out);
 int damvs_conv2d_destroy(damvs_conv2d* layer);
