@@ -59,4 +59,55 @@ __device__ __forceinline__ void store_vec(T* p, const float* v) {
   for (int i = 0; i < C; i += Stor<T>::E) Stor<T>::store16(p + i, v + i);
 }
 
+typedef unsigned int v4u32_t __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u32_t __attribute__((ext_vector_type(2)));
+
+// Buffer loads/stores: 32-bit byte offsets against a descriptor whose range check returns 0 for an
+// offset past the end (and drops such a store), so padding taps and tail pixels need no branch.
+constexpr uint32_t kOOB = 0x80000000u;  // every operand is < 2 GiB (checked by the launcher)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+template <typename T> struct BufIO;
+template <> struct BufIO<float> {
+  typedef float4 raw;   // one MFMA K fragment (4 channels x 4 K-steps)
+  typedef float4 quad;  // 4 output channels
+  __device__ __forceinline__ static raw frag(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  }
+  __device__ __forceinline__ static raw merge(const raw& x, const raw& y) {
+    return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+  }
+  __device__ __forceinline__ static quad ldq(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  }
+  __device__ __forceinline__ static void addq(const quad& q, float* v) { v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w; }
+  __device__ __forceinline__ static void stq(__amdgpu_buffer_rsrc_t r, uint32_t off, const float* v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, make_float4(v[0], v[1], v[2], v[3])), r, off, 0, 0);
+  }
+};
+template <> struct BufIO<bf16_t> {
+  typedef uint4 raw;
+  typedef uint2 quad;
+  __device__ __forceinline__ static raw frag(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  }
+  __device__ __forceinline__ static raw merge(const raw& x, const raw& y) {
+    return make_uint4(x.x | y.x, x.y | y.y, x.z | y.z, x.w | y.w);
+  }
+  __device__ __forceinline__ static quad ldq(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+  }
+  __device__ __forceinline__ static void addq(const quad& q, float* v) {
+    v[0] += __uint_as_float(q.x << 16); v[1] += __uint_as_float(q.x & 0xffff0000u);
+    v[2] += __uint_as_float(q.y << 16); v[3] += __uint_as_float(q.y & 0xffff0000u);
+  }
+  __device__ __forceinline__ static void stq(__amdgpu_buffer_rsrc_t r, uint32_t off, const float* v) {
+    const uint2 w = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                               (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, w), r, off, 0, 0);
+  }
+};
+
 }  // namespace damvs

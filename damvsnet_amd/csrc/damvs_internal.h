@@ -33,6 +33,26 @@ struct WarpArgs {
   float s1, t1, s2, t2;
 };
 
+// n / d for 0 <= n < 2^31 without a hardware divide: q = (umulhi(n, mul) + n) >> shift.
+struct FastDiv {
+  uint32_t mul, shift;
+  int d;
+};
+inline FastDiv make_fastdiv(int d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t sh = 0;
+  while (sh < 31 && (1u << sh) < (uint32_t)d) ++sh;
+  f.shift = sh;
+  f.mul = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << sh) - (uint64_t)d)) / (uint64_t)d + 1);
+  return f;
+}
+#ifdef __HIPCC__
+__device__ __forceinline__ int fdiv(const FastDiv& f, int n) {
+  return (int)((__umulhi((uint32_t)n, f.mul) + (uint32_t)n) >> f.shift);
+}
+#endif
+
 // ---------------------------------------------------------------- MFMA implicit-GEMM conv3d
 // A "phase" is one regular sub-convolution: for an iteration-grid point q,
 //   input  coord = q * in_stride + tap_offset        (zero outside the input)
@@ -57,6 +77,7 @@ struct ConvArgs {
   int in_stride, out_stride;
   int relu;
   int nphase;
+  FastDiv div_wq, div_hq, div_dq;  // set by launch_conv3d
   ConvPhase ph[kMaxPhases];
 };
 
@@ -70,26 +91,6 @@ struct Conv2dPhase {
   signed char wtap[25];    // weight tap index ky*k + kx
   signed char pad_[3];
 };
-
-// n / d for 0 <= n < 2^31 without a hardware divide: q = (umulhi(n, mul) + n) >> shift.
-struct FastDiv {
-  uint32_t mul, shift;
-  int d;
-};
-inline FastDiv make_fastdiv(int d) {
-  FastDiv f;
-  f.d = d;
-  uint32_t sh = 0;
-  while (sh < 31 && (1u << sh) < (uint32_t)d) ++sh;
-  f.shift = sh;
-  f.mul = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << sh) - (uint64_t)d)) / (uint64_t)d + 1);
-  return f;
-}
-#ifdef __HIPCC__
-__device__ __forceinline__ int fdiv(const FastDiv& f, int n) {
-  return (int)((__umulhi((uint32_t)n, f.mul) + (uint32_t)n) >> f.shift);
-}
-#endif
 
 struct Conv2dArgs {
   const void* in0;

@@ -74,11 +74,32 @@ __device__ __forceinline__ void load4<bf16_t>(const bf16_t* p, float* r) {
 
 constexpr int kGroups = 4;  // 16-voxel column groups per wave (64 output voxels per wave)
 
+// Epilogue for 4 channels: bias, ReLU, skip add (after the ReLU, models/module.py:537-539), store.
+template <typename T>
+__device__ __forceinline__ void finish4(const ConvArgs& a, __amdgpu_buffer_rsrc_t ro, __amdgpu_buffer_rsrc_t rr,
+                                        const typename BufIO<T>::quad& q, bool has_res, uint32_t off, bool ok,
+                                        const float* bias, const f32x4_t& acc) {
+  float r[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    r[i] = acc[i] + bias[i];
+    if (a.relu) r[i] = fmaxf(r[i], 0.f);
+  }
+  if (has_res) BufIO<T>::addq(q, r);
+  BufIO<T>::stq(ro, ok ? off : kOOB, r);
+  (void)rr;
+}
+
+// Global-gather implicit GEMM (strided convs, deconv phases, and any layer the LDS variant does not
+// take). 32-bit incremental indexing: no divisions in the K loop, magic-number division for the
+// voxel decomposition, range-checked buffer loads for the zero padding.
 template <typename T, int MT>
 __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int nqblk) {
-  typedef typename Frag<T>::raw raw;
+  typedef BufIO<T> IO;
+  typedef typename IO::raw raw;
   constexpr int E = Stor<T>::E;  // input channels per lane per K-chunk
   constexpr int KC = 4 * E;      // K per chunk (4 lane groups)
+  constexpr uint32_t ES = sizeof(T);
   // Logical block = (q-block, phase) with the phase fastest, dealt XCD-contiguously: the 8 output
   // parities of one deconv q-range run together on one XCD, so their interleaved half-line writes
   // (and the skip tensor's reads) merge in that L2.
@@ -96,21 +117,24 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int 
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
-  const long long Qtot = (long long)a.B * a.Dq * a.Hq * a.Wq;
-  const long long base = ((long long)qblk * 4 + wave) * (kGroups * 16);
+  const int Qtot = a.B * a.Dq * a.Hq * a.Wq;
+  const int base = (qblk * 4 + wave) * (kGroups * 16);
   if (base >= Qtot) return;
 
-  int vb[kGroups], vz[kGroups], vy[kGroups], vx[kGroups];
+  const int IS = a.in_stride, OS = a.out_stride;
+  int zs[kGroups], ys[kGroups], xs[kGroups], pin[kGroups], pout[kGroups];
   bool valid[kGroups];
 #pragma unroll
   for (int j = 0; j < kGroups; ++j) {
-    long long q = base + j * 16 + n;
+    int q = base + j * 16 + n;
     valid[j] = q < Qtot;
-    if (!valid[j]) q = 0;
-    vx[j] = (int)(q % a.Wq); q /= a.Wq;
-    vy[j] = (int)(q % a.Hq); q /= a.Hq;
-    vz[j] = (int)(q % a.Dq);
-    vb[j] = (int)(q / a.Dq);
+    q = valid[j] ? q : 0;
+    const int r1 = fdiv(a.div_wq, q), qx = q - r1 * a.Wq;
+    const int r2 = fdiv(a.div_hq, r1), qy = r1 - r2 * a.Hq;
+    const int b = fdiv(a.div_dq, r2), qz = r2 - b * a.Dq;
+    zs[j] = qz * IS; ys[j] = qy * IS; xs[j] = qx * IS;
+    pin[j] = ((b * a.Di + zs[j]) * a.Hi + ys[j]) * a.Wi + xs[j];
+    pout[j] = ((b * a.Do + qz * OS + ph.pd) * a.Ho + qy * OS + ph.ph) * a.Wo + qx * OS + ph.pw;
   }
 
   f32x4_t acc[kGroups][MT];
@@ -119,61 +143,60 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int 
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
+  const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * a.Cin * ES);
   const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + (size_t)ph.w_off * 64 + lane;
-  const int IS = a.in_stride;
-
+  const int HW = a.Hi * a.Wi;
+  int t = (g * E) / a.Cin, ci = g * E - t * a.Cin;  // this lane's (tap, channel) at k = s*KC + g*E
+  const int qt = KC / a.Cin, rc = KC - qt * a.Cin;
   for (int s = 0; s < ph.kchunks; ++s) {
-    const int k0 = s * KC + g * E;
-    const int t = k0 / a.Cin;
-    const int ci = k0 - t * a.Cin;
-    const bool tv = t < ph.ntaps;
-    const int code = s_tap[tv ? t : 0];
-    const int dz = (code & 0xff) - 8, dy = ((code >> 8) & 0xff) - 8, dx = ((code >> 16) & 0xff) - 8;
     raw wf[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * MT + m) * 64];
+    const bool tv = t < ph.ntaps;
+    const int code = s_tap[tv ? t : 0];
+    const int dz = (code & 0xff) - 8, dy = ((code >> 8) & 0xff) - 8, dx = ((code >> 16) & 0xff) - 8;
+    const int tapoff = dz * HW + dy * a.Wi + dx;
     raw xf[kGroups];
 #pragma unroll
     for (int j = 0; j < kGroups; ++j) {
-      const int iz = vz[j] * IS + dz, iy = vy[j] * IS + dy, ix = vx[j] * IS + dx;
+      const int iz = zs[j] + dz, iy = ys[j] + dy, ix = xs[j] + dx;
       const bool ok = valid[j] && tv && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
                       (unsigned)ix < (unsigned)a.Wi;
-      const size_t off = ok ? ((((size_t)vb[j] * a.Di + iz) * a.Hi + iy) * a.Wi + ix) * a.Cin + ci : 0;
-      raw v = *reinterpret_cast<const raw*>(in + off);  // unconditional load, select after
-      xf[j] = ok ? v : Frag<T>::zero();
+      xf[j] = IO::frag(r0, ok ? (uint32_t)((pin[j] + tapoff) * a.Cin + ci) * ES : kOOB);
     }
 #pragma unroll
     for (int j = 0; j < kGroups; ++j)
 #pragma unroll
       for (int m = 0; m < MT; ++m) Frag<T>::mma(wf[m], xf[j], acc[j][m]);
+    ci += rc;
+    t += qt;
+    if (ci >= a.Cin) { ci -= a.Cin; ++t; }
   }
 
-  T* __restrict__ out = reinterpret_cast<T*>(a.out);
-  const T* __restrict__ res = reinterpret_cast<const T*>(a.resid);
-  const int OS = a.out_stride;
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * ES;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.resid ? a.resid : a.out, a.resid ? nout : 0);
+  float bias[MT][4];
+  bool cok[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int co = m * 16 + g * 4;
+    cok[m] = co < a.Cout;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[m][i] = cok[m] ? a.bias[co + i] : 0.f;
+  }
 #pragma unroll
   for (int j = 0; j < kGroups; ++j) {
-    if (!valid[j]) continue;
-    const int oz = vz[j] * OS + ph.pd, oy = vy[j] * OS + ph.ph, ox = vx[j] * OS + ph.pw;
-    const size_t ob = ((((size_t)vb[j] * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * a.Cout;
+    typename IO::quad q[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const int co = m * 16 + g * 4;
-      if (co >= a.Cout) continue;
-      float r[4];
+      const uint32_t off = (uint32_t)(pout[j] * a.Cout + m * 16 + g * 4) * ES;
+      if (a.resid) q[m] = IO::ldq(rr, valid[j] && cok[m] ? off : kOOB);
+    }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        r[i] = acc[j][m][i] + a.bias[co + i];
-        if (a.relu) r[i] = fmaxf(r[i], 0.f);
-      }
-      if (res) {
-        float q[4];
-        load4<T>(res + ob + co, q);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] += q[i];
-      }
-      store4<T>(out + ob + co, r);
+    for (int m = 0; m < MT; ++m) {
+      const uint32_t off = (uint32_t)(pout[j] * a.Cout + m * 16 + g * 4) * ES;
+      finish4<T>(a, ro, rr, q[m], a.resid != nullptr, off, valid[j] && cok[m], bias[m], acc[j][m]);
     }
   }
 }
@@ -214,15 +237,15 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
   const int b = tt / tiles_z;
   const int z0 = tz * LTD, y0 = ty * LTH, x0 = tx * LTW;
 
-  const T* __restrict__ in = reinterpret_cast<const T*>(a.in) + (size_t)b * a.Di * a.Hi * a.Wi * CIN;
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * sizeof(T));
+  const int vin0 = b * a.Di * a.Hi * a.Wi;
   for (int c = threadIdx.x; c < TILE_CHUNKS; c += 256) {
     const int vox = c / CH, part = c - vox * CH;
     const int hx = vox % LHW, hy = (vox / LHW) % LHH, hz = vox / (LHW * LHH);
     const int iz = z0 - 1 + hz, iy = y0 - 1 + hy, ix = x0 - 1 + hx;
     const bool ok = (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
-    const size_t off = ok ? (((size_t)iz * a.Hi + iy) * a.Wi + ix) * CIN + part * E : 0;
-    const raw v = *reinterpret_cast<const raw*>(in + off);
-    tile[c] = ok ? v : Frag<T>::zero();
+    const uint32_t off = (uint32_t)(((vin0 + (iz * a.Hi + iy) * a.Wi + ix) * CIN + part * E) * sizeof(T));
+    tile[c] = BufIO<T>::frag(rin, ok ? off : kOOB);
   }
   __syncthreads();
 
@@ -257,31 +280,35 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
     }
   }
 
-  T* __restrict__ out = reinterpret_cast<T*>(a.out);
-  const T* __restrict__ res = reinterpret_cast<const T*>(a.resid);
+  constexpr uint32_t ES = sizeof(T);
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * ES;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.resid ? a.resid : a.out, a.resid ? nout : 0);
+  float bias[MT][4];
+  bool cok[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int co = m * 16 + g * 4;
+    cok[m] = co < a.Cout;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[m][i] = cok[m] ? a.bias[co + i] : 0.f;
+  }
 #pragma unroll
   for (int j = 0; j < kLdsGroups; ++j) {
     const int j2 = wave * kLdsGroups + j;
     const int oz = z0 + j2 / LTH, oy = y0 + j2 % LTH, ox = x0 + n;
-    if (oz >= a.Do || oy >= a.Ho || ox >= a.Wo) continue;
-    const size_t ob = ((((size_t)b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * a.Cout;
+    const bool vok = oz < a.Do && oy < a.Ho && ox < a.Wo;
+    const int pout = ((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox;
+    typename BufIO<T>::quad q[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const int co = m * 16 + g * 4;
-      if (co >= a.Cout) continue;
-      float r[4];
+      const uint32_t off = (uint32_t)(pout * a.Cout + m * 16 + g * 4) * ES;
+      if (a.resid) q[m] = BufIO<T>::ldq(rr, vok && cok[m] ? off : kOOB);
+    }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        r[i] = acc[j][m][i] + a.bias[co + i];
-        if (a.relu) r[i] = fmaxf(r[i], 0.f);
-      }
-      if (res) {
-        float q[4];
-        load4<T>(res + ob + co, q);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] += q[i];
-      }
-      store4<T>(out + ob + co, r);
+    for (int m = 0; m < MT; ++m) {
+      const uint32_t off = (uint32_t)(pout * a.Cout + m * 16 + g * 4) * ES;
+      finish4<T>(a, ro, rr, q[m], a.resid != nullptr, off, vok && cok[m], bias[m], acc[j][m]);
     }
   }
 }
@@ -331,7 +358,27 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
 
 }  // namespace
 
-hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a) {
+hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a0) {
+  ConvArgs a = a0;
+  a.div_wq = make_fastdiv(a.Wq);
+  a.div_hq = make_fastdiv(a.Hq);
+  a.div_dq = make_fastdiv(a.Dq);
+  // 32-bit device offsets: operands of 2 GiB or more run one batch element per launch
+  const long long es = store == ST_BF16 ? 2 : 4;
+  const long long in_b = (long long)a.Di * a.Hi * a.Wi * a.Cin * es, out_b = (long long)a.Do * a.Ho * a.Wo * a.Cout * es;
+  if (a.B > 1 && (in_b * a.B >= (1LL << 31) || out_b * a.B >= (1LL << 31))) {
+    for (int b = 0; b < a.B; ++b) {
+      ConvArgs a1 = a0;
+      a1.B = 1;
+      a1.in = static_cast<const char*>(a0.in) + b * in_b;
+      a1.out = static_cast<char*>(a0.out) + b * out_b;
+      a1.resid = a0.resid ? static_cast<const char*>(a0.resid) + b * out_b : nullptr;
+      const hipError_t e = launch_conv3d(s, store, a1);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  if (in_b >= (1LL << 31) || out_b >= (1LL << 31)) return hipErrorInvalidValue;
   if (!conv_lds_disabled()) {
     hipError_t e = store == ST_BF16 ? launch_lds<bf16_t>(s, a) : launch_lds<float>(s, a);
     if (e != hipErrorNotSupported) return e;

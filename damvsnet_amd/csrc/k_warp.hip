@@ -10,9 +10,10 @@
 // the running aggregate in registers, and writes the C-vector of the aggregated volume once
 // (NDHWC, 16-byte stores, consecutive threads -> consecutive voxels).
 //
-// Warp arithmetic follows models/module.py:318-329 exactly: q = (R [x y 1]^T) d + t,
-// u = q_x / q_z, g = u / ((W-1)/2) - 1 (align-corners style normalisation), then grid_sample's
-// align_corners=False unnormalisation ix = ((g + 1) W - 1) / 2, bilinear, zero padding.
+// Warp arithmetic follows models/module.py:318-329: q = (R [x y 1]^T) d + t, u = q_x / q_z,
+// g = u / ((W-1)/2) - 1 (align-corners style normalisation), then grid_sample's
+// align_corners=False unnormalisation ix = ((g + 1) W - 1) / 2, bilinear, zero padding; the
+// normalise/unnormalise pair is folded algebraically (ix = u W/(W-1) - 1/2).
 #include "damvs_device.h"
 
 namespace damvs {
@@ -74,7 +75,7 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
   if (p >= hw) return;
   const int y = p / a.w, x = p - y * a.w;
   const float fx = (float)x, fy = (float)y;
-  const float nx = (float)(a.w - 1) * 0.5f, ny = (float)(a.h - 1) * 0.5f;
+  const float kx = (float)a.w / (float)(a.w - 1), ky = (float)a.h / (float)(a.h - 1);
 
   float ref[C];
   if (MODE != AGG_WARP_ONLY) {
@@ -85,6 +86,7 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
       Stor<T>::load16(BLK ? f0 + ((size_t)q * hw + p) * E : f0 + (size_t)p * C + q * E, ref + q * E);
   }
 
+  const float inv_n = 1.f / (float)a.N, inv_n1 = 1.f / (float)(a.N - 1);  // exact for N = 5 (the default)
   const int d0 = dc * dchunk, d1 = min(a.D, d0 + dchunk);
   for (int d = d0; d < d1; ++d) {
     const size_t vox = ((size_t)b * a.D + d) * hw + p;
@@ -101,9 +103,11 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
       const float ry = m[3] * fx + m[4] * fy + m[5];
       const float rz = m[6] * fx + m[7] * fy + m[8];
       const float qx = rx * hyp + m[9], qy = ry * hyp + m[10], qz = rz * hyp + m[11];
-      const float gx = (qx / qz) / nx - 1.f, gy = (qy / qz) / ny - 1.f;
-      const float ix = ((gx + 1.f) * (float)a.w - 1.f) * 0.5f;
-      const float iy = ((gy + 1.f) * (float)a.h - 1.f) * 0.5f;
+      // g = (q/qz) / ((W-1)/2) - 1 and ix = ((g + 1) W - 1) / 2 fold to ix = (q/qz) W/(W-1) - 1/2:
+      // one reciprocal instead of four IEEE divisions (coordinates agree to ~1 ulp)
+      const float iz = __builtin_amdgcn_rcpf(qz);
+      const float ix = qx * iz * kx - 0.5f;
+      const float iy = qy * iz * ky - 0.5f;
       float s[C];
       sample_bilinear<T, C, BLK>(reinterpret_cast<const T*>(a.feats[v]) + (size_t)b * hw * C, a.h, a.w, ix, iy, s);
       if (MODE == AGG_WARP_ONLY) {
@@ -128,16 +132,14 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
     }
     float o[C];
     if (MODE == AGG_VARIANCE) {
-      const float n = (float)a.N;
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        const float mean = acc[c] / n;
-        o[c] = sq[c] / n - mean * mean;
+        const float mean = acc[c] * inv_n;
+        o[c] = sq[c] * inv_n - mean * mean;
       }
     } else if (MODE == AGG_ADAPTIVE) {
-      const float n1 = (float)(a.N - 1);
 #pragma unroll
-      for (int c = 0; c < C; ++c) o[c] = acc[c] / n1;
+      for (int c = 0; c < C; ++c) o[c] = acc[c] * inv_n1;
     } else {
 #pragma unroll
       for (int c = 0; c < C; ++c) o[c] = acc[c];
