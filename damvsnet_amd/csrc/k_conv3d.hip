@@ -212,6 +212,12 @@ constexpr int LTD = 4, LTH = 8, LTW = 16;
 constexpr int LHD = LTD + 2, LHH = LTH + 2, LHW = LTW + 2;
 constexpr int kLdsGroups = 8;  // per wave: 4 waves x 8 groups x 16 voxels = 512 = LTD*LTH*LTW
 
+// chunk offset of tap t (= (kz, ky, kx) row-major) inside the halo tile, in 16-byte chunks
+template <int CH>
+__device__ constexpr int halo_toff(int t) {
+  return t >= 27 ? halo_toff<CH>(26) : (((t / 9) * LHH + (t / 3) % 3) * LHW + t % 3) * CH;
+}
+
 template <typename T, int CIN>
 constexpr size_t lds_tile_bytes() { return (size_t)LHD * LHH * LHW * CIN * sizeof(T); }
 
@@ -223,7 +229,9 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
   constexpr int KC = 4 * E;
   constexpr int CH = CIN / E;                              // 16-byte chunks per voxel
   constexpr int KCHUNKS = (27 * CIN + KC - 1) / KC;
-  constexpr int TILE_CHUNKS = LHD * LHH * LHW * CH;
+  constexpr int ROW = LHW * CH;                            // 16-byte chunks per halo row
+  constexpr int TILE_CHUNKS = LHD * LHH * ROW;
+  static_assert(kLdsGroups == LTH, "a wave owns one z-slice of the tile");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   raw* tile = reinterpret_cast<raw*>(smem);
 
@@ -237,14 +245,15 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
   const int b = tt / tiles_z;
   const int z0 = tz * LTD, y0 = ty * LTH, x0 = tx * LTW;
 
+  // halo fill: chunk c = (row, col) with row = (hz, hy); one row is LHW contiguous voxels in HBM
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * sizeof(T));
   const int vin0 = b * a.Di * a.Hi * a.Wi;
   for (int c = threadIdx.x; c < TILE_CHUNKS; c += 256) {
-    const int vox = c / CH, part = c - vox * CH;
-    const int hx = vox % LHW, hy = (vox / LHW) % LHH, hz = vox / (LHW * LHH);
-    const int iz = z0 - 1 + hz, iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+    const int row = c / ROW, col = c - row * ROW;
+    const int hz = row / LHH, hy = row - hz * LHH;
+    const int iz = z0 - 1 + hz, iy = y0 - 1 + hy, ix = x0 - 1 + col / CH;
     const bool ok = (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
-    const uint32_t off = (uint32_t)(((vin0 + (iz * a.Hi + iy) * a.Wi + ix) * CIN + part * E) * sizeof(T));
+    const uint32_t off = (uint32_t)(((vin0 + (iz * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16);
     tile[c] = BufIO<T>::frag(rin, ok ? off : kOOB);
   }
   __syncthreads();
@@ -257,26 +266,62 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
+  // wave = output z-slice, group j = output row y, lane column n = output x; group j's chunk is the
+  // lane base + a compile-time offset j * ROW (folds into the ds_read immediate)
+  const raw* tl = tile + (wave * LHH * LHW + n) * CH;
   const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + lane;
-#pragma unroll 2
-  for (int s = 0; s < KCHUNKS; ++s) {
-    const int k0 = s * KC + g * E;
-    const int tap = k0 / CIN, ci = k0 - tap * CIN;
-    const bool tv = tap < 27;
-    const int dz = tap / 9, dy = (tap / 3) % 3, dx = tap % 3;
-    raw wf[MT];
+  // K index s*KC + g*E = tap*CIN + ci with tap = s*KC/CIN + (g*E)/CIN (KC is a multiple of CIN or
+  // CIN a multiple of KC): with the loop fully unrolled, a lane's tap offset is one of <= 4
+  // compile-time constants per chunk, picked by its lane group - no LDS table, no divisions.
+  static_assert(KC % CIN == 0 || CIN % KC == 0, "chunking");
+  const int gi = (g * E) / CIN;          // tap sub-index of this lane group (KC > CIN)
+  const int gc = (g * E) % CIN / E;      // 16-byte channel chunk within the voxel
+  auto frag_src = [&](int s) -> const raw* {
+    const int kt = (s * KC) / CIN;       // first tap of chunk s (compile time after unrolling)
+    const int kc = ((s * KC) % CIN) / E; // channel chunk offset of chunk s
+    int off = halo_toff<CH>(kt);
+    if (KC > CIN) {
+      off = gi == 1 ? halo_toff<CH>(kt + 1) : off;
+      off = gi == 2 ? halo_toff<CH>(kt + 2) : off;
+      off = gi == 3 ? halo_toff<CH>(kt + 3) : off;
+    }
+    return tl + off + kc + gc;
+  };
+  raw xa[kLdsGroups], wa[MT];
+  auto fetch = [&](int s, raw* xf, raw* wf) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * MT + m) * 64];
-    // group j of this wave = output row (z, y) = (j2 / LTH, j2 % LTH), voxel x = n
-    const int base = ((dz * LHH + dy) * LHW + n + dx) * CH + ci / E;
+    const raw* src = frag_src(s);
 #pragma unroll
-    for (int j = 0; j < kLdsGroups; ++j) {
-      const int j2 = wave * kLdsGroups + j;
-      const int zz = j2 / LTH, yy = j2 % LTH;
-      raw xf = tile[base + (zz * LHH + yy) * LHW * CH];
-      if (!tv) xf = Frag<T>::zero();
+    for (int j = 0; j < kLdsGroups; ++j) xf[j] = src[j * ROW];
+  };
+  if constexpr (CIN >= 32 && MT == 1) {
+    // 27 chunks at 2 blocks per CU: the pipelined schedule's extra registers cost more than it hides
 #pragma unroll
-      for (int m = 0; m < MT; ++m) Frag<T>::mma(wf[m], xf, acc[j][m]);
+    for (int s = 0; s < KCHUNKS; ++s) {
+      fetch(s, xa, wa);
+#pragma unroll
+      for (int j = 0; j < kLdsGroups; ++j) Frag<T>::mma(wa[0], xa[j], acc[j][0]);
+    }
+  } else {
+    // software-pipelined one chunk ahead: chunk s+1's fragments are read while chunk s's MFMAs run
+    fetch(0, xa, wa);
+#pragma unroll
+    for (int s = 0; s < KCHUNKS; ++s) {
+      raw xb[kLdsGroups], wb[MT];
+      if (s + 1 < KCHUNKS) fetch(s + 1, xb, wb);
+#pragma unroll
+      for (int j = 0; j < kLdsGroups; ++j)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) Frag<T>::mma(wa[m], xa[j], acc[j][m]);
+      if (s + 1 < KCHUNKS) {
+        __builtin_amdgcn_sched_group_barrier(0x100, kLdsGroups, 0);       // DS reads
+        __builtin_amdgcn_sched_group_barrier(0x008, kLdsGroups * MT, 0);  // MFMA
+#pragma unroll
+        for (int j = 0; j < kLdsGroups; ++j) xa[j] = xb[j];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) wa[m] = wb[m];
+      }
     }
   }
 
@@ -295,8 +340,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
   }
 #pragma unroll
   for (int j = 0; j < kLdsGroups; ++j) {
-    const int j2 = wave * kLdsGroups + j;
-    const int oz = z0 + j2 / LTH, oy = y0 + j2 % LTH, ox = x0 + n;
+    const int oz = z0 + wave, oy = y0 + j, ox = x0 + n;
     const bool vok = oz < a.Do && oy < a.Ho && ox < a.Wo;
     const int pout = ((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox;
     typename BufIO<T>::quad q[MT];

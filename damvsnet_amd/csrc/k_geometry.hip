@@ -94,7 +94,7 @@ __device__ __forceinline__ void src_index(float scale, int dst, int in_size, int
 }
 
 struct FullResPoint {
-  float cur, var, low, step, mx, sum;
+  float cur, var, low, step, mx, rsum, k3;
 };
 
 __device__ __forceinline__ float bilerp(const float* m, int wp, int y0, int y1, int x0, int x1, float ly0, float ly1,
@@ -131,13 +131,12 @@ __global__ void hyp_refine_kernel(int B, int D, int H, int W, int scale, const f
     q.var = bilerp(mv, wp, y0, y1, x0, x1, ly0, ly1, lx0, lx1);
     q.low = -fminf(q.cur, q.var);
     q.step = (q.var - q.low) / rden;
-    float den = q.var + eps;
-    float mx = -INFINITY;
-    for (int i = 0; i < D; ++i) mx = fmaxf(mx, 3.f * (q.low + q.step * (float)i) / den);
+    // softmax logits x_i = 3 (low + step i) / (var + eps) are linear in i: the max is an endpoint
+    q.k3 = 3.f / (q.var + eps);
+    q.mx = fmaxf(q.low * q.k3, (q.low + q.step * (float)(D - 1)) * q.k3);
     float s = 0.f;
-    for (int i = 0; i < D; ++i) s += expf(3.f * (q.low + q.step * (float)i) / den - mx);
-    q.mx = mx;
-    q.sum = s;
+    for (int i = 0; i < D; ++i) s += __expf((q.low + q.step * (float)i) * q.k3 - q.mx);
+    q.rsum = 1.f / s;
     P[k] = q;
   }
   float* o = out + (size_t)b * D * h * w + p;
@@ -147,8 +146,7 @@ __global__ void hyp_refine_kernel(int B, int D, int H, int W, int scale, const f
     for (int k = 0; k < 4; ++k) {
       if (k >= n) break;
       const FullResPoint& q = P[k];
-      float den = q.var + eps;
-      float off = expf(3.f * (q.low + q.step * (float)i) / den - q.mx) / q.sum;
+      const float off = __expf((q.low + q.step * (float)i) * q.k3 - q.mx) * q.rsum;
       v[k] = (q.cur + q.low + q.step * (float)i + eps) + off * q.step;
     }
     float r = (scale == 1) ? v[0] : 0.5f * (0.5f * v[0] + 0.5f * v[1]) + 0.5f * (0.5f * v[2] + 0.5f * v[3]);
