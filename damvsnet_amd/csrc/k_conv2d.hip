@@ -442,10 +442,13 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
     return hipGetLastError();
   }
   if (a.ngeo > 1) return hipErrorInvalidValue;  // the MFMA path takes at most one plane
-  // widest cout tile: each loaded input fragment feeds MT MFMAs
-  if (a.MTtot % 8 == 0 && T_is_bf16<T>::value) return launch_mt<T, 8>(s, a);
-  if (a.MTtot % 4 == 0) return launch_mt<T, 4>(s, a);
-  if (a.MTtot % 2 == 0) return launch_mt<T, 2>(s, a);
+  // Widest cout tile (each loaded input fragment feeds MT MFMAs) that still puts about one wave on
+  // every SIMD: the low-resolution GeoFeatureFusion layers have few pixels and many channels.
+  const long long tiles = ((long long)a.B * a.Hq * a.Wq + 63) / 64 * a.nphase;
+  const long long want = 900;
+  if (T_is_bf16<T>::value && a.MTtot % 8 == 0 && tiles * (a.MTtot / 8) >= want) return launch_mt<T, 8>(s, a);
+  if (a.MTtot % 4 == 0 && tiles * (a.MTtot / 4) >= want) return launch_mt<T, 4>(s, a);
+  if (a.MTtot % 2 == 0 && tiles * (a.MTtot / 2) >= want) return launch_mt<T, 2>(s, a);
   return launch_mt<T, 1>(s, a);
 }
 
