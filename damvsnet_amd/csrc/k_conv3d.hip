@@ -295,7 +295,42 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
 #pragma unroll
     for (int j = 0; j < kLdsGroups; ++j) xf[j] = src[j * ROW];
   };
-  if constexpr (CIN >= 32 && MT == 1) {
+  // K = 9 tap rows (kz, ky) x 3 taps (kx) x CIN. Long K loops (>= 54 chunks) iterate over the tap
+  // rows at run time with the row body unrolled: a fully unrolled 108-chunk f32 loop takes the
+  // compiler tens of minutes and buys nothing over a 12-chunk unrolled body.
+  constexpr int CPT = CIN >= KC ? CIN / KC : 1;  // chunks per tap
+  constexpr int RCH = 3 * CPT;                   // chunks per tap row
+  if constexpr (CIN >= KC && KCHUNKS >= 54) {
+    auto fetch_row = [&](int r, int s, raw* xf, raw* wf) {
+      const int kz = r / 3, ky = r - kz * 3;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)((r * RCH + s) * MT + m) * 64];
+      const raw* src = tl + ((kz * LHH + ky) * LHW + s / CPT) * CH + (s % CPT) * (KC / E) + gc;
+#pragma unroll
+      for (int j = 0; j < kLdsGroups; ++j) xf[j] = src[j * ROW];
+    };
+    fetch_row(0, 0, xa, wa);
+#pragma unroll 1
+    for (int r = 0; r < 9; ++r) {
+#pragma unroll
+      for (int s = 0; s < RCH; ++s) {
+        raw xb[kLdsGroups], wb[MT];
+        const bool more = s + 1 < RCH || r + 1 < 9;
+        if (s + 1 < RCH) fetch_row(r, s + 1, xb, wb);
+        else if (r + 1 < 9) fetch_row(r + 1, 0, xb, wb);
+#pragma unroll
+        for (int j = 0; j < kLdsGroups; ++j)
+#pragma unroll
+          for (int m = 0; m < MT; ++m) Frag<T>::mma(wa[m], xa[j], acc[j][m]);
+        if (more) {
+#pragma unroll
+          for (int j = 0; j < kLdsGroups; ++j) xa[j] = xb[j];
+#pragma unroll
+          for (int m = 0; m < MT; ++m) wa[m] = wb[m];
+        }
+      }
+    }
+  } else if constexpr (CIN >= 32 && MT == 1) {
     // 27 chunks at 2 blocks per CU: the pipelined schedule's extra registers cost more than it hides
 #pragma unroll
     for (int s = 0; s < KCHUNKS; ++s) {
