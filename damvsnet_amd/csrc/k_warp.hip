@@ -14,6 +14,8 @@
 // g = u / ((W-1)/2) - 1 (align-corners style normalisation), then grid_sample's
 // align_corners=False unnormalisation ix = ((g + 1) W - 1) / 2, bilinear, zero padding; the
 // normalise/unnormalise pair is folded algebraically (ix = u W/(W-1) - 1/2).
+#include <cstdlib>
+
 #include "damvs_device.h"
 
 namespace damvs {
@@ -61,7 +63,7 @@ __device__ __forceinline__ void sample_bilinear(const T* __restrict__ src, int h
 // inside a narrow band of each source image; blocks are dealt so that each XCD gets a contiguous
 // range of (pixel-chunk, depth-chunk) work and its L2 holds that band (the naive (pixels, D) grid
 // spreads every depth slice over all 8 XCDs and serves the gathers from the Infinity Cache).
-template <typename T, int C, int MODE, bool BLK>
+template <typename T, int C, int MODE, bool BLK, int NVC>
 __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, int npix_blocks, int dchunk,
                                                              int ndchunks) {
   const int hw = a.h * a.w;
@@ -71,6 +73,12 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
   const int dc = L % ndchunks; L /= ndchunks;
   const int pb = L % npix_blocks;
   const int b = L / npix_blocks;
+  // this batch element's [N-1][12] source cameras in LDS: the per-plane reads below are broadcast
+  // ds_reads instead of 12 vector-memory loads per view per plane through the (gather-bound) TA
+  __shared__ __attribute__((aligned(16))) float s_rtf[(kMaxViews - 1) * 12];
+  if (threadIdx.x < (a.N - 1) * 12) s_rtf[threadIdx.x] = a.rt[(size_t)b * (a.N - 1) * 12 + threadIdx.x];
+  __syncthreads();
+  const float4* s_rt = reinterpret_cast<const float4*>(s_rtf);
   const int p = pb * 256 + threadIdx.x;
   if (p >= hw) return;
   const int y = p / a.w, x = p - y * a.w;
@@ -97,8 +105,13 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
       acc[c] = (MODE == AGG_VARIANCE) ? ref[c] : 0.f;
       sq[c] = (MODE == AGG_VARIANCE) ? ref[c] * ref[c] : 0.f;
     }
-    for (int v = 1; v < a.N; ++v) {
-      const float* m = a.rt + ((size_t)b * (a.N - 1) + (v - 1)) * 12;
+    // NVC > 0: the source-view count is a compile-time constant and the view loop unrolls, so the
+    // gathers of several views are in flight together
+    const int nviews = NVC > 0 ? NVC + 1 : a.N;
+#pragma unroll
+    for (int v = 1; v < nviews; ++v) {
+      const float4 m0 = s_rt[(v - 1) * 3], m1 = s_rt[(v - 1) * 3 + 1], m2 = s_rt[(v - 1) * 3 + 2];
+      const float m[12] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w, m2.x, m2.y, m2.z, m2.w};
       const float rx = m[0] * fx + m[1] * fy + m[2];
       const float ry = m[3] * fx + m[4] * fy + m[5];
       const float rz = m[6] * fx + m[7] * fy + m[8];
@@ -148,18 +161,30 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
   }
 }
 
+template <typename T, int C, int MODE, bool BLK>
+void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, int ndc) {
+  if (a.N == 5 && C <= 16)  // C = 32: the unrolled views cost more registers than they hide
+    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 4>), grid, dim3(256), 0, s, a, npb, dchunk, ndc);
+  else
+    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 0>), grid, dim3(256), 0, s, a, npb, dchunk, ndc);
+}
+
 template <typename T, int MODE, bool BLK>
 hipError_t launch_c(hipStream_t s, const WarpArgs& a) {
   const int npb = (a.h * a.w + 255) / 256;
   // depth chunk: as long as possible (locality) while keeping >= ~4 blocks per CU in flight
   int dchunk = a.D;
-  while (dchunk > 2 && (long long)npb * a.B * ((a.D + dchunk - 1) / dchunk) < 2048) dchunk = (dchunk + 1) / 2;
+  static const long long minblk = [] {
+    const char* e = getenv("DAMVS_WARP_MINBLK");
+    return e ? atoll(e) : 2048LL;
+  }();
+  while (dchunk > 2 && (long long)npb * a.B * ((a.D + dchunk - 1) / dchunk) < minblk) dchunk = (dchunk + 1) / 2;
   const int ndc = (a.D + dchunk - 1) / dchunk;
   dim3 grid((unsigned)(npb * ndc * a.B));
   switch (a.C) {
-    case 8: hipLaunchKernelGGL((warp_aggregate_kernel<T, 8, MODE, BLK>), grid, dim3(256), 0, s, a, npb, dchunk, ndc); break;
-    case 16: hipLaunchKernelGGL((warp_aggregate_kernel<T, 16, MODE, BLK>), grid, dim3(256), 0, s, a, npb, dchunk, ndc); break;
-    case 32: hipLaunchKernelGGL((warp_aggregate_kernel<T, 32, MODE, BLK>), grid, dim3(256), 0, s, a, npb, dchunk, ndc); break;
+    case 8: launch_k<T, 8, MODE, BLK>(s, a, grid, npb, dchunk, ndc); break;
+    case 16: launch_k<T, 16, MODE, BLK>(s, a, grid, npb, dchunk, ndc); break;
+    case 32: launch_k<T, 32, MODE, BLK>(s, a, grid, npb, dchunk, ndc); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

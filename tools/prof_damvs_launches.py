@@ -9,11 +9,18 @@ ends = reg[2::3]
 step = int(sys.argv[2]) if len(sys.argv) > 2 else len(ends) - 1
 sel = rows[ends[step - 1] + 1:ends[step] + 1]
 tot = 0.0
+
+
+def short(n):
+    n = n.replace("(anonymous namespace)::", "")
+    return n.split("(")[0].replace("void ", "").replace("damvs::", "").replace(" ", "")[:60]
+
+
 for r in sel:
     n = r["Kernel_Name"]
     if "damvs" in n:
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         tot += d
         print("%8.1f us  grid %9s x %2s  vgpr %3s lds %6s  %s" % (d, r["Grid_Size_X"], r["Grid_Size_Y"], r["VGPR_Count"],
-                                                               r["LDS_Block_Size"], n.split("(")[0].split("::")[-1][:60]))
+                                                               r["LDS_Block_Size"], short(n)))
 print("damvs total %.1f us" % tot)
