@@ -108,7 +108,8 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
     // NVC > 0: the source-view count is a compile-time constant and the view loop unrolls, so the
     // gathers of several views are in flight together
     const int nviews = NVC > 0 ? NVC + 1 : a.N;
-#pragma unroll(NVC > 0 ? NVC : 1)
+    constexpr int kUnrollV = NVC > 0 ? NVC : 1;
+#pragma unroll kUnrollV
     for (int v = 1; v < nviews; ++v) {
       const float4 m0 = s_rt[(v - 1) * 3], m1 = s_rt[(v - 1) * 3 + 1], m2 = s_rt[(v - 1) * 3 + 2];
       const float m[12] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w, m2.x, m2.y, m2.z, m2.w};
