@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the library load: shared HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdamvs.so")
+LIB_PATH = os.environ.get("DAMVS_LIB") or os.path.join(_HERE, "libdamvs.so")  # DAMVS_LIB: A/B builds in tools
 
 DAMVS_F32, DAMVS_BF16 = 0, 1
 DAMVS_AGG_ADAPTIVE, DAMVS_AGG_VARIANCE = 0, 1

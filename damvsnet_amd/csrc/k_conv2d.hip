@@ -158,8 +158,8 @@ __global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, in
     const __amdgpu_buffer_rsrc_t r1 = make_rsrc(TWO ? a.in1 : a.in0, TWO ? (long long)npix * a.c1 * ES : 0);
     int t = (g * E) / ctot, ci = g * E - t * ctot;  // this lane's (tap, channel) at k = s*KC + g*E
     const int qt = KC / ctot, rc = KC - qt * ctot;
-    for (int s = 0; s < nk; ++s) {
-      raw wf[MT];
+    // fragments of chunk s (then advances the lane's (tap, channel) to chunk s+1)
+    auto fetch = [&](int s, raw* wf, raw* xf) {
 #pragma unroll
       for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * a.MTtot + m) * 64];
       const bool tv = t < ph.ntaps;
@@ -168,7 +168,6 @@ __global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, in
       const int tapoff = dy * a.Wi + dx;
       const bool second = TWO && ci >= a.c0;
       const int cs = second ? a.c1 : a.c0, cl = second ? ci - a.c0 : ci;
-      raw xf[kG2];
 #pragma unroll
       for (int j = 0; j < kG2; ++j) {
         const int iy = ys[j] + dy, ix = xs[j] + dx;
@@ -179,13 +178,39 @@ __global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, in
         else
           xf[j] = IO::frag(r0, ok ? off : kOOB);
       }
-#pragma unroll
-      for (int j = 0; j < kG2; ++j)
-#pragma unroll
-        for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf[j], acc[j][m]);
       ci += rc;
       t += qt;
       if (ci >= ctot) { ci -= ctot; ++t; }
+    };
+    // software-pipelined one chunk ahead: chunk s+1's loads are in flight during chunk s's MFMAs
+    // (the deep low-resolution layers run at 1-2 waves per SIMD, too few to hide load latency)
+    raw wf[MT], xf[kG2];
+    if constexpr (MT <= 2) {  // thin layers: occupancy hides the latency, the registers buy nothing
+#pragma unroll 1
+      for (int s = 0; s < nk; ++s) {
+        fetch(s, wf, xf);
+#pragma unroll
+        for (int j = 0; j < kG2; ++j)
+#pragma unroll
+          for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf[j], acc[j][m]);
+      }
+    } else {
+      fetch(0, wf, xf);
+      for (int s = 0; s < nk; ++s) {
+        raw wn[MT], xn[kG2];
+        const bool more = s + 1 < nk;
+        if (more) fetch(s + 1, wn, xn);
+#pragma unroll
+        for (int j = 0; j < kG2; ++j)
+#pragma unroll
+          for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf[j], acc[j][m]);
+        if (more) {
+#pragma unroll
+          for (int m = 0; m < MT; ++m) wf[m] = wn[m];
+#pragma unroll
+          for (int j = 0; j < kG2; ++j) xf[j] = xn[j];
+        }
+      }
     }
   }
 

@@ -80,6 +80,38 @@ def planes(t):
     return [(t[:, c], C * H * W) for c in range(C)]
 
 
+def fpn_top_layers(inner2, out3, dtype):
+    """FeatureNet's last FPN level, out3(up2(f) + inner2(c0)) (models/module.py:455-459: nearest x2
+    upsample, 1x1 conv with bias, 3x3 conv without bias, no BN/ReLU), re-associated so the
+    32-channel full-resolution sum is never written:
+
+      out3(up2(f))        = ConvTranspose2d(k4, s2, p1) of f whose taps are sums of out3's taps
+                            (per axis, transposed tap a in {0..3} collects 3x3 taps S(a) =
+                            {2}, {1,2}, {0,1}, {0}: nearest upsampling merges them pairwise);
+      out3(inner2(c0))    = 3x3 conv of c0 with weights out3 . inner2 (8 -> 8);
+      out3(inner2's bias) = a plane of ones as one extra input channel with weights out3 . bias
+                            (zero padding keeps the border exact).
+
+    Returns (transposed layer on f, 3x3 layer on c0 + ones plane) as HipConv2d; the second takes
+    the first's output as its pre-activation residual."""
+    W3 = out3.weight.detach().to("cpu", torch.float64)                 # (co, m, 3, 3)
+    W1 = inner2.weight.detach().to("cpu", torch.float64)[:, :, 0, 0]   # (m, ci)
+    b1 = inner2.bias.detach().to("cpu", torch.float64)                 # (m,)
+    co, m = W3.shape[:2]
+    ci = W1.shape[1]
+    S = ((2,), (1, 2), (0, 1), (0,))
+    wt = torch.zeros(m, co, 4, 4, dtype=torch.float64)
+    for a in range(4):
+        for b in range(4):
+            wt[:, :, a, b] = sum(W3[:, :, ky, kx] for ky in S[a] for kx in S[b]).t()
+    up = nn.ConvTranspose2d(m, co, 4, stride=2, padding=1, bias=False)
+    up.weight.data = wt.float()
+    wc = torch.cat([torch.einsum("omyx,mi->oiyx", W3, W1), torch.einsum("omyx,m->oyx", W3, b1)[:, None]], 1)
+    c0 = nn.Conv2d(ci + 1, co, 3, padding=1, bias=False)
+    c0.weight.data = wc.float()
+    return (HipConv2d(up, dtype, False, c0=m), HipConv2d(c0, dtype, False, c0=ci, geo_at=(ci,)))
+
+
 class HipFeatureNet:
     """FeatureNet (fpn or unet) on libdamvs. Input imgs (B, 3, H, W) fp32; outputs NHWC."""
 
@@ -95,8 +127,8 @@ class HipFeatureNet:
             self.inner1 = L(fnet.inner1, False, c0=fnet.inner1.in_channels)
             self.out2 = L(fnet.out2, False, c0=fnet.out2.in_channels)
             if self.num_stage == 3:
-                self.inner2 = L(fnet.inner2, False, c0=fnet.inner2.in_channels)
-                self.out3 = L(fnet.out3, False, c0=fnet.out3.in_channels)
+                self.top_up, self.top_c0 = fpn_top_layers(fnet.inner2, fnet.out3, dtype)
+                self._ones = {}
         else:
             self.up = []
             for fu in [fnet.deconv1] + ([fnet.deconv2] if self.num_stage == 3 else []):
@@ -124,8 +156,12 @@ class HipFeatureNet:
             f = self.inner1(B, c1.shape[1], c1.shape[2], c1, res_post=c2, post_up=2)
             out["stage2"] = self.out2(B, f.shape[1], f.shape[2], f)
             if self.num_stage == 3:
-                f = self.inner2(B, c0.shape[1], c0.shape[2], c0, res_post=f, post_up=2)
-                out["stage3"] = self.out3(B, f.shape[1], f.shape[2], f)
+                # out3(up2(f) + inner2(c0)) without the 32-channel full-resolution sum (fpn_top_layers)
+                t = self.top_up(B, f.shape[1], f.shape[2], f)
+                key = (h, w, c0.device)
+                if key not in self._ones:
+                    self._ones[key] = torch.ones(h, w, device=c0.device, dtype=torch.float32)
+                out["stage3"] = self.top_c0(B, h, w, c0, geo=[(self._ones[key], 0)], res_pre=t)
             return out
         f = c2
         for i, (dec, conv) in enumerate(self.up):
