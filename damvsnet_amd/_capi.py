@@ -76,6 +76,8 @@ SIGNATURES = (
     ("damvs_conv2d_forward", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                      ctypes.POINTER(c_void_p), ctypes.POINTER(ctypes.c_longlong), c_void_p, c_void_p,
                                      c_int, c_void_p)),
+    ("damvs_conv2d_border_bias", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                         ctypes.POINTER(ctypes.c_float), c_void_p)),
 )
 
 _lib = None
@@ -113,6 +115,12 @@ def check(rc: int):
 
 def ptr(t) -> int | None:
     return None if t is None else t.data_ptr()
+
+
+def float_ptr(t):
+    """ctypes float* into a contiguous host fp32 tensor (kept alive by the caller)."""
+    assert t.device.type == "cpu" and t.dtype == torch.float32 and t.is_contiguous()
+    return ctypes.cast(t.data_ptr(), ctypes.POINTER(ctypes.c_float))
 
 
 def stream_ptr(device=None) -> int:

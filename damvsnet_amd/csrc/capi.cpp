@@ -682,6 +682,21 @@ int damvs_conv2d_create(const damvs_conv2d_desc* desc, const float* weight, cons
   return DAMVS_OK;
 }
 
+int damvs_conv2d_border_bias(void* stream, int dtype, int B, int H, int W, int cout_stored, int cout, const float* corr,
+                             void* out) {
+  if (!corr || !out) return fail(DAMVS_E_ARG, "null argument");
+  if (dtype != DAMVS_F32 && dtype != DAMVS_BF16) return fail(DAMVS_E_DTYPE, "dtype %d unsupported", dtype);
+  if (B < 1 || H < 2 || W < 2 || cout < 1 || cout > 16 || cout_stored < cout)
+    return fail(DAMVS_E_SHAPE, "B %d H %d W %d cout %d stored %d unsupported", B, H, W, cout, cout_stored);
+  BorderArgs a;
+  std::memset(&a, 0, sizeof(a));
+  for (int t = 0; t < 9; ++t)
+    for (int c = 0; c < cout; ++c) a.corr[t * 16 + c] = corr[t * cout + c];
+  return hip_check(launch_border_bias(static_cast<hipStream_t>(stream), dtype == DAMVS_BF16 ? ST_BF16 : ST_F32, a, B, H,
+                                      W, cout_stored, cout, out),
+                   "border_bias launch");
+}
+
 int damvs_conv2d_destroy(damvs_conv2d* L) {
   if (!L) return DAMVS_OK;
   if (L->wpack) (void)hipFree(L->wpack);

@@ -26,9 +26,13 @@ template <> struct Stor<float> {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   }
   __device__ __forceinline__ static float ld(const float* p) { return *p; }
+  __device__ __forceinline__ static float to_f(float v) { return v; }
+  __device__ __forceinline__ static float from_f(float v) { return v; }
 };
 template <> struct Stor<bf16_t> {
   static constexpr int E = 8;
+  __device__ __forceinline__ static float to_f(bf16_t v) { return __uint_as_float((uint32_t)v << 16); }
+  __device__ __forceinline__ static bf16_t from_f(float v) { return f2bf(v); }
   __device__ __forceinline__ static void load16(const bf16_t* p, float* v) {
     uint4 q = *reinterpret_cast<const uint4*>(p);
     uint32_t w[4] = {q.x, q.y, q.z, q.w};

@@ -126,6 +126,11 @@ hipError_t launch_block_channels(hipStream_t s, int store, const FeatPtrs& src, 
                                  int hw, int C);
 hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a);
 hipError_t launch_conv2d(hipStream_t s, int store, const Conv2dArgs& a);
+struct BorderArgs {
+  float corr[9 * 16];  // [tap][channel] of a 3x3 conv, channels < 16
+};
+hipError_t launch_border_bias(hipStream_t s, int store, const BorderArgs& a, int B, int H, int W, int cstored, int cout,
+                              void* out);
 bool conv_lds_disabled();  // DAMVS_CONV_NO_LDS=1 selects the global-gather conv kernel (A/B testing)
 hipError_t launch_prob_conv(hipStream_t s, int store, int B, int Cb, int D, int h, int w, const void* feat,
                             const float* wprob, const float* prob_init, float* logits);

@@ -300,6 +300,183 @@ __global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, in
   }
 }
 
+// LDS-staged variant for the thin stride-1 3x3 layers (one tensor input of CIN <= 32 channels, no
+// fp32 plane): the full-resolution FeatureNet / GeoFeatureFusion convs that the global-gather
+// kernel runs TA-bound (each input pixel is fetched by 9 taps through L1). A block owns an
+// 8-row x 64-column output tile; its (8+2) x (64+2) x CIN halo is read once with 16-byte loads
+// (zero padding by range-checked buffer loads) and every B fragment is a ds_read_b128. Wave w owns
+// columns [16w, 16w+16), group j output row j. For CIN < KC a K chunk spans KC/CIN taps; the
+// per-lane tap offsets are compile-time constants once the K loop unrolls (see conv3d_lds_kernel).
+constexpr int L2H = 8, L2W = 64, L2HH = L2H + 2, L2HW = L2W + 2;
+
+template <int CH>
+__device__ constexpr int halo2_toff(int t) {
+  return t >= 9 ? halo2_toff<CH>(8) : ((t / 3) * L2HW + t % 3) * CH;
+}
+
+template <typename T, int CIN, int MT>
+__global__ __launch_bounds__(256) void conv2d_lds_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int ntiles) {
+  typedef BufIO<T> IO;
+  typedef typename IO::raw raw;
+  constexpr int E = Stor<T>::E;
+  constexpr int KC = 4 * E;
+  constexpr int CH = CIN / E;  // 16-byte chunks per pixel
+  constexpr int KCHUNKS = (9 * CIN + KC - 1) / KC;
+  constexpr int ROW = L2HW * CH;
+  constexpr int TILE_CHUNKS = L2HH * ROW;
+  constexpr uint32_t ES = sizeof(T);
+  static_assert(KC % CIN == 0 || CIN % KC == 0, "chunking");
+  __shared__ raw tile[TILE_CHUNKS];
+
+  // XCD-aware bijective remap (consecutive tiles along x share an XCD and its L2)
+  const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
+  int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tx = tt % tiles_x; tt /= tiles_x;
+  const int ty = tt % tiles_y;
+  const int b = tt / tiles_y;
+  const int y0 = ty * L2H, x0 = tx * L2W;
+
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in0, (long long)a.B * a.Hi * a.Wi * CIN * ES);
+  const int pin0 = b * a.Hi * a.Wi;
+  for (int c = threadIdx.x; c < TILE_CHUNKS; c += 256) {
+    const int row = c / ROW, col = c - row * ROW;
+    const int iy = y0 - 1 + row, ix = x0 - 1 + col / CH;
+    const bool ok = (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+    const uint32_t off = (uint32_t)(((pin0 + iy * a.Wi + x0 - 1) * CH + col) * 16);
+    tile[c] = IO::frag(rin, ok ? off : kOOB);
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  f32x4_t acc[L2H][MT];
+#pragma unroll
+  for (int j = 0; j < L2H; ++j)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const raw* tl = tile + (wave * 16 + n) * CH;
+  const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + lane;
+  const int gi = (g * E) / CIN;      // tap sub-index of this lane group (KC > CIN)
+  const int gc = (g * E) % CIN / E;  // 16-byte channel chunk within the pixel
+  auto fetch = [&](int s, raw* xf, raw* wf) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * a.MTtot + m) * 64];
+    const int kt = (s * KC) / CIN, kc = ((s * KC) % CIN) / E;
+    int off = halo2_toff<CH>(kt);
+    if (KC > CIN) {
+      off = gi == 1 ? halo2_toff<CH>(kt + 1) : off;
+      off = gi == 2 ? halo2_toff<CH>(kt + 2) : off;
+      off = gi == 3 ? halo2_toff<CH>(kt + 3) : off;
+    }
+    // taps past the 9th (K padding) read a valid pixel against zero weights
+    const raw* src = tl + off + kc + gc;
+#pragma unroll
+    for (int j = 0; j < L2H; ++j) xf[j] = src[j * ROW];
+  };
+  raw xa[L2H], wa[MT];
+  fetch(0, xa, wa);
+#pragma unroll
+  for (int s = 0; s < KCHUNKS; ++s) {
+    raw xb[L2H], wb[MT];
+    if (s + 1 < KCHUNKS) fetch(s + 1, xb, wb);
+#pragma unroll
+    for (int j = 0; j < L2H; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) Frag2<T>::mma(wa[m], xa[j], acc[j][m]);
+    if (s + 1 < KCHUNKS) {
+#pragma unroll
+      for (int j = 0; j < L2H; ++j) xa[j] = xb[j];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) wa[m] = wb[m];
+    }
+  }
+
+  // epilogue (as conv2d_mfma_kernel): bias, residual before ReLU, ReLU, residual after ReLU, store
+  typedef typename IO::quad quad;
+  const int up = a.post_up, us = a.post_up >> 1;
+  const long long nout = (long long)a.B * a.Ho * a.Wo * a.cout;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout * ES);
+  const __amdgpu_buffer_rsrc_t rpre = make_rsrc(a.res_pre ? a.res_pre : a.out, a.res_pre ? nout * ES : 0);
+  const __amdgpu_buffer_rsrc_t rpost = make_rsrc(a.res_post ? a.res_post : a.out, a.res_post ? nout / (up * up) * ES : 0);
+  float bias[MT][4];
+  bool cok[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int co = m * 16 + g * 4;
+    cok[m] = co < a.cout;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[m][i] = a.bias[co + i];  // padded to cout_pad
+  }
+  const int ox = x0 + wave * 16 + n;
+#pragma unroll
+  for (int j = 0; j < L2H; ++j) {
+    const int oy = y0 + j;
+    const bool vok = oy < a.Ho && ox < a.Wo;
+    const int pout = (b * a.Ho + oy) * a.Wo + ox;
+    const int ppost = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
+    quad qpre[MT], qpost[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const bool ok = vok && cok[m];
+      const int co = m * 16 + g * 4;
+      if (a.res_pre) qpre[m] = IO::ldq(rpre, ok ? (uint32_t)(pout * a.cout + co) * ES : kOOB);
+      if (a.res_post) qpost[m] = IO::ldq(rpost, ok ? (uint32_t)(ppost * a.cout + co) * ES : kOOB);
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      float r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = acc[j][m][i] + bias[m][i];
+      if (a.res_pre) IO::addq(qpre[m], r);
+      if (a.relu) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = fmaxf(r[i], 0.f);
+      }
+      if (a.res_post) IO::addq(qpost[m], r);
+      const uint32_t off = (uint32_t)(pout * a.cout + m * 16 + g * 4) * ES;
+      IO::stq(ro, vok && cok[m] ? off : kOOB, r);
+    }
+  }
+}
+
+// True when the layer is a plain 3x3 stride-1 padding-1 conv with dense row-major taps.
+bool lds3_ok(const Conv2dArgs& a) {
+  if (a.nphase != 1 || a.out_stride != 1 || a.in_stride != 1 || a.ph[0].ntaps != 9 || a.ngeo != 0 || a.c1 != 0 ||
+      a.Ho != a.Hi || a.Wo != a.Wi)
+    return false;
+  for (int t = 0; t < 9; ++t)
+    if (a.ph[0].tap[t][0] != t / 3 - 1 || a.ph[0].tap[t][1] != t % 3 - 1) return false;
+  return true;
+}
+
+template <typename T, int CIN, int MT>
+hipError_t launch_lds2_t(hipStream_t s, const Conv2dArgs& a) {
+  const int tx = (a.Wo + L2W - 1) / L2W, ty = (a.Ho + L2H - 1) / L2H;
+  const long long nt = (long long)tx * ty * a.B;
+  hipLaunchKernelGGL((conv2d_lds_kernel<T, CIN, MT>), dim3((unsigned)nt), dim3(256), 0, s, a, tx, ty, (int)nt);
+  return hipGetLastError();
+}
+
+// Returns hipErrorNotSupported when the LDS variant does not take the layer.
+template <typename T>
+hipError_t launch_lds2(hipStream_t s, const Conv2dArgs& a) {
+  static const bool off = [] {
+    const char* v = getenv("DAMVS_CONV2D_NO_LDS");
+    return v && v[0] == '1';
+  }();
+  if (off || !lds3_ok(a) || a.MTtot > 2 || (sizeof(T) == 4 && a.c0 > 16)) return hipErrorNotSupported;  // LDS <= 42 KB
+  const int MT = a.MTtot;
+  switch (a.c0) {
+    case 8: return MT == 1 ? launch_lds2_t<T, 8, 1>(s, a) : launch_lds2_t<T, 8, 2>(s, a);
+    case 16: return MT == 1 ? launch_lds2_t<T, 16, 1>(s, a) : launch_lds2_t<T, 16, 2>(s, a);
+    case 32:
+      if constexpr (sizeof(T) == 2) return MT == 1 ? launch_lds2_t<T, 32, 1>(s, a) : launch_lds2_t<T, 32, 2>(s, a);
+      return hipErrorNotSupported;
+    default: return hipErrorNotSupported;
+  }
+}
+
 // Direct conv for layers whose only inputs are fp32 planes (c0 = c1 = 0: FeatureNet's RGB conv
 // 3x3 3->8, GeoFeatureFusion's RGB+depth 5x5 4->8 and depth+depth 5x5 2->8 init convs). The MFMA
 // kernel would run these in its epilogue with half the lanes idle and one dependent load chain per
@@ -467,6 +644,10 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
     return hipGetLastError();
   }
   if (a.ngeo > 1) return hipErrorInvalidValue;  // the MFMA path takes at most one plane
+  {
+    const hipError_t e = launch_lds2<T>(s, a);
+    if (e != hipErrorNotSupported) return e;
+  }
   // Widest cout tile (each loaded input fragment feeds MT MFMAs) that still puts about one wave on
   // every SIMD: the low-resolution GeoFeatureFusion layers have few pixels and many channels.
   const long long tiles = ((long long)a.B * a.Hq * a.Wq + 63) / 64 * a.nphase;
@@ -477,7 +658,42 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
   return launch_mt<T, 1>(s, a);
 }
 
+// Border correction of a 3x3 padding-1 conv whose bias was the full 9-tap sum: at each border pixel
+// subtract the taps that fall outside the image (used by the re-associated FPN top level, where the
+// bias of a 1x1 conv travels through a zero-padded 3x3 conv).
+template <typename T>
+__global__ __launch_bounds__(256) void border_bias_kernel(BorderArgs a, int B, int H, int W, int cstored, int cout, T* out) {
+  const int per = 2 * W + 2 * (H - 2);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * per) return;
+  const int b = i / per;
+  int r = i - b * per, y, x;
+  if (r < W) { y = 0; x = r; }
+  else if (r < 2 * W) { y = H - 1; x = r - W; }
+  else { r -= 2 * W; y = 1 + r / 2; x = (r & 1) ? W - 1 : 0; }
+  T* o = out + (((size_t)b * H + y) * W + x) * cstored;
+  for (int c = 0; c < cout; ++c) {
+    float v = Stor<T>::to_f(o[c]);
+    for (int t = 0; t < 9; ++t) {
+      const int iy = y + t / 3 - 1, ix = x + t % 3 - 1;
+      if (iy < 0 || iy >= H || ix < 0 || ix >= W) v -= a.corr[t * 16 + c];
+    }
+    o[c] = Stor<T>::from_f(v);
+  }
+}
+
 }  // namespace
+
+hipError_t launch_border_bias(hipStream_t s, int store, const BorderArgs& a, int B, int H, int W, int cstored, int cout,
+                              void* out) {
+  const long long n = (long long)B * (2 * W + 2 * (H - 2));
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (store == ST_BF16)
+    hipLaunchKernelGGL(border_bias_kernel<bf16_t>, grid, dim3(256), 0, s, a, B, H, W, cstored, cout, static_cast<bf16_t*>(out));
+  else
+    hipLaunchKernelGGL(border_bias_kernel<float>, grid, dim3(256), 0, s, a, B, H, W, cstored, cout, static_cast<float*>(out));
+  return hipGetLastError();
+}
 
 hipError_t launch_conv2d(hipStream_t s, int store, const Conv2dArgs& a) {
   return store == ST_BF16 ? launch_t<bf16_t>(s, a) : launch_t<float>(s, a);

@@ -89,10 +89,11 @@ def fpn_top_layers(inner2, out3, dtype):
                             (per axis, transposed tap a in {0..3} collects 3x3 taps S(a) =
                             {2}, {1,2}, {0,1}, {0}: nearest upsampling merges them pairwise);
       out3(inner2(c0))    = 3x3 conv of c0 with weights out3 . inner2 (8 -> 8);
-      out3(inner2's bias) = a plane of ones as one extra input channel with weights out3 . bias
-                            (zero padding keeps the border exact).
+      out3(inner2's bias) = the full 9-tap sum out3 . bias as that conv's bias, minus the taps that
+                            fall outside the image at border pixels (zero padding of the sum):
+                            damvs_conv2d_border_bias with corr[tap] = out3[tap] . bias.
 
-    Returns (transposed layer on f, 3x3 layer on c0 + ones plane) as HipConv2d; the second takes
+    Returns (transposed layer on f, 3x3 layer on c0, corr [9 * cout] fp32) — the second layer takes
     the first's output as its pre-activation residual."""
     W3 = out3.weight.detach().to("cpu", torch.float64)                 # (co, m, 3, 3)
     W1 = inner2.weight.detach().to("cpu", torch.float64)[:, :, 0, 0]   # (m, ci)
@@ -106,10 +107,11 @@ def fpn_top_layers(inner2, out3, dtype):
             wt[:, :, a, b] = sum(W3[:, :, ky, kx] for ky in S[a] for kx in S[b]).t()
     up = nn.ConvTranspose2d(m, co, 4, stride=2, padding=1, bias=False)
     up.weight.data = wt.float()
-    wc = torch.cat([torch.einsum("omyx,mi->oiyx", W3, W1), torch.einsum("omyx,m->oyx", W3, b1)[:, None]], 1)
-    c0 = nn.Conv2d(ci + 1, co, 3, padding=1, bias=False)
-    c0.weight.data = wc.float()
-    return (HipConv2d(up, dtype, False, c0=m), HipConv2d(c0, dtype, False, c0=ci, geo_at=(ci,)))
+    corr = torch.einsum("omyx,m->yxo", W3, b1)                        # (3, 3, co)
+    c0 = nn.Conv2d(ci, co, 3, padding=1, bias=True)
+    c0.weight.data = torch.einsum("omyx,mi->oiyx", W3, W1).float()
+    c0.bias.data = corr.sum((0, 1)).float()
+    return HipConv2d(up, dtype, False, c0=m), HipConv2d(c0, dtype, False, c0=ci), corr.reshape(-1).float().contiguous()
 
 
 class HipFeatureNet:
@@ -127,8 +129,7 @@ class HipFeatureNet:
             self.inner1 = L(fnet.inner1, False, c0=fnet.inner1.in_channels)
             self.out2 = L(fnet.out2, False, c0=fnet.out2.in_channels)
             if self.num_stage == 3:
-                self.top_up, self.top_c0 = fpn_top_layers(fnet.inner2, fnet.out3, dtype)
-                self._ones = {}
+                self.top_up, self.top_c0, self.top_corr = fpn_top_layers(fnet.inner2, fnet.out3, dtype)
         else:
             self.up = []
             for fu in [fnet.deconv1] + ([fnet.deconv2] if self.num_stage == 3 else []):
@@ -158,10 +159,11 @@ class HipFeatureNet:
             if self.num_stage == 3:
                 # out3(up2(f) + inner2(c0)) without the 32-channel full-resolution sum (fpn_top_layers)
                 t = self.top_up(B, f.shape[1], f.shape[2], f)
-                key = (h, w, c0.device)
-                if key not in self._ones:
-                    self._ones[key] = torch.ones(h, w, device=c0.device, dtype=torch.float32)
-                out["stage3"] = self.top_c0(B, h, w, c0, geo=[(self._ones[key], 0)], res_pre=t)
+                o3 = self.top_c0(B, h, w, c0, res_pre=t)
+                lib = self.top_c0._lib
+                check(lib.damvs_conv2d_border_bias(_capi.stream_ptr(o3.device), DTYPES[o3.dtype], B, h, w, o3.shape[3],
+                                                   self.top_c0.cout, _capi.float_ptr(self.top_corr), ptr(o3)))
+                out["stage3"] = o3
             return out
         f = c2
         for i, (dec, conv) in enumerate(self.up):

@@ -176,6 +176,13 @@ int damvs_conv2d_forward(const damvs_conv2d* layer, void* stream, int B, int Hi,
                          const void* in1, const float* const* geo, const long long* geo_batch_stride, const void* res_pre,
                          const void* res_post, int post_up, void* out);
 
+/* Border fix-up for a 3x3 padding-1 conv whose bias held the full 9-tap sum of a per-tap constant
+ * (a bias that reached the 3x3 conv through a 1x1 conv, FeatureNet's inner2 -> out3,
+ * models/module.py:455-459): at every border pixel of out [B][H][W][cout_stored] subtract
+ * corr[t * cout + c] (host fp32, t = ky*3 + kx, cout <= 16) for the taps t outside the image. */
+int damvs_conv2d_border_bias(void* stream, int dtype, int B, int H, int W, int cout_stored, int cout, const float* corr,
+                             void* out);
+
 #ifdef __cplusplus
 }
 #endif
