@@ -53,6 +53,7 @@ struct LayerPlan {
   int kind = 0, cin = 0, cout = 0, mt = 0, nphase = 0;
   ConvPhase ph[kMaxPhases];
   void* wpack = nullptr;
+  void* wpack_pair = nullptr;  // row-pair packing for Cout <= 8 stride-1 layers (conv3d_lds_pair_kernel)
   float* bias = nullptr;
 };
 
@@ -138,6 +139,27 @@ void pack_layer(LayerPlan& P, const std::vector<float>& wf, int E, std::vector<S
   }
 }
 
+// Row-pair packing for a stride-1 layer with cout <= 8: the 16 MFMA rows are (r, co) = output rows
+// y + r (r = 0, 1) x 8 channels; K runs over 36 taps (dz, dy' = 0..3, dx) x cin, where dy' is the
+// input row relative to y - 1, so row r sees kernel row ky = dy' - r (zero outside 0..2):
+//   element (s * 64 + lane) * E + e  =  A[row = lane & 15][k = s*KC + (lane >> 4)*E + e].
+template <typename S>
+void pack_layer_pair(const LayerPlan& P, const std::vector<float>& wf, int E, std::vector<S>& out, S (*cvt)(float)) {
+  const int KC = 4 * E;
+  const int nch = (36 * P.cin + KC - 1) / KC;
+  for (int s = 0; s < nch; ++s)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int e = 0; e < E; ++e) {
+        const int row = lane & 15, r = row >> 3, co = row & 7;
+        const int k = s * KC + (lane >> 4) * E + e;
+        const int t2 = k / P.cin, ci = k % P.cin;
+        const int dz = t2 / 12, dy = (t2 / 3) % 4, dx = t2 % 3, ky = dy - r;
+        float v = 0.f;
+        if (t2 < 36 && co < P.cout && ky >= 0 && ky <= 2) v = wf[((size_t)co * P.cin + ci) * 27 + (dz * 3 + ky) * 3 + dx];
+        out.push_back(cvt(v));
+      }
+}
+
 float cvt_f32(float v) { return v; }
 uint16_t cvt_bf16(float v) { return to_bf16(v); }
 
@@ -220,6 +242,7 @@ ConvArgs conv_args(const damvs_stage* st, int li, int B, const Shapes& S, int li
   a.out = out;
   a.resid = resid;
   a.wpack = P.wpack;
+  a.wpack_pair = P.wpack_pair;
   a.bias = P.bias;
   a.B = B;
   a.Cin = P.cin;
@@ -342,6 +365,17 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
       pack_layer<float>(P, wf, E, pk, cvt_f32);
       rc = upload(pk.data(), pk.size() * 4, &P.wpack);
     }
+    if (rc == DAMVS_OK && P.kind == CONV_S1 && P.cout <= 8) {
+      if (dtype == DAMVS_BF16) {
+        std::vector<uint16_t> pk;
+        pack_layer_pair<uint16_t>(P, wf, E, pk, cvt_bf16);
+        rc = upload(pk.data(), pk.size() * 2, &P.wpack_pair);
+      } else {
+        std::vector<float> pk;
+        pack_layer_pair<float>(P, wf, E, pk, cvt_f32);
+        rc = upload(pk.data(), pk.size() * 4, &P.wpack_pair);
+      }
+    }
     if (rc == DAMVS_OK) rc = upload(shift.data(), shift.size() * 4, reinterpret_cast<void**>(&P.bias));
   }
   if (rc == DAMVS_OK) {
@@ -378,6 +412,7 @@ int damvs_stage_destroy(damvs_stage* st) {
   if (!st) return DAMVS_OK;
   for (auto& P : st->L) {
     if (P.wpack) (void)hipFree(P.wpack);
+    if (P.wpack_pair) (void)hipFree(P.wpack_pair);
     if (P.bias) (void)hipFree(P.bias);
   }
   if (st->prob_w) (void)hipFree(st->prob_w);

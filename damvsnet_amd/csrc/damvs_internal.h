@@ -69,6 +69,7 @@ struct ConvArgs {
   void* out;
   const void* resid;   // added after ReLU (may alias out); nullptr if none
   const void* wpack;   // packed A fragments, see pack_conv_weights()
+  const void* wpack_pair;  // row-pair packing (stride-1, Cout <= 8), nullptr if none
   const float* bias;   // [Cout] (folded BN shift)
   int B, Cin, Cout, MT;
   int Di, Hi, Wi;

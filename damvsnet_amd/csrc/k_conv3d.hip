@@ -392,6 +392,127 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
   }
 }
 
+// Row-pair variant for Cout <= 8 (conv0 of every stage): a 16-row MFMA tile holds 8 channels of
+// output rows y and y+1 (pack_layer_pair), so no A row is padding and each B fragment (input row
+// y-1+dy', dy' = 0..3) feeds both rows: per output row 18*CIN K instead of 27*CIN, i.e. 1.5x fewer
+// MFMAs and LDS reads than conv3d_lds_kernel with half its M rows empty. Same tile and halo; a
+// wave's 4 groups are the 4 row pairs of its z-slice, and every lane stores 4 useful channels.
+template <int CH>
+__device__ constexpr int halo_pair_toff(int t) {
+  return t >= 36 ? halo_pair_toff<CH>(35) : (((t / 12) * LHH + (t / 3) % 4) * LHW + t % 3) * CH;
+}
+
+template <typename T, int CIN>
+__global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, int tiles_x, int tiles_y, int tiles_z,
+                                                              int ntiles) {
+  typedef typename Frag<T>::raw raw;
+  constexpr int E = Stor<T>::E;
+  constexpr int KC = 4 * E;
+  constexpr int CH = CIN / E;
+  constexpr int KCHUNKS = (36 * CIN + KC - 1) / KC;
+  constexpr int ROW = LHW * CH;
+  constexpr int TILE_CHUNKS = LHD * LHH * ROW;
+  constexpr int NP = LTH / 2;  // row pairs per z-slice
+  static_assert(KC % CIN == 0 || CIN % KC == 0, "chunking");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  raw* tile = reinterpret_cast<raw*>(smem);
+
+  const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  int tt = t;
+  const int tx = tt % tiles_x; tt /= tiles_x;
+  const int ty = tt % tiles_y; tt /= tiles_y;
+  const int tz = tt % tiles_z;
+  const int b = tt / tiles_z;
+  const int z0 = tz * LTD, y0 = ty * LTH, x0 = tx * LTW;
+
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * sizeof(T));
+  const int vin0 = b * a.Di * a.Hi * a.Wi;
+  for (int c = threadIdx.x; c < TILE_CHUNKS; c += 256) {
+    const int row = c / ROW, col = c - row * ROW;
+    const int hz = row / LHH, hy = row - hz * LHH;
+    const int iz = z0 - 1 + hz, iy = y0 - 1 + hy, ix = x0 - 1 + col / CH;
+    const bool ok = (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+    const uint32_t off = (uint32_t)(((vin0 + (iz * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16);
+    tile[c] = BufIO<T>::frag(rin, ok ? off : kOOB);
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  f32x4_t acc[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const raw* tl = tile + (wave * LHH * LHW + n) * CH;
+  const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack_pair) + lane;
+  const int gi = (g * E) / CIN;
+  const int gc = (g * E) % CIN / E;
+  auto fetch = [&](int s, raw* xf, raw& wf) {
+    wf = wp[(size_t)s * 64];
+    const int kt = (s * KC) / CIN, kc = ((s * KC) % CIN) / E;
+    int off = halo_pair_toff<CH>(kt);
+    if (KC > CIN) {
+      off = gi == 1 ? halo_pair_toff<CH>(kt + 1) : off;
+      off = gi == 2 ? halo_pair_toff<CH>(kt + 2) : off;
+      off = gi == 3 ? halo_pair_toff<CH>(kt + 3) : off;
+    }
+    const raw* src = tl + off + kc + gc;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) xf[j] = src[2 * j * ROW];
+  };
+  raw xa[NP], wa;
+  fetch(0, xa, wa);
+#pragma unroll
+  for (int s = 0; s < KCHUNKS; ++s) {
+    raw xb[NP], wb;
+    if (s + 1 < KCHUNKS) fetch(s + 1, xb, wb);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) Frag<T>::mma(wa, xa[j], acc[j]);
+    if (s + 1 < KCHUNKS) {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) xa[j] = xb[j];
+      wa = wb;
+    }
+  }
+
+  // lane group g holds rows 4g..4g+3 = channels (g & 1)*4 .. +3 of output row y + (g >> 1)
+  constexpr uint32_t ES = sizeof(T);
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * ES;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.resid ? a.resid : a.out, a.resid ? nout : 0);
+  const int co = (g & 1) * 4, r = g >> 1;
+  const bool cok = co < a.Cout;
+  float bias[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias[i] = cok ? a.bias[co + i] : 0.f;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int oz = z0 + wave, oy = y0 + 2 * j + r, ox = x0 + n;
+    const bool vok = oz < a.Do && oy < a.Ho && ox < a.Wo && cok;
+    const int pout = ((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox;
+    const uint32_t off = (uint32_t)(pout * a.Cout + co) * ES;
+    typename BufIO<T>::quad q;
+    if (a.resid) q = BufIO<T>::ldq(rr, vok ? off : kOOB);
+    finish4<T>(a, ro, rr, q, a.resid != nullptr, off, vok, bias, acc[j]);
+  }
+}
+
+template <typename T, int CIN>
+hipError_t launch_lds_pair_t(hipStream_t s, const ConvArgs& a) {
+  const size_t smem = lds_tile_bytes<T, CIN>();
+  auto k = conv3d_lds_pair_kernel<T, CIN>;
+  if (smem > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)smem);
+    if (e != hipSuccess) return e;
+  }
+  const int tx = (a.Wo + LTW - 1) / LTW, ty = (a.Ho + LTH - 1) / LTH, tz = (a.Do + LTD - 1) / LTD;
+  const long long nt = (long long)tx * ty * tz * a.B;
+  hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, tz, (int)nt);
+  return hipGetLastError();
+}
+
 template <typename T, int CIN, int MT>
 hipError_t launch_lds_t(hipStream_t s, const ConvArgs& a) {
   const size_t smem = lds_tile_bytes<T, CIN>();
@@ -412,6 +533,15 @@ template <typename T>
 hipError_t launch_lds(hipStream_t s, const ConvArgs& a) {
   if (a.nphase != 1 || a.in_stride != 1 || a.out_stride != 1 || a.ph[0].ntaps != 27) return hipErrorNotSupported;
   const int MT = a.MT;
+  static const bool no_pair = [] {
+    const char* v = getenv("DAMVS_CONV_NO_PAIR");
+    return v && v[0] == '1';
+  }();
+  if (a.wpack_pair && a.Cout <= 8 && !no_pair) {
+    if (a.Cin == 8) return launch_lds_pair_t<T, 8>(s, a);
+    if (a.Cin == 16) return launch_lds_pair_t<T, 16>(s, a);
+    if (a.Cin == 32 && sizeof(T) == 2) return launch_lds_pair_t<T, 32>(s, a);
+  }
   if (a.Cin == 8 && MT == 1) return launch_lds_t<T, 8, 1>(s, a);
   if (a.Cin == 16 && MT == 1) return launch_lds_t<T, 16, 1>(s, a);
   if (a.Cin == 32 && MT == 1) return launch_lds_t<T, 32, 1>(s, a);
