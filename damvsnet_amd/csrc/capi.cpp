@@ -53,7 +53,10 @@ struct LayerPlan {
   int kind = 0, cin = 0, cout = 0, mt = 0, nphase = 0;
   ConvPhase ph[kMaxPhases];
   void* wpack = nullptr;
-  void* wpack_pair = nullptr;  // row-pair packing for Cout <= 8 stride-1 layers (conv3d_lds_pair_kernel)
+  void* wpack_pair = nullptr;  // Cout <= 8: row-pair packing (stride 1, conv3d_lds_pair_kernel) or
+                               // x-parity-pair phases (deconv, conv3d_mfma_kernel<.., XP>)
+  int nphase_pair = 0;
+  ConvPhase ph_pair[4];
   float* bias = nullptr;
 };
 
@@ -160,6 +163,62 @@ void pack_layer_pair(const LayerPlan& P, const std::vector<float>& wf, int E, st
       }
 }
 
+// ConvTranspose k3 s2 (Cout <= 8) as 4 phases (pz, py) whose 16 MFMA rows are the two x parities
+// x 8 channels: x-parity 0 takes kx = 1 at input offset 0, parity 1 takes kx = 2 at offset 0 and
+// kx = 0 at offset +1, so both share the input x-offsets {0, +1} (tap[t][2] = dx, tap[t][3] = the
+// (kz, ky) part of the weight tap). K per phase = nz * ny * 2 * cin; over the 4 phases 18 * cin
+// instead of 27 * cin for the 8 single-parity phases, and no M row is padding.
+void build_phases_xpair(LayerPlan& P, int kchunk_k) {
+  const int ks[2][2] = {{1, -1}, {0, 2}};
+  const int off[2][2] = {{0, 0}, {1, 0}};
+  const int cnt[2] = {1, 2};
+  std::memset(P.ph_pair, 0, sizeof(P.ph_pair));
+  P.nphase_pair = 4;
+  for (int p = 0; p < 4; ++p) {
+    ConvPhase& ph = P.ph_pair[p];
+    ph.pd = (p >> 1) & 1;
+    ph.ph = p & 1;
+    ph.pw = 0;
+    int t = 0;
+    for (int a = 0; a < cnt[ph.pd]; ++a)
+      for (int b = 0; b < cnt[ph.ph]; ++b)
+        for (int dx = 0; dx < 2; ++dx) {
+          ph.tap[t][0] = (signed char)off[ph.pd][a];
+          ph.tap[t][1] = (signed char)off[ph.ph][b];
+          ph.tap[t][2] = (signed char)dx;
+          ph.tap[t][3] = (signed char)(ks[ph.pd][a] * 9 + ks[ph.ph][b] * 3);  // + kx by (row parity, dx)
+          ++t;
+        }
+    ph.ntaps = t;
+    ph.kchunks = (t * P.cin + kchunk_k - 1) / kchunk_k;
+  }
+}
+
+template <typename S>
+void pack_layer_xpair(LayerPlan& P, const std::vector<float>& wf, int E, std::vector<S>& out, S (*cvt)(float)) {
+  const int KC = 4 * E;
+  const int kx_of[2][2] = {{1, -1}, {2, 0}};  // [x parity][dx]
+  int w_off = 0;
+  for (int p = 0; p < P.nphase_pair; ++p) {
+    ConvPhase& ph = P.ph_pair[p];
+    ph.w_off = w_off;
+    for (int s = 0; s < ph.kchunks; ++s)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int e = 0; e < E; ++e) {
+          const int row = lane & 15, px = row >> 3, co = row & 7;
+          const int k = s * KC + (lane >> 4) * E + e;
+          const int t = k / P.cin, ci = k % P.cin;
+          float v = 0.f;
+          if (co < P.cout && t < ph.ntaps) {
+            const int kx = kx_of[px][(int)ph.tap[t][2]];
+            if (kx >= 0) v = wf[((size_t)co * P.cin + ci) * 27 + (unsigned char)ph.tap[t][3] + kx];
+          }
+          out.push_back(cvt(v));
+        }
+    w_off += ph.kchunks;
+  }
+}
+
 float cvt_f32(float v) { return v; }
 uint16_t cvt_bf16(float v) { return to_bf16(v); }
 
@@ -262,6 +321,13 @@ ConvArgs conv_args(const damvs_stage* st, int li, int B, const Shapes& S, int li
   a.relu = 1;
   a.nphase = P.nphase;
   std::memcpy(a.ph, P.ph, sizeof(a.ph));
+  if (P.kind == DECONV_S2 && P.wpack_pair && !conv_xpair_disabled()) {
+    a.xpair = 1;
+    a.wpack = P.wpack_pair;
+    a.nphase = P.nphase_pair;
+    std::memset(a.ph, 0, sizeof(a.ph));
+    std::memcpy(a.ph, P.ph_pair, sizeof(P.ph_pair));
+  }
   return a;
 }
 
@@ -364,6 +430,18 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
       std::vector<float> pk;
       pack_layer<float>(P, wf, E, pk, cvt_f32);
       rc = upload(pk.data(), pk.size() * 4, &P.wpack);
+    }
+    if (rc == DAMVS_OK && P.kind == DECONV_S2 && P.cout <= 8) {
+      build_phases_xpair(P, 4 * E);
+      if (dtype == DAMVS_BF16) {
+        std::vector<uint16_t> pk;
+        pack_layer_xpair<uint16_t>(P, wf, E, pk, cvt_bf16);
+        rc = upload(pk.data(), pk.size() * 2, &P.wpack_pair);
+      } else {
+        std::vector<float> pk;
+        pack_layer_xpair<float>(P, wf, E, pk, cvt_f32);
+        rc = upload(pk.data(), pk.size() * 4, &P.wpack_pair);
+      }
     }
     if (rc == DAMVS_OK && P.kind == CONV_S1 && P.cout <= 8) {
       if (dtype == DAMVS_BF16) {

@@ -78,6 +78,7 @@ struct ConvArgs {
   int in_stride, out_stride;
   int relu;
   int nphase;
+  int xpair;  // deconv phases are (pz, py) with both x parities in the MFMA rows (Cout <= 8)
   FastDiv div_wq, div_hq, div_dq;  // set by launch_conv3d
   ConvPhase ph[kMaxPhases];
 };
@@ -133,6 +134,7 @@ struct BorderArgs {
 hipError_t launch_border_bias(hipStream_t s, int store, const BorderArgs& a, int B, int H, int W, int cstored, int cout,
                               void* out);
 bool conv_lds_disabled();  // DAMVS_CONV_NO_LDS=1 selects the global-gather conv kernel (A/B testing)
+bool conv_xpair_disabled();  // DAMVS_CONV_NO_XPAIR=1: single-parity deconv phases (A/B testing)
 hipError_t launch_prob_conv(hipStream_t s, int store, int B, int Cb, int D, int h, int w, const void* feat,
                             const float* wprob, const float* prob_init, float* logits);
 hipError_t launch_prob_regress(hipStream_t s, int store, int B, int Cb, int D, int h, int w, const void* feat,

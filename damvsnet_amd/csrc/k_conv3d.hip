@@ -93,7 +93,9 @@ __device__ __forceinline__ void finish4(const ConvArgs& a, __amdgpu_buffer_rsrc_
 // Global-gather implicit GEMM (strided convs, deconv phases, and any layer the LDS variant does not
 // take). 32-bit incremental indexing: no divisions in the K loop, magic-number division for the
 // voxel decomposition, range-checked buffer loads for the zero padding.
-template <typename T, int MT>
+// XP: x-parity-pair deconv phases (build_phases_xpair): MFMA row r = (x parity r >> 3, channel r & 7),
+// so lane group g stores channels (g & 1) * 4 .. +3 of output x = 2 qx + (g >> 1).
+template <typename T, int MT, bool XP>
 __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int nqblk) {
   typedef BufIO<T> IO;
   typedef typename IO::raw raw;
@@ -134,7 +136,7 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int 
     const int b = fdiv(a.div_dq, r2), qz = r2 - b * a.Dq;
     zs[j] = qz * IS; ys[j] = qy * IS; xs[j] = qx * IS;
     pin[j] = ((b * a.Di + zs[j]) * a.Hi + ys[j]) * a.Wi + xs[j];
-    pout[j] = ((b * a.Do + qz * OS + ph.pd) * a.Ho + qy * OS + ph.ph) * a.Wo + qx * OS + ph.pw;
+    pout[j] = ((b * a.Do + qz * OS + ph.pd) * a.Ho + qy * OS + ph.ph) * a.Wo + qx * OS + (XP ? (g >> 1) : ph.pw);
   }
 
   f32x4_t acc[kGroups][MT];
@@ -178,9 +180,10 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int 
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.resid ? a.resid : a.out, a.resid ? nout : 0);
   float bias[MT][4];
   bool cok[MT];
+  const int cg = XP ? (g & 1) * 4 : g * 4;  // first channel of this lane group's 4
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
-    const int co = m * 16 + g * 4;
+    const int co = m * 16 + cg;
     cok[m] = co < a.Cout;
 #pragma unroll
     for (int i = 0; i < 4; ++i) bias[m][i] = cok[m] ? a.bias[co + i] : 0.f;
@@ -190,12 +193,12 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int 
     typename IO::quad q[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const uint32_t off = (uint32_t)(pout[j] * a.Cout + m * 16 + g * 4) * ES;
+      const uint32_t off = (uint32_t)(pout[j] * a.Cout + m * 16 + cg) * ES;
       if (a.resid) q[m] = IO::ldq(rr, valid[j] && cok[m] ? off : kOOB);
     }
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const uint32_t off = (uint32_t)(pout[j] * a.Cout + m * 16 + g * 4) * ES;
+      const uint32_t off = (uint32_t)(pout[j] * a.Cout + m * 16 + cg) * ES;
       finish4<T>(a, ro, rr, q[m], a.resid != nullptr, off, valid[j] && cok[m], bias[m], acc[j][m]);
     }
   }
@@ -556,10 +559,15 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
   long long per_block = 4LL * kGroups * 16;
   const int nq = (int)((Qtot + per_block - 1) / per_block);
   dim3 grid((unsigned)(nq * a.nphase));
+  if (a.xpair) {
+    if (a.MT != 1 || a.Cout > 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, true>), grid, dim3(256), 0, s, a, nq);
+    return hipGetLastError();
+  }
   switch (a.MT) {
-    case 1: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1>), grid, dim3(256), 0, s, a, nq); break;
-    case 2: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 2>), grid, dim3(256), 0, s, a, nq); break;
-    case 4: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 4>), grid, dim3(256), 0, s, a, nq); break;
+    case 1: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, false>), grid, dim3(256), 0, s, a, nq); break;
+    case 2: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 2, false>), grid, dim3(256), 0, s, a, nq); break;
+    case 4: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 4, false>), grid, dim3(256), 0, s, a, nq); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -593,6 +601,14 @@ hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a0) {
     if (e != hipErrorNotSupported) return e;
   }
   return store == ST_BF16 ? launch_t<bf16_t>(s, a) : launch_t<float>(s, a);
+}
+
+bool conv_xpair_disabled() {
+  static const bool off = [] {
+    const char* v = getenv("DAMVS_CONV_NO_XPAIR");
+    return v && v[0] == '1';
+  }();
+  return off;
 }
 
 bool conv_lds_disabled() {
