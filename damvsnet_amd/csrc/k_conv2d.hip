@@ -651,8 +651,15 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
   // Widest cout tile (each loaded input fragment feeds MT MFMAs) that still puts about one wave on
   // every SIMD: the low-resolution GeoFeatureFusion layers have few pixels and many channels.
   const long long tiles = ((long long)a.B * a.Hq * a.Wq + 63) / 64 * a.nphase;
-  const long long want = 900;
-  if (T_is_bf16<T>::value && a.MTtot % 8 == 0 && tiles * (a.MTtot / 8) >= want) return launch_mt<T, 8>(s, a);
+  static const long long want = [] {
+    const char* v = getenv("DAMVS_CONV2D_WANT_TILES");
+    return v ? atoll(v) : 900LL;
+  }();
+  static const int maxmt = [] {
+    const char* v = getenv("DAMVS_CONV2D_MAXMT");
+    return v ? atoi(v) : 8;
+  }();
+  if (T_is_bf16<T>::value && maxmt >= 8 && a.MTtot % 8 == 0 && tiles * (a.MTtot / 8) >= want) return launch_mt<T, 8>(s, a);
   if (a.MTtot % 4 == 0 && tiles * (a.MTtot / 4) >= want) return launch_mt<T, 4>(s, a);
   if (a.MTtot % 2 == 0 && tiles * (a.MTtot / 2) >= want) return launch_mt<T, 2>(s, a);
   return launch_mt<T, 1>(s, a);

@@ -9,6 +9,7 @@
 //              confidence = sum of p over [i*-1, i*+2] at i* = clamp(long(sum p*i), 0, D-1)
 //              (:113-118, the 4*avg_pool3d of the padded volume), exp-variance
 //              3*sqrt(sum (d - depth)^2 p) (:121-124); optional prob volume write.
+#include <cstdlib>
 #include <type_traits>
 
 #include "damvs_device.h"
@@ -108,7 +109,10 @@ __global__ __launch_bounds__(256) void regress_kernel(int B, int D, int hw, cons
 // an LDS column [D][256] and the regression runs from there. Logits never reach HBM.
 constexpr int kTY = 8, kTX = 32, kHY = kTY + 2, kHX = kTX + 2;
 
-template <typename T, int CB>
+// TWO: first pass of the two-pass form — the same LDS-tiled prob conv, logits (+prob_init) written
+// to HBM ([B][D][h][w], argument `prob`) for regress_kernel; LDS then holds only the plane tiles, so
+// 3x more blocks share a CU than with the D-deep logit column.
+template <typename T, int CB, bool TWO>
 __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, int w, const T* __restrict__ feat,
                                                            const float* __restrict__ wprob,
                                                            const float* __restrict__ prob_init,
@@ -192,11 +196,27 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
           c2 += w2[c] * v[c];
         }
       }
-    if (pl >= 1) lg[(pl - 1) * 256 + tid] = am1 + c2;
+    if (TWO) {
+      const int y = y0 + ty, x = x0 + tx;
+      if (pl >= 1 && y < h && x < w) {
+        const size_t o = (((size_t)b * D + pl - 1) * h + y) * w + x;
+        prob[o] = am1 + c2 + (prob_init ? prob_init[o] : 0.f);
+      }
+    } else if (pl >= 1) {
+      lg[(pl - 1) * 256 + tid] = am1 + c2;
+    }
     am1 = a0 + c1;
     a0 = c0;
     if (pl + 1 < D) lstore((pl + 1) & 1);
     __syncthreads();
+  }
+  if (TWO) {
+    const int y = y0 + ty, x = x0 + tx;
+    if (y < h && x < w) {
+      const size_t o = (((size_t)b * D + D - 1) * h + y) * w + x;
+      prob[o] = am1 + (prob_init ? prob_init[o] : 0.f);
+    }
+    return;
   }
   lg[(D - 1) * 256 + tid] = am1;
 
@@ -250,7 +270,7 @@ hipError_t launch_pr_t(hipStream_t s, int B, int D, int h, int w, const void* fe
                        const float* prob_init, const float* hyps, float* depth, float* conf, float* var, float* prob) {
   const size_t smem = prob_regress_smem<T, CB>(D);
   if (smem > 160 * 1024) return hipErrorInvalidValue;
-  auto k = prob_regress_kernel<T, CB>;
+  auto k = prob_regress_kernel<T, CB, false>;
   if (smem > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)smem);
@@ -262,9 +282,21 @@ hipError_t launch_pr_t(hipStream_t s, int B, int D, int h, int w, const void* fe
   return hipGetLastError();
 }
 
+template <typename T, int CB>
+hipError_t launch_pc_lds(hipStream_t s, int B, int D, int h, int w, const void* feat, const float* wprob,
+                         const float* prob_init, float* logits) {
+  const size_t smem = prob_regress_smem<T, CB>(0);
+  dim3 grid((w + kTX - 1) / kTX, (h + kTY - 1) / kTY, B);
+  hipLaunchKernelGGL((prob_regress_kernel<T, CB, true>), grid, dim3(256), smem, s, B, D, h, w,
+                     reinterpret_cast<const T*>(feat), wprob, prob_init, nullptr, nullptr, nullptr, nullptr, logits);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_pc(hipStream_t s, int B, int Cb, int D, int h, int w, const void* feat, const float* wprob,
                      const float* prob_init, float* logits) {
+  if (Cb == 8) return launch_pc_lds<T, 8>(s, B, D, h, w, feat, wprob, prob_init, logits);
+  if (Cb == 16) return launch_pc_lds<T, 16>(s, B, D, h, w, feat, wprob, prob_init, logits);
   dim3 grid((h * w + 255) / 256, B);
   const T* f = reinterpret_cast<const T*>(feat);
   switch (Cb) {
@@ -296,6 +328,11 @@ hipError_t launch_prob_regress(hipStream_t s, int store, int B, int Cb, int D, i
 }
 
 size_t prob_regress_smem_bytes(int store, int Cb, int D) {
+  static const bool two_pass = [] {  // measured slower at cfgC (A/B knob)
+    const char* v = getenv("DAMVS_PROBREG_TWOPASS");
+    return v && v[0] == '1';
+  }();
+  if (two_pass) return (size_t)-1;  // the caller takes the two-pass form
   if (Cb == 8) return store == ST_BF16 ? prob_regress_smem<bf16_t, 8>(D) : prob_regress_smem<float, 8>(D);
   return store == ST_BF16 ? prob_regress_smem<bf16_t, 16>(D) : prob_regress_smem<float, 16>(D);
 }

@@ -107,6 +107,43 @@ def test_conv2d_layer_vs_torch(case, dtype):
     assert rel_max(got.numpy(), y.detach().numpy()) < tol
 
 
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
+def test_fpn_top_reassociation_vs_torch(dtype, tol):
+    """out3(up2(f) + inner2(c0)) (models/module.py:455-459) against fpn_top_layers' re-associated form:
+    transposed sum-of-taps conv of f + composed 3x3 conv of c0 + full-sum bias with the border fix-up
+    (damvs_conv2d_border_bias) — every border pixel and corner included."""
+    from damvsnet_amd import _capi
+    from damvsnet_amd.engine import DTYPES
+    from damvsnet_amd.frontend_hip import fpn_top_layers
+    g = torch.Generator().manual_seed(3)
+    inner2, out3 = nn.Conv2d(8, 32, 1, bias=True), nn.Conv2d(32, 8, 3, padding=1, bias=False)
+    with torch.no_grad():
+        for m in (inner2, out3):
+            m.weight.copy_(torch.randn(m.weight.shape, generator=g) * 0.2)
+        inner2.bias.copy_(torch.randn(32, generator=g))
+    B, H, W = 2, 12, 20
+    c0 = torch.randn(B, 8, H, W, generator=g)
+    f = torch.randn(B, 32, H // 2, W // 2, generator=g)
+    if dtype == torch.bfloat16:
+        c0, f = c0.to(dtype).float(), f.to(dtype).float()
+    ref = out3(F.interpolate(f, scale_factor=2, mode="nearest") + inner2(c0)).detach()
+    up, conv, corr = fpn_top_layers(inner2, out3, dtype)
+    t = up(B, H // 2, W // 2, nhwc(f).to(DEV, dtype))
+    o = conv(B, H, W, nhwc(c0).to(DEV, dtype), res_pre=t)
+    lib = _capi.load_library()
+    _capi.check(lib.damvs_conv2d_border_bias(_capi.stream_ptr(o.device), DTYPES[dtype], B, H, W, o.shape[3], 8,
+                                             _capi.float_ptr(corr), o.data_ptr()))
+    got = o.float().cpu().permute(0, 3, 1, 2)
+    assert rel_max(got.numpy(), ref.numpy()) < tol
+    # argument checks: cout beyond the 16-channel table, null output
+    with pytest.raises(_capi.DamvsError):
+        _capi.check(lib.damvs_conv2d_border_bias(_capi.stream_ptr(o.device), DTYPES[dtype], B, H, W, 32, 17,
+                                                 _capi.float_ptr(torch.zeros(9 * 17)), o.data_ptr()))
+    with pytest.raises(_capi.DamvsError):
+        _capi.check(lib.damvs_conv2d_border_bias(_capi.stream_ptr(o.device), DTYPES[dtype], B, H, W, 8, 8,
+                                                 _capi.float_ptr(corr), None))
+
+
 def _folded(sd, dtype):
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.frontend_fold import fold_frontend
