@@ -62,6 +62,9 @@ __device__ __forceinline__ void st4<bf16_t>(bf16_t* p, const float* r) {
                                             (uint32_t)f2bf(r[2]) | ((uint32_t)f2bf(r[3]) << 16));
 }
 
+template <typename T> struct T_is_bf16 { static constexpr bool value = false; };
+template <> struct T_is_bf16<bf16_t> { static constexpr bool value = true; };
+
 constexpr int kG2 = 4;  // 16-pixel groups per wave
 
 template <typename T> __device__ __forceinline__ typename Frag2<T>::raw pack_vals(const float* v);
@@ -440,6 +443,245 @@ __global__ __launch_bounds__(256) void conv2d_lds_kernel(const Conv2dArgs a, int
   }
 }
 
+// Halo-tiled implicit GEMM for the wide layers (Cin a multiple of KC, in_stride 1: GeoFeatureFusion's
+// stride-1 GeoBlock convs, k3/k5 decoders and the k5 s2 transposed decoders' phases). A block owns a
+// 4-row x 64-column tile of the q-grid for one phase and MT 16-channel output tiles; wave w owns
+// columns [16w, 16w+16) and group j row j (wave tile MT x 4 MFMA tiles, as conv2d_mfma_kernel). K
+// runs over Cin slices of KC channels: each slice's input halo ((4 + span) x (64 + span) pixels x KC
+// channels, one 16-byte chunk per lane group) is staged in LDS once and feeds every tap of the phase
+// (the gather kernel re-fetches each input pixel once per tap through L1), double-buffered so slice
+// c+1 streams in during slice c's MFMAs. A fragments come from global (L2-resident packed weights,
+// one coalesced 1 KB load per MFMA tile), prefetched one tap ahead. The fp32 plane, if any, runs as
+// the trailing K chunk(s) with global loads.
+constexpr int HGR = 4, HGC = 64;  // q-tile rows (one per group) x columns (16 per wave)
+
+template <typename T, int MT, bool TWO>
+__global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int nsl,
+                                                          int dmin, int span) {
+  typedef BufIO<T> IO;
+  typedef typename IO::raw raw;
+  constexpr int E = Stor<T>::E;
+  constexpr int KC = 4 * E;
+  constexpr uint32_t ES = sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  raw* buf = reinterpret_cast<raw*>(smem);
+  const int HR = HGR + span - 1, HC = HGC + span - 1;  // halo rows / columns
+  const int HP = HR * HC;                               // halo pixels (4 chunks each)
+
+  // logical block = (tile, phase), phase fastest, XCD-contiguous
+  const int ntile = tiles_x * tiles_y * a.B;
+  const int nblk = ntile * a.nphase;
+  const int bid = blockIdx.x, q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tl = L / a.nphase;
+  const Conv2dPhase& ph = a.ph[L - tl * a.nphase];
+  const int tx = tl % tiles_x, ty = (tl / tiles_x) % tiles_y, b = tl / (tiles_x * tiles_y);
+  const int qy0 = ty * HGR, qx0 = tx * HGC;
+  const int mt0 = blockIdx.y * MT;
+
+  __shared__ int s_toff[32];  // tap offset inside the halo, in pixels
+  if (threadIdx.x < 25)
+    s_toff[threadIdx.x] = threadIdx.x < ph.ntaps ? (ph.tap[threadIdx.x][0] - dmin) * HC + (ph.tap[threadIdx.x][1] - dmin) : 0;
+
+  // halo fill of slice c into buffer bi: pixel p = (row, col), 4 chunks of E channels
+  const int npix = a.B * a.Hi * a.Wi;
+  const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.in0, (long long)npix * a.c0 * ES);
+  const __amdgpu_buffer_rsrc_t r1 = make_rsrc(TWO ? a.in1 : a.in0, TWO ? (long long)npix * a.c1 * ES : 0);
+  const int iy0 = qy0 + dmin, ix0 = qx0 + dmin, pb = b * a.Hi * a.Wi;
+  constexpr int PER = 8;  // 16-byte pieces per thread per fill (covers 2048 pieces = 512 halo pixels)
+  raw regs[PER];
+  auto gfill = [&](int c) {
+    const bool second = TWO && c * KC >= a.c0;
+    const int cs = second ? a.c1 : a.c0, cb = (second ? c * KC - a.c0 : c * KC);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = threadIdx.x + k * 256;
+      const int p = i >> 2, part = i & 3;
+      const int row = p / HC, col = p - row * HC;
+      const int iy = iy0 + row, ix = ix0 + col;
+      const bool ok = p < HP && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+      const uint32_t off = (uint32_t)((pb + iy * a.Wi + ix) * cs + cb + part * E) * ES;
+      regs[k] = (TWO && second) ? IO::frag(r1, ok ? off : kOOB) : IO::frag(r0, ok ? off : kOOB);
+    }
+  };
+  auto lstore = [&](int bi) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = threadIdx.x + k * 256;
+      if ((i >> 2) < HP) buf[bi * HP * 4 + i] = regs[k];
+    }
+  };
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  f32x4_t acc[HGR][MT];
+#pragma unroll
+  for (int j = 0; j < HGR; ++j)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + ((size_t)ph.w_off * a.MTtot + mt0) * 64 + lane;
+  const int nt = ph.ntaps;
+  const int lbase = (wave * 16 + n) * 4 + g;  // this lane's chunk at halo pixel (0, 16w + n)
+
+  gfill(0);
+  lstore(0);
+  __syncthreads();
+  for (int c = 0; c < nsl; ++c) {
+    if (c + 1 < nsl) gfill(c + 1);
+    const raw* hb = buf + (c & 1) * HP * 4 + lbase;
+    raw wf[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(c * a.MTtot + m) * 64];  // chunk (tap 0, slice c)
+    for (int t = 0; t < nt; ++t) {
+      raw wn[MT];
+      if (t + 1 < nt) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) wn[m] = wp[(size_t)(((t + 1) * nsl + c) * a.MTtot + m) * 64];
+      }
+      const int to = s_toff[t] * 4;
+      raw xf[HGR];
+#pragma unroll
+      for (int j = 0; j < HGR; ++j) xf[j] = hb[to + j * HC * 4];
+#pragma unroll
+      for (int j = 0; j < HGR; ++j)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf[j], acc[j][m]);
+      if (t + 1 < nt) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) wf[m] = wn[m];
+      }
+    }
+    if (c + 1 < nsl) {  // buffer (c + 1) & 1 was last read before the previous barrier
+      lstore((c + 1) & 1);
+      __syncthreads();
+    }
+  }
+
+  // the fp32 plane as trailing K chunks (tap x plane), as in conv2d_mfma_kernel
+  if (ph.gchunks > 0) {
+    const raw* __restrict__ wg = wp + (size_t)ph.kchunks * a.MTtot * 64;
+    const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.geo[0], ((long long)(a.B - 1) * a.geo_bstride[0] + a.Hi * a.Wi) * 4);
+    const int pg0 = b * (int)a.geo_bstride[0];
+    for (int s = 0; s < ph.gchunks; ++s) {
+      raw wf[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) wf[m] = wg[(size_t)(s * a.MTtot + m) * 64];
+      float v[HGR][E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int t = s * KC + g * E + e;
+        const bool tv = t < nt;
+        const int dy = tv ? ph.tap[t][0] : 0, dx = tv ? ph.tap[t][1] : 0;
+#pragma unroll
+        for (int j = 0; j < HGR; ++j) {
+          const int iy = qy0 + j + dy, ix = qx0 + wave * 16 + n + dx;
+          const bool ok = tv && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+          v[j][e] = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(rg, ok ? (uint32_t)(pg0 + iy * a.Wi + ix) * 4u : kOOB, 0, 0));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < HGR; ++j) {
+        const raw xf = pack_vals<T>(v[j]);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf, acc[j][m]);
+      }
+    }
+  }
+
+  // epilogue (as conv2d_mfma_kernel)
+  typedef typename IO::quad quad;
+  const int up = a.post_up, us = a.post_up >> 1;
+  const long long nout = (long long)a.B * a.Ho * a.Wo * a.cout;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout * ES);
+  const __amdgpu_buffer_rsrc_t rpre = make_rsrc(a.res_pre ? a.res_pre : a.out, a.res_pre ? nout * ES : 0);
+  const __amdgpu_buffer_rsrc_t rpost = make_rsrc(a.res_post ? a.res_post : a.out, a.res_post ? nout / (up * up) * ES : 0);
+  float bias[MT][4];
+  bool cok[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int co = (mt0 + m) * 16 + g * 4;
+    cok[m] = co < a.cout;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[m][i] = a.bias[co + i];
+  }
+  const int qx = qx0 + wave * 16 + n;
+#pragma unroll
+  for (int j = 0; j < HGR; ++j) {
+    const int qy = qy0 + j;
+    const int oy = qy * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
+    const bool vok = qy < a.Hq && qx < a.Wq;
+    const int pout = (b * a.Ho + oy) * a.Wo + ox;
+    const int ppost = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
+    quad qpre[MT], qpost[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const bool ok = vok && cok[m];
+      const int co = (mt0 + m) * 16 + g * 4;
+      if (a.res_pre) qpre[m] = IO::ldq(rpre, ok ? (uint32_t)(pout * a.cout + co) * ES : kOOB);
+      if (a.res_post) qpost[m] = IO::ldq(rpost, ok ? (uint32_t)(ppost * a.cout + co) * ES : kOOB);
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      float r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = acc[j][m][i] + bias[m][i];
+      if (a.res_pre) IO::addq(qpre[m], r);
+      if (a.relu) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = fmaxf(r[i], 0.f);
+      }
+      if (a.res_post) IO::addq(qpost[m], r);
+      const uint32_t off = (uint32_t)(pout * a.cout + (mt0 + m) * 16 + g * 4) * ES;
+      IO::stq(ro, vok && cok[m] ? off : kOOB, r);
+    }
+  }
+}
+
+template <typename T, int MT>
+hipError_t launch_halo_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span) {
+  constexpr int KC = 4 * Stor<T>::E;
+  const int tx = (a.Wq + HGC - 1) / HGC, ty = (a.Hq + HGR - 1) / HGR;
+  const int nsl = (a.c0 + a.c1) / KC;
+  const size_t smem = 2 * (size_t)(HGR + span - 1) * (HGC + span - 1) * 4 * 16;
+  const long long nblk = (long long)tx * ty * a.B * a.nphase;
+  const dim3 grid((unsigned)nblk, (unsigned)(a.MTtot / MT));
+  if (a.c1 > 0)
+    hipLaunchKernelGGL((conv2d_halo_kernel<T, MT, true>), grid, dim3(256), smem, s, a, tx, ty, nsl, dmin, span);
+  else
+    hipLaunchKernelGGL((conv2d_halo_kernel<T, MT, false>), grid, dim3(256), smem, s, a, tx, ty, nsl, dmin, span);
+  return hipGetLastError();
+}
+
+// Returns hipErrorNotSupported when the halo kernel does not take the layer.
+template <typename T>
+hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a) {
+  constexpr int KC = 4 * Stor<T>::E;
+  // largest cout tile count (MTtot) the halo kernel takes: its B reuse pays off for narrow outputs,
+  // while wide outputs are bound by the A (weight) stream the gather kernel already amortises
+  static const int max_mt = [] {
+    const char* v = getenv("DAMVS_CONV2D_HALO");
+    return v ? atoi(v) : 2;
+  }();
+  if (a.MTtot > max_mt || a.in_stride != 1 || a.c0 % KC || a.c1 % KC || a.c0 + a.c1 < 2 * KC || a.MTtot < 2 || a.ngeo > 1)
+    return hipErrorNotSupported;
+  int dmin = 0, dmax = 0;
+  for (int p = 0; p < a.nphase; ++p)
+    for (int t = 0; t < a.ph[p].ntaps; ++t)
+      for (int d = 0; d < 2; ++d) {
+        dmin = a.ph[p].tap[t][d] < dmin ? a.ph[p].tap[t][d] : dmin;
+        dmax = a.ph[p].tap[t][d] > dmax ? a.ph[p].tap[t][d] : dmax;
+      }
+  const int span = dmax - dmin + 1;
+  if ((HGR + span - 1) * (HGC + span - 1) > 512) return hipErrorNotSupported;  // PER = 8 fill pieces a thread
+  // cout tile as wide as keeps about one wave per SIMD busy (the tile count is small for these layers)
+  const long long tiles = (long long)((a.Wq + HGC - 1) / HGC) * ((a.Hq + HGR - 1) / HGR) * a.B * a.nphase;
+  if (T_is_bf16<T>::value && a.MTtot % 8 == 0 && tiles * (a.MTtot / 8) >= 240) return launch_halo_t<T, 8>(s, a, dmin, span);
+  if (a.MTtot % 4 == 0 && tiles * (a.MTtot / 4) >= 240) return launch_halo_t<T, 4>(s, a, dmin, span);
+  if (a.MTtot % 2 == 0) return launch_halo_t<T, 2>(s, a, dmin, span);
+  return hipErrorNotSupported;
+}
+
 // True when the layer is a plain 3x3 stride-1 padding-1 conv with dense row-major taps.
 bool lds3_ok(const Conv2dArgs& a) {
   if (a.nphase != 1 || a.out_stride != 1 || a.in_stride != 1 || a.ph[0].ntaps != 9 || a.ngeo != 0 || a.c1 != 0 ||
@@ -623,8 +865,6 @@ hipError_t launch_mt(hipStream_t s, const Conv2dArgs& a) {
   return hipGetLastError();
 }
 
-template <typename T> struct T_is_bf16 { static constexpr bool value = false; };
-template <> struct T_is_bf16<bf16_t> { static constexpr bool value = true; };
 
 template <typename T>
 hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
@@ -645,7 +885,9 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
   }
   if (a.ngeo > 1) return hipErrorInvalidValue;  // the MFMA path takes at most one plane
   {
-    const hipError_t e = launch_lds2<T>(s, a);
+    hipError_t e = launch_lds2<T>(s, a);
+    if (e != hipErrorNotSupported) return e;
+    e = launch_halo<T>(s, a);
     if (e != hipErrorNotSupported) return e;
   }
   // Widest cout tile (each loaded input fragment feeds MT MFMAs) that still puts about one wave on

@@ -47,6 +47,9 @@ CASES = [
     (True, 3, 1, 1, 0, 16, 0, (), 8, True, False, 1),
     (True, 3, 1, 1, 0, 8, 0, (), 2, True, False, 0),                # rgb_decoder_output (cout 2)
     (False, 3, 1, 1, 0, 256, 0, (), 256, True, False, 0),           # wide layer (cout tiling)
+    (False, 3, 1, 1, 0, 32, 32, (64,), 64, True, True, 0),          # halo kernel: two inputs + plane
+    (True, 5, 2, 2, 1, 128, 0, (), 32, True, False, 1),             # halo kernel: k5 s2 phases, cout 32
+    (True, 3, 1, 1, 0, 64, 0, (), 128, True, True, 0),              # halo kernel: transposed k3 s1, MT 8
 ]
 
 

@@ -28,6 +28,9 @@ CASES = {
     "H geo conv1 32+32+g->64 s2": (False, 3, 2, 1, 0, 32, 32, 1, 64, True, 1, 592, 800, False, 0),
     "I geo conv1 8+g->16 s2 full": (False, 3, 2, 1, 0, 8, 0, 1, 16, True, 1, 1184, 1600, False, 0),
     "J geo conv2 16+g->16 r2": (False, 3, 1, 1, 0, 16, 0, 1, 16, True, 1, 592, 800, True, 0),
+    "K geo conv2 64+g->64 r4": (False, 3, 1, 1, 0, 64, 0, 1, 64, True, 1, 296, 400, True, 0),
+    "L dec4 128->64 k3 r4": (True, 3, 1, 1, 0, 128, 0, 0, 64, True, 1, 296, 400, False, 0),
+    "M dec5 64->32 k5s2 r2": (True, 5, 2, 2, 1, 64, 0, 0, 32, True, 1, 296, 400, False, 1),
 }
 
 
