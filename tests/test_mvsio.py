@@ -119,7 +119,10 @@ def test_eval_scenes_sample(tmp_path):
         cam[0] = E[v]
         cam[1, :3, :3] = K[v] * np.array([[4], [4], [1]], np.float32)  # files hold full-resolution K
         cam[1, 3, :2] = 425.0, 2.65
-        mvsio.write_cam(str(scan / "cams" / ("%08d_cam.txt" % v)), cam)
+        cp = str(scan / "cams" / ("%08d_cam.txt" % v))
+        mvsio.write_cam(cp, cam)
+        lines = open(cp).read().rstrip().split("\n")
+        open(cp, "w").write("\n".join(lines[:-1] + ["425.0 2.65"]) + "\n")  # DTU cams: min, interval
         Image.fromarray(np.full((H, W, 3), 40 * v, np.uint8)).save(str(scan / "images" / ("%08d.jpg" % v)))
     open(scan / "pair.txt", "w").write("3\n0\n2 1 9.0 2 8.0\n1\n2 0 9.0 2 8.0\n2\n1 0 9.0\n")
     ds = mvsio.EvalScenes(str(tmp_path), ["scan1"], nviews=3, ndepths=48, interval_scale=1.0, max_h=H, max_w=W)
