@@ -44,6 +44,16 @@ class DamvsConv2dDesc(ctypes.Structure):
                 ("c1", c_int), ("c1_at", c_int), ("ngeo", c_int), ("geo_at", c_int * 4), ("relu", c_int)]
 
 
+FUSION_MAX_SRC = 10
+_f = ctypes.c_float
+
+
+class DamvsFusionCams(ctypes.Structure):
+    _fields_ = [("kinv_ref", _f * 9), ("k_ref", _f * 9), ("einv_ref", _f * 16),
+                ("t_sr", (_f * 16) * FUSION_MAX_SRC), ("k_src", (_f * 9) * FUSION_MAX_SRC),
+                ("kinv_src", (_f * 9) * FUSION_MAX_SRC), ("t_rs", (_f * 16) * FUSION_MAX_SRC)]
+
+
 # (name, restype, argtypes) — the full exported surface of include/damvs.h
 SIGNATURES = (
     ("damvs_abi_version", c_int, ()),
@@ -76,6 +86,9 @@ SIGNATURES = (
     ("damvs_conv2d_forward", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                      ctypes.POINTER(c_void_p), ctypes.POINTER(ctypes.c_longlong), c_void_p, c_void_p,
                                      c_int, c_void_p)),
+    ("damvs_fusion_view", c_int, (c_void_p, c_int, c_int, c_int, c_void_p, ctypes.POINTER(c_void_p),
+                                  ctypes.POINTER(c_void_p), ctypes.POINTER(ctypes.c_float), ctypes.POINTER(DamvsFusionCams),
+                                  ctypes.c_double, ctypes.c_double, c_void_p, c_void_p, c_void_p)),
     ("damvs_conv2d_border_bias", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                          ctypes.POINTER(ctypes.c_float), c_void_p)),
 )

@@ -810,6 +810,45 @@ int damvs_conv2d_border_bias(void* stream, int dtype, int B, int H, int W, int c
                    "border_bias launch");
 }
 
+int damvs_fusion_view(void* stream, int H, int W, int nsrc, const float* depth_ref, const float* const* depth_src,
+                      const float* const* conf, const float* conf_thr, const damvs_fusion_cams* cams, double dist_base,
+                      double rel_diff_base, float* depth_avg, unsigned char* mask, float* xyz) {
+  if (!depth_ref || !depth_src || !cams || !depth_avg || !mask) return fail(DAMVS_E_ARG, "null argument");
+  if (H < 1 || W < 1 || (long long)H * W >= (1LL << 31)) return fail(DAMVS_E_SHAPE, "bad shape %d x %d", H, W);
+  if (nsrc < 1 || nsrc > kFusionMaxSrc) return fail(DAMVS_E_SHAPE, "nsrc %d not in [1, %d]", nsrc, kFusionMaxSrc);
+  if (conf && (!conf[0] || !conf[1] || !conf[2] || !conf_thr)) return fail(DAMVS_E_ARG, "incomplete confidence maps");
+  FusionArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.H = H;
+  a.W = W;
+  a.nsrc = nsrc;
+  a.depth_ref = depth_ref;
+  for (int v = 0; v < nsrc; ++v) {
+    if (!depth_src[v]) return fail(DAMVS_E_ARG, "null source depth %d", v);
+    a.depth_src[v] = depth_src[v];
+    std::memcpy(a.src[v].t_sr, cams->t_sr[v], sizeof(a.src[v].t_sr));
+    std::memcpy(a.src[v].k_src, cams->k_src[v], sizeof(a.src[v].k_src));
+    std::memcpy(a.src[v].kinv_src, cams->kinv_src[v], sizeof(a.src[v].kinv_src));
+    std::memcpy(a.src[v].t_rs, cams->t_rs[v], sizeof(a.src[v].t_rs));
+  }
+  if (conf)
+    for (int i = 0; i < 3; ++i) {
+      a.conf[i] = conf[i];
+      a.conf_thr[i] = conf_thr[i];
+    }
+  std::memcpy(a.kinv_ref, cams->kinv_ref, sizeof(a.kinv_ref));
+  std::memcpy(a.k_ref, cams->k_ref, sizeof(a.k_ref));
+  std::memcpy(a.einv_ref, cams->einv_ref, sizeof(a.einv_ref));
+  for (int i = 2; i <= 10; ++i) {
+    a.dist_thr[i - 2] = i * dist_base;
+    a.rel_thr[i - 2] = (float)(i * rel_diff_base);
+  }
+  a.depth_avg = depth_avg;
+  a.mask = mask;
+  a.xyz = xyz;
+  return hip_check(launch_fusion_view(static_cast<hipStream_t>(stream), a), "fusion_view launch");
+}
+
 int damvs_conv2d_destroy(damvs_conv2d* L) {
   if (!L) return DAMVS_OK;
   if (L->wpack) (void)hipFree(L->wpack);

@@ -133,6 +133,27 @@ struct BorderArgs {
 };
 hipError_t launch_border_bias(hipStream_t s, int store, const BorderArgs& a, int B, int H, int W, int cstored, int cout,
                               void* out);
+// ---------------------------------------------------------------- depth fusion (filter/dypcd.py)
+constexpr int kFusionMaxSrc = 10;  // the reference's masks run to i = 10 (dypcd.py:152)
+struct FusionCam {
+  float t_sr[16], k_src[9], kinv_src[9], t_rs[16];  // E_src inv(E_ref), K_src, inv(K_src), E_ref inv(E_src)
+};
+struct FusionArgs {
+  int H, W, nsrc;
+  const float* depth_ref;
+  const float* depth_src[kFusionMaxSrc];
+  const float* conf[3];  // final, stage-2, stage-1 confidences (nullptr: photometric test off)
+  float conf_thr[3];     // args.conf: stage-1, stage-2, stage-3 thresholds
+  float kinv_ref[9], k_ref[9], einv_ref[16];
+  FusionCam src[kFusionMaxSrc];
+  double dist_thr[9];    // i * dist_base, i = 2..10
+  float rel_thr[9];      // float32(i * rel_diff_base)
+  float* depth_avg;
+  unsigned char* mask;   // bit 0 photo, bit 1 geo, bit 2 final
+  float* xyz;            // world points of final pixels (0 elsewhere), or nullptr
+};
+hipError_t launch_fusion_view(hipStream_t s, const FusionArgs& a);
+
 bool conv_lds_disabled();  // DAMVS_CONV_NO_LDS=1 selects the global-gather conv kernel (A/B testing)
 bool conv_xpair_disabled();  // DAMVS_CONV_NO_XPAIR=1: single-parity deconv phases (A/B testing)
 hipError_t launch_prob_conv(hipStream_t s, int store, int B, int Cb, int D, int h, int w, const void* feat,

@@ -183,6 +183,27 @@ int damvs_conv2d_forward(const damvs_conv2d* layer, void* stream, int B, int Hi,
 int damvs_conv2d_border_bias(void* stream, int dtype, int B, int H, int W, int cout_stored, int cout, const float* corr,
                              void* out);
 
+/* ------------------------------------------------------------------ depth fusion (f4)
+ * One reference view of the reference's dynamic-consistency fusion (filter/dypcd.py:98-297,
+ * filter_depth per ref view): all maps [H][W] fp32 device buffers of one resolution. Camera
+ * products are float32, formed on the host exactly as numpy forms them for float32 matrices. */
+#define DAMVS_FUSION_MAX_SRC 10
+typedef struct {
+  float kinv_ref[9], k_ref[9], einv_ref[16];            /* inv(K_ref), K_ref, inv(E_ref) */
+  float t_sr[DAMVS_FUSION_MAX_SRC][16];                  /* E_src . inv(E_ref) */
+  float k_src[DAMVS_FUSION_MAX_SRC][9];
+  float kinv_src[DAMVS_FUSION_MAX_SRC][9];
+  float t_rs[DAMVS_FUSION_MAX_SRC][16];                  /* E_ref . inv(E_src) */
+} damvs_fusion_cams;
+
+/* conf: 3 maps (final-stage, stage-2, stage-1 confidence at the final resolution) or NULL (photo
+ * test off); conf_thr: args.conf[0..2] (stage-1, stage-2, stage-3). Outputs: depth_avg (averaged
+ * depth), mask (bit 0 photo, bit 1 geometric, bit 2 final), xyz [H][W][3] world points of final
+ * pixels (0 elsewhere; NULL: not written). 1 <= nsrc <= DAMVS_FUSION_MAX_SRC. */
+int damvs_fusion_view(void* stream, int H, int W, int nsrc, const float* depth_ref, const float* const* depth_src,
+                      const float* const* conf, const float* conf_thr, const damvs_fusion_cams* cams, double dist_base,
+                      double rel_diff_base, float* depth_avg, unsigned char* mask, float* xyz);
+
 #ifdef __cplusplus
 }
 #endif
