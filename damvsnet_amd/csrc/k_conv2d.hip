@@ -455,7 +455,10 @@ __global__ __launch_bounds__(256) void conv2d_lds_kernel(const Conv2dArgs a, int
 // the trailing K chunk(s) with global loads.
 constexpr int HGR = 4, HGC = 64;  // q-tile rows (one per group) x columns (16 per wave)
 
-template <typename T, int MT, bool TWO>
+// WM: waves stacked along the output channels (1: 4 waves side by side over the 4 column groups,
+// each with MT cout tiles x 4 rows; 2: a 2 x 2 wave grid, each wave MT cout tiles x 2 column groups x
+// 4 rows — half the A (weight) stream per MFMA for the wide layers).
+template <typename T, int MT, int WM, bool TWO>
 __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int nsl,
                                                           int dmin, int span) {
   typedef BufIO<T> IO;
@@ -477,7 +480,9 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
   const Conv2dPhase& ph = a.ph[L - tl * a.nphase];
   const int tx = tl % tiles_x, ty = (tl / tiles_x) % tiles_y, b = tl / (tiles_x * tiles_y);
   const int qy0 = ty * HGR, qx0 = tx * HGC;
-  const int mt0 = blockIdx.y * MT;
+  constexpr int WN = 4 / WM, CG = 4 / WN, GW = HGR * CG;  // waves along N, column groups and groups per wave
+  const int wm = (threadIdx.x >> 6) / WN, wn = (threadIdx.x >> 6) % WN;
+  const int mt0 = blockIdx.y * (MT * WM) + wm * MT;
 
   __shared__ int s_toff[32];  // tap offset inside the halo, in pixels
   if (threadIdx.x < 25)
@@ -514,14 +519,15 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
-  f32x4_t acc[HGR][MT];
+  f32x4_t acc[GW][MT];
 #pragma unroll
-  for (int j = 0; j < HGR; ++j)
+  for (int j = 0; j < GW; ++j)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + ((size_t)ph.w_off * a.MTtot + mt0) * 64 + lane;
   const int nt = ph.ntaps;
-  const int lbase = (wave * 16 + n) * 4 + g;  // this lane's chunk at halo pixel (0, 16w + n)
+  const int lbase = (wn * CG * 16 + n) * 4 + g;  // this lane's chunk at halo pixel (0, first column + n)
+  (void)wave;
 
   gfill(0);
   lstore(0);
@@ -539,11 +545,11 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
         for (int m = 0; m < MT; ++m) wn[m] = wp[(size_t)(((t + 1) * nsl + c) * a.MTtot + m) * 64];
       }
       const int to = s_toff[t] * 4;
-      raw xf[HGR];
+      raw xf[GW];  // group j: row j % HGR, column group j / HGR of this wave
 #pragma unroll
-      for (int j = 0; j < HGR; ++j) xf[j] = hb[to + j * HC * 4];
+      for (int j = 0; j < GW; ++j) xf[j] = hb[to + ((j % HGR) * HC + (j / HGR) * 16) * 4];
 #pragma unroll
-      for (int j = 0; j < HGR; ++j)
+      for (int j = 0; j < GW; ++j)
 #pragma unroll
         for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf[j], acc[j][m]);
       if (t + 1 < nt) {
@@ -566,22 +572,22 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
       raw wf[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) wf[m] = wg[(size_t)(s * a.MTtot + m) * 64];
-      float v[HGR][E];
+      float v[GW][E];
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int t = s * KC + g * E + e;
         const bool tv = t < nt;
         const int dy = tv ? ph.tap[t][0] : 0, dx = tv ? ph.tap[t][1] : 0;
 #pragma unroll
-        for (int j = 0; j < HGR; ++j) {
-          const int iy = qy0 + j + dy, ix = qx0 + wave * 16 + n + dx;
+        for (int j = 0; j < GW; ++j) {
+          const int iy = qy0 + j % HGR + dy, ix = qx0 + (wn * CG + j / HGR) * 16 + n + dx;
           const bool ok = tv && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
           v[j][e] = __uint_as_float(
               __builtin_amdgcn_raw_buffer_load_b32(rg, ok ? (uint32_t)(pg0 + iy * a.Wi + ix) * 4u : kOOB, 0, 0));
         }
       }
 #pragma unroll
-      for (int j = 0; j < HGR; ++j) {
+      for (int j = 0; j < GW; ++j) {
         const raw xf = pack_vals<T>(v[j]);
 #pragma unroll
         for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf, acc[j][m]);
@@ -605,10 +611,9 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
 #pragma unroll
     for (int i = 0; i < 4; ++i) bias[m][i] = a.bias[co + i];
   }
-  const int qx = qx0 + wave * 16 + n;
 #pragma unroll
-  for (int j = 0; j < HGR; ++j) {
-    const int qy = qy0 + j;
+  for (int j = 0; j < GW; ++j) {
+    const int qy = qy0 + j % HGR, qx = qx0 + (wn * CG + j / HGR) * 16 + n;
     const int oy = qy * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
     const bool vok = qy < a.Hq && qx < a.Wq;
     const int pout = (b * a.Ho + oy) * a.Wo + ox;
@@ -638,18 +643,18 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
   }
 }
 
-template <typename T, int MT>
+template <typename T, int MT, int WM>
 hipError_t launch_halo_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span) {
   constexpr int KC = 4 * Stor<T>::E;
   const int tx = (a.Wq + HGC - 1) / HGC, ty = (a.Hq + HGR - 1) / HGR;
   const int nsl = (a.c0 + a.c1) / KC;
   const size_t smem = 2 * (size_t)(HGR + span - 1) * (HGC + span - 1) * 4 * 16;
   const long long nblk = (long long)tx * ty * a.B * a.nphase;
-  const dim3 grid((unsigned)nblk, (unsigned)(a.MTtot / MT));
+  const dim3 grid((unsigned)nblk, (unsigned)(a.MTtot / (MT * WM)));
   if (a.c1 > 0)
-    hipLaunchKernelGGL((conv2d_halo_kernel<T, MT, true>), grid, dim3(256), smem, s, a, tx, ty, nsl, dmin, span);
+    hipLaunchKernelGGL((conv2d_halo_kernel<T, MT, WM, true>), grid, dim3(256), smem, s, a, tx, ty, nsl, dmin, span);
   else
-    hipLaunchKernelGGL((conv2d_halo_kernel<T, MT, false>), grid, dim3(256), smem, s, a, tx, ty, nsl, dmin, span);
+    hipLaunchKernelGGL((conv2d_halo_kernel<T, MT, WM, false>), grid, dim3(256), smem, s, a, tx, ty, nsl, dmin, span);
   return hipGetLastError();
 }
 
@@ -663,7 +668,7 @@ hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a) {
     const char* v = getenv("DAMVS_CONV2D_HALO");
     return v ? atoi(v) : 2;
   }();
-  if (a.MTtot > max_mt || a.in_stride != 1 || a.c0 % KC || a.c1 % KC || a.c0 + a.c1 < 2 * KC || a.MTtot < 2 || a.ngeo > 1)
+  if (a.MTtot > max_mt || (a.MTtot > 2 && a.MTtot < 8) || a.in_stride != 1 || a.c0 % KC || a.c1 % KC || a.c0 + a.c1 < 2 * KC || a.MTtot < 2 || a.ngeo > 1)
     return hipErrorNotSupported;
   int dmin = 0, dmax = 0;
   for (int p = 0; p < a.nphase; ++p)
@@ -676,9 +681,13 @@ hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a) {
   if ((HGR + span - 1) * (HGC + span - 1) > 512) return hipErrorNotSupported;  // PER = 8 fill pieces a thread
   // cout tile as wide as keeps about one wave per SIMD busy (the tile count is small for these layers)
   const long long tiles = (long long)((a.Wq + HGC - 1) / HGC) * ((a.Hq + HGR - 1) / HGR) * a.B * a.nphase;
-  if (T_is_bf16<T>::value && a.MTtot % 8 == 0 && tiles * (a.MTtot / 8) >= 240) return launch_halo_t<T, 8>(s, a, dmin, span);
-  if (a.MTtot % 4 == 0 && tiles * (a.MTtot / 4) >= 240) return launch_halo_t<T, 4>(s, a, dmin, span);
-  if (a.MTtot % 2 == 0) return launch_halo_t<T, 2>(s, a, dmin, span);
+  if (a.MTtot >= 8) {  // wide: 2 x 2 wave grid, 4 cout tiles x 128 pixels a wave
+    if (a.MTtot % 8 == 0) return launch_halo_t<T, 4, 2>(s, a, dmin, span);
+    return hipErrorNotSupported;
+  }
+  if (T_is_bf16<T>::value && a.MTtot % 8 == 0 && tiles * (a.MTtot / 8) >= 240) return launch_halo_t<T, 8, 1>(s, a, dmin, span);
+  if (a.MTtot % 4 == 0 && tiles * (a.MTtot / 4) >= 240) return launch_halo_t<T, 4, 1>(s, a, dmin, span);
+  if (a.MTtot % 2 == 0) return launch_halo_t<T, 2, 1>(s, a, dmin, span);
   return hipErrorNotSupported;
 }
 
