@@ -68,6 +68,7 @@ struct damvs_stage {
   int C = 0, base = 0, mode = 0, dtype = 0, device = 0;
   LayerPlan L[10];
   float* prob_w = nullptr;  // device [kd][kh][kw][c]
+  void* prob_pack = nullptr;  // bf16, base 8: banded MFMA form of the prob conv (pack_prob_banded)
   float k1[32] = {0};
   float s1 = 0, t1 = 0, s2 = 0, t2 = 0;
 };
@@ -462,6 +463,31 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
       for (int t = 0; t < 27; ++t) pw[(size_t)t * b + c] = cr->prob_weight[(size_t)c * 27 + t];
     rc = upload(pw.data(), pw.size() * 4, reinterpret_cast<void**>(&st->prob_w));
   }
+  if (rc == DAMVS_OK && dtype == DAMVS_BF16 && b == 8) {
+    // Prob conv (Conv3d(8, 1, k3), models/module.py:530) as one 16 x K MFMA operand per 32-wide K
+    // chunk: rows m = 16 consecutive output planes d0 + m, K = (input plane d0 - 1 + r, r = 0..17;
+    // ky; kx; channel), entry W[kd = r - m][ky][kx][c] when 0 <= kd <= 2 (banded), else 0. The fp32
+    // weights are split into bf16 hi + lo parts (two MFMAs) so the logits keep ~16 mantissa bits.
+    const int nch = kProbChunks;
+    std::vector<uint16_t> pk((size_t)nch * 2 * 64 * 8, 0);
+    for (int s = 0; s < nch; ++s)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int e = 0; e < 8; ++e) {
+          const int m = lane & 15, k = s * 32 + (lane >> 4) * 8 + e, tp = k / 8, c = k % 8;
+          float v = 0.f;
+          if (tp < 18 * 9) {
+            const int kd = tp / 9 - m;
+            if (kd >= 0 && kd <= 2) v = cr->prob_weight[(size_t)c * 27 + kd * 9 + tp % 9];
+          }
+          const uint16_t hi = to_bf16(v);
+          float hf;
+          const uint32_t hb = (uint32_t)hi << 16;
+          std::memcpy(&hf, &hb, 4);
+          pk[(((size_t)s * 2 + 0) * 64 + lane) * 8 + e] = hi;
+          pk[(((size_t)s * 2 + 1) * 64 + lane) * 8 + e] = to_bf16(v - hf);
+        }
+    rc = upload(pk.data(), pk.size() * 2, &st->prob_pack);
+  }
   if (rc == DAMVS_OK && agg_mode == DAMVS_AGG_ADAPTIVE) {
     std::vector<float> sc1, sh1, sc2, sh2;
     rc = fold_bn(aw->bn1, 1, sc1, sh1);
@@ -494,6 +520,7 @@ int damvs_stage_destroy(damvs_stage* st) {
     if (P.bias) (void)hipFree(P.bias);
   }
   if (st->prob_w) (void)hipFree(st->prob_w);
+  if (st->prob_pack) (void)hipFree(st->prob_pack);
   delete st;
   return DAMVS_OK;
 }
@@ -536,6 +563,13 @@ int damvs_stage_forward(const damvs_stage* st, void* stream, int B, int N, int D
   DAMVS_TRY(hip_check(launch_warp_aggregate(s, st->dtype, st->mode, wa, blk), "warp_aggregate launch"));
   DAMVS_TRY(run_unet(st, s, B, D, h, w, ws + W.vol, ws, W));
   const void* feat = ws + W.c[0];
+  // banded MFMA prob conv + regression: TA-bound on its per-tap B loads, it beats the LDS-tiled VALU
+  // kernel only with >= 2 plane groups (measured at cfgC: stage 2 -26 us, stage 3 +50 us)
+  if (st->prob_pack && D >= 32 && D <= 64 && !prob_mfma_disabled()) {
+    DAMVS_TRY(hip_check(launch_prob_mfma(s, B, D, h, w, feat, st->prob_pack, prob_init, hyps, depth, conf, var, prob),
+                        "prob_mfma launch"));
+    return DAMVS_OK;
+  }
   if (prob_regress_smem_bytes(st->dtype, st->base, D) <= 160 * 1024) {  // fused: logits stay in LDS
     DAMVS_TRY(hip_check(launch_prob_regress(s, st->dtype, B, st->base, D, h, w, feat, st->prob_w, prob_init, hyps,
                                             depth, conf, var, prob),

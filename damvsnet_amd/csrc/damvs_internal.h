@@ -155,13 +155,19 @@ struct FusionArgs {
 hipError_t launch_fusion_view(hipStream_t s, const FusionArgs& a);
 
 bool conv_lds_disabled();  // DAMVS_CONV_NO_LDS=1 selects the global-gather conv kernel (A/B testing)
-bool conv_xpair_disabled();  // DAMVS_CONV_NO_XPAIR=1: single-parity deconv phases (A/B testing)
+bool conv_xpair_disabled();  // x-pair deconv phases only with DAMVS_CONV_XPAIR=1
 hipError_t launch_prob_conv(hipStream_t s, int store, int B, int Cb, int D, int h, int w, const void* feat,
                             const float* wprob, const float* prob_init, float* logits);
 hipError_t launch_prob_regress(hipStream_t s, int store, int B, int Cb, int D, int h, int w, const void* feat,
                                const float* wprob, const float* prob_init, const float* hyps, float* depth,
                                float* conf, float* var, float* prob);
 size_t prob_regress_smem_bytes(int store, int Cb, int D);
+// banded-MFMA prob conv + regression (bf16 storage, base 8, D <= 64): apack from pack_prob_banded
+constexpr int kProbChunks = (18 * 9 * 8 + 31) / 32;  // 18 input planes x 9 taps x 8 channels, 32-wide chunks
+hipError_t launch_prob_mfma(hipStream_t s, int B, int D, int h, int w, const void* feat, const void* apack,
+                            const float* prob_init, const float* hyps, float* depth, float* conf, float* var,
+                            float* prob);
+bool prob_mfma_disabled();  // DAMVS_PROB_MFMA=0 (A/B testing)
 hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float* logits, const float* hyps,
                           float* depth, float* conf, float* var, float* prob);
 

@@ -603,10 +603,12 @@ hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a0) {
   return store == ST_BF16 ? launch_t<bf16_t>(s, a) : launch_t<float>(s, a);
 }
 
+// Off by default: at D = 64 (cfgD/E stage 1) repeated bf16 U-Net runs with the x-pair conv11 are
+// not bitwise reproducible (root cause open); DAMVS_CONV_XPAIR=1 enables it.
 bool conv_xpair_disabled() {
   static const bool off = [] {
-    const char* v = getenv("DAMVS_CONV_NO_XPAIR");
-    return v && v[0] == '1';
+    const char* v = getenv("DAMVS_CONV_XPAIR");
+    return !(v && v[0] == '1');
   }();
   return off;
 }

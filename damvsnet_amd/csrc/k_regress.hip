@@ -259,6 +259,120 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
   var[(size_t)b * hw + pix] = 3.f * sqrtf(vs);
 }
 
+// Prob conv on MFMA (bf16 storage, 8 channels). Cout = 1 would leave 15 of 16 MFMA rows empty, so
+// the rows are 16 consecutive OUTPUT PLANES instead: with K = (input plane r = 0..17 relative to
+// d0 - 1, ky, kx, channel), the 16 x K operand is the banded weight matrix W[r - m] (capi.cpp,
+// pack_prob_banded; fp32 weights as bf16 hi + lo, two MFMAs per chunk). Lane group g of a B
+// fragment is one tap = one 16-byte voxel (8 channels), so every B load is a coalesced 16-pixel row
+// segment. Wave w owns planes [16w, 16w+16) of a 64-pixel row segment (4 N-tiles reuse each A
+// fragment); the D logits of the block's 64 pixels meet in LDS and 64 threads run the regression.
+constexpr int kPR = 4;  // 16-pixel N-tiles per wave
+
+__global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int w, int tiles_x,
+                                                        const bf16_t* __restrict__ feat, const uint4* __restrict__ apack,
+                                                        const float* __restrict__ prob_init,
+                                                        const float* __restrict__ hyps, float* __restrict__ depth,
+                                                        float* __restrict__ conf, float* __restrict__ var,
+                                                        float* __restrict__ prob) {
+  __shared__ float lg[64 * 64];  // [plane][pixel of the block]
+  const int tx = blockIdx.x % tiles_x, yb = blockIdx.x / tiles_x;
+  const int y = yb % h, b = yb / h;
+  const int x0 = tx * 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const int d0 = wave * 16;
+  const __amdgpu_buffer_rsrc_t rf = make_rsrc(feat, (long long)B * D * h * w * 8 * 2);
+  const uint4* ap = apack + lane;
+  f32x4_t acc[kPR];
+#pragma unroll
+  for (int r = 0; r < kPR; ++r) acc[r] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  auto fetch = [&](int s, uint4& ah, uint4& al, uint4* xb) {
+    ah = ap[(size_t)(2 * s) * 64];
+    al = ap[(size_t)(2 * s + 1) * 64];
+    const int tp = s * 4 + g;  // this lane group's tap
+    const int rr = tp / 9, t9 = tp - rr * 9;
+    const int iz = d0 - 1 + rr, yy = y + t9 / 3 - 1, dx = t9 % 3 - 1;
+    const bool okz = tp < 18 * 9 && (unsigned)iz < (unsigned)D && (unsigned)yy < (unsigned)h;
+    const int rowbase = ((b * D + iz) * h + yy) * w;
+#pragma unroll
+    for (int r = 0; r < kPR; ++r) {
+      const int xx = x0 + r * 16 + n + dx;
+      const bool ok = okz && (unsigned)xx < (unsigned)w;
+      xb[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rf, ok ? (uint32_t)(rowbase + xx) * 16u : kOOB, 0, 0));
+    }
+  };
+  // only input planes d0 - 1 .. min(d0 + 16, D - 1) exist: skip the chunks past them (D = 8: 21 of 41)
+  const int nplanes = min(18, D - d0 + 1);
+  const int nch = min(kProbChunks, (nplanes * 9 + 3) / 4);
+  uint4 ah, al, xb[kPR];
+  fetch(0, ah, al, xb);
+  for (int s = 0; s < nch; ++s) {
+    uint4 nh, nl, nb[kPR];
+    if (s + 1 < nch) fetch(s + 1, nh, nl, nb);
+#pragma unroll
+    for (int r = 0; r < kPR; ++r) {
+      acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ah), __builtin_bit_cast(bf16x8_t, xb[r]),
+                                                       acc[r], 0, 0, 0);
+      acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, al), __builtin_bit_cast(bf16x8_t, xb[r]),
+                                                       acc[r], 0, 0, 0);
+    }
+    if (s + 1 < nch) {
+      ah = nh;
+      al = nl;
+#pragma unroll
+      for (int r = 0; r < kPR; ++r) xb[r] = nb[r];
+    }
+  }
+  // lane (n, g) holds planes d0 + 4g .. +3 of pixel r * 16 + n
+  const size_t hw = (size_t)h * w;
+#pragma unroll
+  for (int r = 0; r < kPR; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int d = d0 + 4 * g + i, px = r * 16 + n, x = x0 + px;
+      if (d < D) {
+        float l = acc[r][i];
+        if (prob_init && x < w) l += prob_init[((size_t)b * D + d) * hw + (size_t)y * w + x];
+        lg[d * 64 + px] = l;
+      }
+    }
+  __syncthreads();
+  const int t = threadIdx.x, x = x0 + t;
+  if (t >= 64 || x >= w) return;
+  const size_t pix = (size_t)y * w + x;
+  const float* hy = hyps + (size_t)b * D * hw + pix;
+  float* lcol = lg + t;
+  float mx = -INFINITY;
+  for (int d = 0; d < D; ++d) mx = fmaxf(mx, lcol[d * 64]);
+  float sum = 0.f;
+  for (int d = 0; d < D; ++d) {
+    const float e = expf(lcol[d * 64] - mx);
+    lcol[d * 64] = e;
+    sum += e;
+  }
+  float dep = 0.f, idx = 0.f;
+  for (int d = 0; d < D; ++d) {
+    const float pr = lcol[d * 64] / sum;
+    lcol[d * 64] = pr;
+    dep += pr * hy[(size_t)d * hw];
+    idx += pr * (float)d;
+  }
+  int ii = (int)idx;
+  ii = ii < 0 ? 0 : (ii > D - 1 ? D - 1 : ii);
+  float c = 0.f, vs = 0.f;
+  float* po = prob ? prob + (size_t)b * D * hw + pix : nullptr;
+  for (int d = 0; d < D; ++d) {
+    const float pr = lcol[d * 64];
+    const float df = hy[(size_t)d * hw] - dep;
+    vs += df * df * pr;
+    if (d >= ii - 1 && d <= ii + 2) c += pr;
+    if (po) po[(size_t)d * hw] = pr;
+  }
+  depth[(size_t)b * hw + pix] = dep;
+  conf[(size_t)b * hw + pix] = c;
+  var[(size_t)b * hw + pix] = 3.f * sqrtf(vs);
+}
+
 template <typename T, int CB>
 size_t prob_regress_smem(int D) {
   constexpr int CH = CB / Stor<T>::E;
@@ -343,6 +457,31 @@ hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float
   hipLaunchKernelGGL(regress_kernel, dim3((hw + 255) / 256, B), dim3(256), 0, s, B, D, hw, logits, hyps, depth, conf,
                      var, prob);
   return hipGetLastError();
+}
+
+}  // namespace damvs
+
+namespace damvs {
+
+hipError_t launch_prob_mfma(hipStream_t s, int B, int D, int h, int w, const void* feat, const void* apack,
+                            const float* prob_init, const float* hyps, float* depth, float* conf, float* var,
+                            float* prob) {
+  if (D < 1 || D > 64) return hipErrorInvalidValue;
+  if ((long long)B * D * h * w * 16 >= (1LL << 32)) return hipErrorInvalidValue;  // 32-bit buffer offsets
+  const int tiles_x = (w + 63) / 64, ngroups = (D + 15) / 16;
+  const long long nblk = (long long)tiles_x * h * B;
+  hipLaunchKernelGGL(prob_mfma_kernel, dim3((unsigned)nblk), dim3(64 * ngroups), 0, s, B, D, h, w, tiles_x,
+                     reinterpret_cast<const bf16_t*>(feat), reinterpret_cast<const uint4*>(apack), prob_init, hyps,
+                     depth, conf, var, prob);
+  return hipGetLastError();
+}
+
+bool prob_mfma_disabled() {
+  static const bool off = [] {
+    const char* v = getenv("DAMVS_PROB_MFMA");
+    return v && v[0] == '0';
+  }();
+  return off;
 }
 
 }  // namespace damvs

@@ -129,6 +129,29 @@ def test_warp_aggregate_channel_blocked_layout(C, dtype):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("s,D", [(0, 48), (1, 32), (0, 64)])
+def test_prob_mfma_vs_split_path(s, D):
+    """bf16 stage forward (banded-MFMA prob conv + regression, k_regress.hip) against the split path on
+    the same U-Net output (damvs_costreg_logits: fp32-weight VALU prob conv, then damvs_regress):
+    they differ only in the prob conv's weight split (bf16 hi + lo) and summation order."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine, regress
+    C = (32, 16, 8)[s]
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    feats, P, hyps = depthnet_inputs(B=2, N=3, H=32, W=80, D=D, stage_idx=s, C=C)
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.bfloat16,
+                      torch.device(DEV))
+    nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats]
+    depth, conf, var, prob = eng.forward(nhwc, cuda(P), cuda(hyps))
+    logits = eng.costreg_logits(eng.warp_aggregate(nhwc, cuda(P), cuda(hyps)))
+    d2, c2, v2, p2 = regress(logits, cuda(hyps))
+    assert rel_max(np_(depth), np_(d2)) < 1e-4
+    assert np.abs(np_(conf) - np_(c2)).max() < 2e-3
+    assert np.abs(np_(prob) - np_(p2)).max() < 2e-3
+    assert rel_max(np_(var), np_(v2)) < 2e-2
+
+
 # ----------------------------------------------------------------------------- CostRegNet (A6)
 
 @pytest.mark.parametrize("s", [0, 1, 2])
@@ -361,6 +384,27 @@ def test_depthnet_deterministic():
         b = net.DepthNet(2, [cuda(f) for f in feats], cuda(P), cuda(hyps), 8, net.cost_regularization[2])
     for k in ("depth", "photometric_confidence", "variance", "prob_volume"):
         assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("s,D", [(0, 64), (0, 48), (1, 32), (2, 8)])
+def test_costreg_bf16_deterministic(s, D):
+    """Repeated bf16 U-Net + prob conv runs on one volume are bitwise identical (cfgD/E's D = 64
+    included: this caught an in-place hazard in an earlier conv11 variant)."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine
+    C = (32, 16, 8)[s]
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    feats, P, hyps = depthnet_inputs(B=2, N=3, H=32, W=80, D=D, stage_idx=s, C=C)
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.bfloat16,
+                      torch.device(DEV))
+    nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats]
+    vol = eng.warp_aggregate(nhwc, cuda(P), cuda(hyps))
+    outs = [eng.costreg_logits(vol).clone() for _ in range(4)]
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    d = [eng.forward(nhwc, cuda(P), cuda(hyps))[0].clone() for _ in range(3)]
+    assert torch.equal(d[1], d[0]) and torch.equal(d[2], d[0])
 
 
 def test_forward_batch2_matches_batch1():
