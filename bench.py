@@ -80,6 +80,26 @@ class StageTimer:
         return out
 
 
+def latency_b1(net, imgs, proj, dv, ins, steps=10):
+    """Single-view latency (SURVEY.md 8(d) 'B=1 for latency'): the first batch element alone, HIP
+    events around each step and phase; reported beside the throughput line, never as `value`."""
+    one = lambda x: x[:1] if torch.is_tensor(x) else {k: v[:1] for k, v in x.items()}
+    imgs, proj, dv, ins = one(imgs), one(proj), one(dv), one(ins)
+    with torch.no_grad():
+        for _ in range(2):
+            net(imgs, proj, dv, ins)
+        torch.cuda.synchronize()
+        timer = StageTimer()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(steps):
+            net(imgs, proj, dv, ins, stage_hook=timer)
+        e1.record()
+        torch.cuda.synchronize()
+    return {"ms_per_map": round(e0.elapsed_time(e1) / steps, 3),
+            "ms_per_stage": {k: round(statistics.mean(v), 3) for k, v in timer.per_phase_ms().items()}}
+
+
 def warp_roofline(net, imgs, proj, dv, stage, dtype, iters=20):
     """Time the product-path fused warp+aggregation kernel of one stage alone (HIP events on the
     stream it is launched on): channel-blocked features and cameras prepared outside the loop.
@@ -119,12 +139,12 @@ def warp_roofline(net, imgs, proj, dv, stage, dtype, iters=20):
     return ms, alg
 
 
-def pmc_traffic(config, kernel_substr="warp_aggregate"):
+def pmc_traffic(config, batch, kernel_substr="warp_aggregate"):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC summary
     (profiles/<round>/pmc_*.json, produced by tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE,
     the gfx950 correction of MI355X_MICROARCH.md), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_%s_%s.json" % (kernel_substr, config))))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_%s_%s_b%d.json" % (kernel_substr, config, batch))))
     if not files:
         return None
     with open(files[-1]) as f:
@@ -166,7 +186,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfgC", choices=sorted(CONFIGS))
-    ap.add_argument("--batch", type=int, default=1, help="depth maps (reference views) per GPU per step")
+    ap.add_argument("--batch", type=int, default=4,
+                    help="depth maps (reference views) per GPU per step; default 4 = the reference's own "
+                         "test batch (scripts/test.sh:25 --batch_size=4), SURVEY.md 8(d) 'B=4 for throughput'")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--frontend", default="hip", choices=["hip", "torch"], help="2D front-end implementation")
     ap.add_argument("--cpu-budget", type=float, default=60.0)
@@ -210,9 +232,10 @@ def main():
 
     result = None
     if rank == 0:
+        lat = latency_b1(net, imgs, proj, dv, ins)
         ms, alg = warp_roofline(net, imgs, proj, dv, 1, dtype)
         achieved = alg / (ms * 1e-3) / 1e9
-        tr = pmc_traffic(args.config)
+        tr = pmc_traffic(args.config, args.batch)
         result = {
             "metric": "depth maps/sec (full CascadeMVSNet forward)",
             "value": round(maps / elapsed, 4),
@@ -231,6 +254,7 @@ def main():
                        "global_batch": args.batch * world, "height": H, "width": W, "views": N,
                        "ndepths": list(nd), "parallelism": "replicas x%d (reference views sharded over ranks)" % world},
             "ms_per_stage": phases,
+            "latency_b1": lat,
             "roofline": {"kernel": "warp_aggregate stage2 (fused homography warp + adaptive aggregation)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr["bytes"] if tr else None,

@@ -24,7 +24,7 @@ def run_pass(counter, args, tmp):
     d = os.path.join(tmp, counter)
     cmd = ["rocprofv3", "--pmc", counter, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run", "--",
            sys.executable, os.path.join(REPO, "tools", "kbench.py"), "--kernel", args.kernel, "--stage",
-           str(args.stage), "--config", args.config, "--iters", "3"]
+           str(args.stage), "--config", args.config, "--iters", "3", "--batch", str(args.batch)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd="/tmp",
                        env=dict(os.environ, TMPDIR="/tmp"))
     if r.returncode != 0:
@@ -45,18 +45,19 @@ def main():
     ap.add_argument("--kernel", default="warp", choices=sorted(KNAME))
     ap.add_argument("--stage", type=int, default=2)
     ap.add_argument("--config", default="cfgC")
+    ap.add_argument("--batch", type=int, default=4, help="reference views per launch (bench.py's default batch)")
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r01"))
     ap.add_argument("--tmp", default=os.path.join(REPO, "gpurun_out", "pmc_traffic"))
     args = ap.parse_args()
     fetch_kb, d1, n1 = run_pass("FETCH_SIZE", args, args.tmp)
     write_kb, d2, n2 = run_pass("WRITE_SIZE", args, args.tmp)
     hbm = (2.0 * fetch_kb + write_kb) * 1024.0
-    res = {"kernel": KNAME[args.kernel], "stage": args.stage, "config": args.config,
+    res = {"kernel": KNAME[args.kernel], "stage": args.stage, "config": args.config, "batch": args.batch,
            "FETCH_SIZE_kb_raw": fetch_kb, "WRITE_SIZE_kb": write_kb, "launches": [n1, n2],
            "hbm_bytes_per_launch": hbm, "profiled_duration_ns": [d1, d2],
            "correction": "FETCH_SIZE x2 (gfx950: reads 1/2 of wide coalesced stream bytes), WRITE_SIZE as is"}
     os.makedirs(args.out, exist_ok=True)
-    path = os.path.join(args.out, "pmc_%s_%s.json" % (KNAME[args.kernel], args.config))
+    path = os.path.join(args.out, "pmc_%s_%s_b%d.json" % (KNAME[args.kernel], args.config, args.batch))
     with open(path, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))

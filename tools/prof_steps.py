@@ -1,14 +1,19 @@
 """Per-kernel time inside the timed bench steps from a rocprofv3 kernel trace (csv).
 
-Steps are delimited by the stage-3 regression kernel (3 regress launches per forward)."""
+Steps are delimited by the regression kernels (one prob_regress / prob_mfma launch per stage, 3 per
+forward). Also prints the average of the last `roofline_iters` launches of the roofline kernel
+(bench.py's warp_roofline loop runs last), to check against the bench line's roofline.ms_per_launch."""
 import collections
 import csv
 import sys
 
 
-def main(path, warmup=2, steps=5, top=40):
+ROOFLINE_KERNEL = "warp_aggregate_kernel<unsigned short, 16,"  # stage 2 (C = 16), bf16
+
+
+def main(path, warmup=2, steps=5, top=40, roofline_iters=20):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    reg = [i for i, r in enumerate(rows) if "regress_kernel" in r["Kernel_Name"]]
+    reg = [i for i, r in enumerate(rows) if "regress_kernel" in r["Kernel_Name"] or "prob_mfma_kernel" in r["Kernel_Name"]]
     ends = reg[2::3]  # last regress of each forward
     first = ends[warmup - 1] + 1
     last = ends[warmup + steps - 1]
@@ -25,6 +30,10 @@ def main(path, warmup=2, steps=5, top=40):
     for name, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
         print("%9.1f us/step %4d/step avg %8.1f us  %5.1f%%  %s" % (t / steps, n // steps, t / n, 100 * t / steps / busy,
                                                                    name[:100]))
+    rl = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows if ROOFLINE_KERNEL in r["Kernel_Name"]]
+    if len(rl) >= roofline_iters:
+        print("roofline kernel (%s...): last %d launches avg %.4f ms" % (ROOFLINE_KERNEL, roofline_iters,
+                                                                       sum(rl[-roofline_iters:]) / roofline_iters))
 
 
 if __name__ == "__main__":
