@@ -322,7 +322,7 @@ ConvArgs conv_args(const damvs_stage* st, int li, int B, const Shapes& S, int li
   a.relu = 1;
   a.nphase = P.nphase;
   std::memcpy(a.ph, P.ph, sizeof(a.ph));
-  if (P.kind == DECONV_S2 && P.wpack_pair && !conv_xpair_disabled()) {
+  if (P.kind == DECONV_S2 && P.wpack_pair && P.cout == 8 && !conv_xpair_disabled()) {
     a.xpair = 1;
     a.wpack = P.wpack_pair;
     a.nphase = P.nphase_pair;

@@ -90,6 +90,41 @@ __device__ __forceinline__ void finish4(const ConvArgs& a, __amdgpu_buffer_rsrc_
   (void)rr;
 }
 
+// One whole 8-channel voxel record (16 B bf16 / 32 B f32): load into floats / store from floats.
+template <typename T> struct Vox8;
+template <> struct Vox8<bf16_t> {
+  __device__ __forceinline__ static void add(__amdgpu_buffer_rsrc_t r, uint32_t off, float* v) {
+    const uint4 q = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] += __uint_as_float(w[i] << 16);
+      v[2 * i + 1] += __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ __forceinline__ static void store(__amdgpu_buffer_rsrc_t r, uint32_t off, const float* v) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, make_uint4(w[0], w[1], w[2], w[3])), r, off, 0, 0);
+  }
+};
+template <> struct Vox8<float> {
+  __device__ __forceinline__ static void add(__amdgpu_buffer_rsrc_t r, uint32_t off, float* v) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 q = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * h, 0, 0));
+      v[4 * h] += q.x; v[4 * h + 1] += q.y; v[4 * h + 2] += q.z; v[4 * h + 3] += q.w;
+    }
+  }
+  __device__ __forceinline__ static void store(__amdgpu_buffer_rsrc_t r, uint32_t off, const float* v) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(v4u32_t, make_float4(v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3])), r, off + 16 * h, 0, 0);
+  }
+};
+
 // Global-gather implicit GEMM (strided convs, deconv phases, and any layer the LDS variant does not
 // take). 32-bit incremental indexing: no divisions in the K loop, magic-number division for the
 // voxel decomposition, range-checked buffer loads for the zero padding.
@@ -178,6 +213,65 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int 
   const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * ES;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.resid ? a.resid : a.out, a.resid ? nout : 0);
+  if constexpr (XP) {
+    // Cout = 8: lane group g + 1 hands its 4 channels to group g (g even), which then owns the whole
+    // 8-channel record of output x = 2 qx + (g >> 1): one 16-byte (bf16) skip load and store per voxel.
+    const bool lead = (g & 1) == 0;
+    float b8[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b8[i] = a.bias[i];
+#pragma unroll
+    for (int j = 0; j < kGroups; ++j) {
+      float r[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        r[i] = acc[j][0][i];
+        r[4 + i] = __shfl_down(acc[j][0][i], 16);
+      }
+      if (!lead) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        r[i] += b8[i];
+        if (a.relu) r[i] = fmaxf(r[i], 0.f);
+      }
+      const uint32_t off = valid[j] ? (uint32_t)(pout[j] * 8) * ES : kOOB;
+      if (a.resid) Vox8<T>::add(rr, off, r);
+      Vox8<T>::store(ro, off, r);
+    }
+    return;
+  }
+  if constexpr (sizeof(T) == 2) {
+    if (a.resid && (a.Cout & 7) == 0) {
+      // bf16 in-place skip: lane group g + 1 hands its 4 channels to group g (g even), which loads / stores the
+      // 8 channels as one 16-byte access. (The 8-byte-per-lane form of this in-place skip epilogue
+      // lost the skip term of lane group 3's even channels in a few hundred voxels per launch on
+      // gfx950, nondeterministically: tools/diag_unet_repro.py)
+      const bool lead = (g & 1) == 0;
+#pragma unroll
+      for (int j = 0; j < kGroups; ++j) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          float r[8];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            r[i] = acc[j][m][i];
+            r[4 + i] = __shfl_down(acc[j][m][i], 16);
+          }
+          const int co = m * 16 + g * 4;
+          if (!lead || co >= a.Cout) continue;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            r[i] += a.bias[co + i];
+            if (a.relu) r[i] = fmaxf(r[i], 0.f);
+          }
+          const uint32_t off = valid[j] ? (uint32_t)(pout[j] * a.Cout + co) * ES : kOOB;
+          if (a.resid) Vox8<T>::add(rr, off, r);
+          Vox8<T>::store(ro, off, r);
+        }
+      }
+      return;
+    }
+  }
   float bias[MT][4];
   bool cok[MT];
   const int cg = XP ? (g & 1) * 4 : g * 4;  // first channel of this lane group's 4
@@ -560,7 +654,7 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
   const int nq = (int)((Qtot + per_block - 1) / per_block);
   dim3 grid((unsigned)(nq * a.nphase));
   if (a.xpair) {
-    if (a.MT != 1 || a.Cout > 8) return hipErrorInvalidValue;
+    if (a.MT != 1 || a.Cout != 8) return hipErrorInvalidValue;
     hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, true>), grid, dim3(256), 0, s, a, nq);
     return hipGetLastError();
   }
@@ -603,12 +697,11 @@ hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a0) {
   return store == ST_BF16 ? launch_t<bf16_t>(s, a) : launch_t<float>(s, a);
 }
 
-// Off by default: at D = 64 (cfgD/E stage 1) repeated bf16 U-Net runs with the x-pair conv11 are
-// not bitwise reproducible (root cause open); DAMVS_CONV_XPAIR=1 enables it.
+// The x-pair conv11 runs by default; DAMVS_CONV_XPAIR=0 selects the 8-phase form (A/B and diagnosis).
 bool conv_xpair_disabled() {
   static const bool off = [] {
     const char* v = getenv("DAMVS_CONV_XPAIR");
-    return !(v && v[0] == '1');
+    return v && v[0] == '0';
   }();
   return off;
 }

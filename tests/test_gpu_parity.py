@@ -386,21 +386,23 @@ def test_depthnet_deterministic():
         assert torch.equal(a[k], b[k]), k
 
 
-@pytest.mark.parametrize("s,D", [(0, 64), (0, 48), (1, 32), (2, 8)])
-def test_costreg_bf16_deterministic(s, D):
-    """Repeated bf16 U-Net + prob conv runs on one volume are bitwise identical (cfgD/E's D = 64
-    included: this caught an in-place hazard in an earlier conv11 variant)."""
+@pytest.mark.parametrize("s,D,B,H,W", [(0, 64, 2, 32, 80), (0, 48, 2, 32, 80), (1, 32, 2, 32, 80), (2, 8, 2, 32, 80),
+                                         (1, 64, 4, 64, 160)])
+def test_costreg_bf16_deterministic(s, D, B, H, W):
+    """Repeated bf16 U-Net + prob conv runs on one volume are bitwise identical. The last case is
+    the one where the 8-byte-per-lane in-place skip epilogue of the deconvs lost skip terms
+    (conv9, lane group 3, a few hundred voxels per run; tools/diag_unet_repro.py)."""
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import StageEngine
     C = (32, 16, 8)[s]
     net = CascadeMVSNet(ndepths=[48, 32, 8])
     net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
-    feats, P, hyps = depthnet_inputs(B=2, N=3, H=32, W=80, D=D, stage_idx=s, C=C)
+    feats, P, hyps = depthnet_inputs(B=B, N=3, H=H, W=W, D=D, stage_idx=s, C=C)
     eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.bfloat16,
                       torch.device(DEV))
     nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats]
     vol = eng.warp_aggregate(nhwc, cuda(P), cuda(hyps))
-    outs = [eng.costreg_logits(vol).clone() for _ in range(4)]
+    outs = [eng.costreg_logits(vol).clone() for _ in range(5)]
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
     d = [eng.forward(nhwc, cuda(P), cuda(hyps))[0].clone() for _ in range(3)]

@@ -2,7 +2,7 @@
 the caller): runs costreg_logits repeatedly on one volume and reports, per run, which regions of
 the workspace (the U-Net's level buffers) and the logits differ from run 0.
 
-  DAMVS_CONV_XPAIR=1 python tools/diag_xpair.py [--D 64 --stage 0 --runs 6]
+  DAMVS_CONV_XPAIR=1 python tools/diag_unet_repro.py [--D 64 --stage 0 --runs 6]
 """
 import argparse
 import os
@@ -23,7 +23,8 @@ def main():
     ap.add_argument("--B", type=int, default=2)
     ap.add_argument("--H", type=int, default=32)
     ap.add_argument("--W", type=int, default=80)
-    ap.add_argument("--save", default=None, help="torch.save the c0 snapshots (bf16) here")
+    ap.add_argument("--save", default=None, help="torch.save the --buf snapshots (bf16) here")
+    ap.add_argument("--buf", default="c0")
     args = ap.parse_args()
     from common import model_state, depthnet_inputs
     from damvsnet_amd import _capi
@@ -61,8 +62,8 @@ def main():
         o += al(z)
     print("workspace layout:", [(nm, a0, a1) for nm, a0, a1 in layout], flush=True)
     if args.save:
-        a0, a1 = [(x, y) for nm, x, y in layout if nm == "c0"][0]
-        torch.save([sw[a0:a1].cpu().view(torch.bfloat16).reshape(B, D, h, w, bb) for _, sw in snaps], args.save)
+        a0, a1 = [(x, y) for nm, x, y in layout if nm == args.buf][0]
+        torch.save([sw[a0:a0 + (a1 - a0) // B].cpu().view(torch.bfloat16) for _, sw in snaps], args.save)  # batch 0
     l0, w0 = snaps[0]
     region = 1 << 16
     for r, (l, wsr) in enumerate(snaps[1:], 1):
