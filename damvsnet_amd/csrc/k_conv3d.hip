@@ -595,8 +595,161 @@ __global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, 
   }
 }
 
+// z-sliding row-pair variant (bf16 conv0): a block owns an 8-row x TX-column output window over ZC
+// consecutive z-planes and streams the input through a 4-plane ring of (8+2) x (TX+2) x CIN halo
+// planes in LDS. Each output plane needs one new input plane, fetched into registers while the
+// current plane's MFMAs run and written to the ring slot freed by the plane before (one barrier
+// per plane): HBM/L2 re-reads drop from 2.1x (6x10x18 halo per 4x8x16 tile) to ~1.66x and the
+// fill latency is hidden behind compute instead of preceding it. Same K order, weights
+// (pack_layer_pair) and accumulation chain as conv3d_lds_pair_kernel: identical results.
+// Wave w owns row pair (y0 + 2w, y0 + 2w + 1); lane column n the output x = x0 + 16 xg + n.
+template <int CIN, int TXG>
+__global__ __launch_bounds__(256) void conv3d_zslide_pair_kernel(const ConvArgs a, int tiles_x, int tiles_y,
+                                                                 int nzc, int zc, int ntiles) {
+  typedef uint4 raw;
+  constexpr int E = 8, KC = 32, CH = CIN / E;
+  constexpr int TX = 16 * TXG, PW = TX + 2, PH = LTH + 2;
+  constexpr int PLANE = PH * PW * CH;  // 16-byte chunks per halo plane
+  constexpr int NLD = (PLANE + 255) / 256;
+  constexpr int KCHUNKS = 36 * CIN / KC;
+  static_assert(KC % CIN == 0 || CIN % KC == 0, "chunking");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  raw* ring = reinterpret_cast<raw*>(smem);
+
+  const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
+  int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tx = tt % tiles_x; tt /= tiles_x;
+  const int ty = tt % tiles_y; tt /= tiles_y;
+  const int tz = tt % nzc;
+  const int b = tt / nzc;
+  const int x0 = tx * TX, y0 = ty * LTH, zb = tz * zc;
+  const int zend = min(zb + zc, a.Do);
+
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * 2);
+  auto load_plane = [&](int iz, raw* v) {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * 256;
+      const int row = c / (PW * CH), col = c - row * (PW * CH);
+      const int iy = y0 - 1 + row, ix = x0 - 1 + col / CH;
+      const bool ok = c < PLANE && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+                      (unsigned)ix < (unsigned)a.Wi;
+      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16u;
+      v[i] = BufIO<bf16_t>::frag(rin, ok ? off : kOOB);
+    }
+  };
+  auto store_plane = [&](int iz, const raw* v) {
+    raw* dst = ring + ((iz + 4) & 3) * PLANE;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * 256;
+      if (c < PLANE) dst[c] = v[i];
+    }
+  };
+  // the layer's A fragments stay in registers for all ZC planes (18 / 36 VGPR quads for CIN 16 / 32)
+  raw wreg[KCHUNKS];
+  {
+    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack_pair) + (threadIdx.x & 63);
+#pragma unroll
+    for (int s = 0; s < KCHUNKS; ++s) wreg[s] = wsrc[(size_t)s * 64];
+  }
+  raw pa[NLD], pb[NLD];
+#pragma unroll
+  for (int p = -1; p <= 1; ++p) {
+    load_plane(zb + p, pa);
+    store_plane(zb + p, pa);
+  }
+  if (zb + 1 < zend) load_plane(zb + 2, pa);  // two planes ahead from here on
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const int gi = (g * E) / CIN, gc = (g * E) % CIN / E;
+  const int lbase = (2 * wave * PW + n) * CH + gc;  // this lane's chunk at tap (dy' = 0, dx = 0)
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * 2;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
+  const int co = (g & 1) * 4, r = g >> 1;
+  float bias[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias[i] = a.bias[co + i];
+  const int oy = y0 + 2 * wave + r;
+
+  // one output plane: plane z + 2 (in `cur`, loaded one plane earlier) goes to the ring after the
+  // MFMAs; plane z + 3 is fetched into `nxt` before them, so each load has two planes of cover
+  auto step = [&](int z, raw* cur, raw* nxt) {
+    if (z + 2 < zend) load_plane(z + 3, nxt);
+    const raw* pl[3] = {ring + ((z + 3) & 3) * PLANE + lbase, ring + ((z + 4) & 3) * PLANE + lbase,
+                        ring + ((z + 5) & 3) * PLANE + lbase};
+    f32x4_t acc[TXG];
+#pragma unroll
+    for (int xg = 0; xg < TXG; ++xg) acc[xg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KCHUNKS; ++s) {
+      const raw wf = wreg[s];
+      const int kt = (s * KC) / CIN, kc = ((s * KC) % CIN) / E;
+      const int dz = kt / 12;  // uniform over the chunk's taps (12 taps per dz, 1/2/4 taps per chunk)
+      auto toff = [](int t) { return (((t / 3) % 4) * PW + t % 3) * CH; };
+      int off = toff(kt);
+      if (KC > CIN) {
+        off = gi == 1 ? toff(kt + 1) : off;
+        off = gi == 2 ? toff(kt + 2) : off;
+        off = gi == 3 ? toff(kt + 3) : off;
+      }
+      const raw* src = pl[dz] + off + kc;
+#pragma unroll
+      for (int xg = 0; xg < TXG; ++xg) Frag<bf16_t>::mma(wf, src[16 * xg * CH], acc[xg]);
+    }
+#pragma unroll
+    for (int xg = 0; xg < TXG; ++xg) {
+      const int ox = x0 + 16 * xg + n;
+      const bool vok = oy < a.Ho && ox < a.Wo && co < a.Cout;
+      const uint32_t off = (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * a.Cout + co) * 2u;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = acc[xg][i] + bias[i];
+        if (a.relu) v[i] = fmaxf(v[i], 0.f);
+      }
+      BufIO<bf16_t>::stq(ro, vok ? off : kOOB, v);
+    }
+    if (z + 1 < zend) store_plane(z + 2, cur);  // slot of plane z - 2, last read before the previous barrier
+    __syncthreads();
+  };
+  for (int z = zb; z < zend; z += 2) {
+    step(z, pa, pb);
+    if (z + 1 < zend) step(z + 1, pb, pa);
+  }
+}
+
+bool zslide_disabled() {  // read per call: tests flip it between launches
+  const char* v = getenv("DAMVS_CONV_NO_ZSLIDE");
+  return v && v[0] == '1';
+}
+
+template <int CIN, int TXG>
+hipError_t launch_zslide_pair_t(hipStream_t s, const ConvArgs& a) {
+  constexpr int PLANE = (LTH + 2) * (16 * TXG + 2) * (CIN / 8);
+  const size_t smem = 4 * PLANE * 16;
+  static const int zc = [] {
+    const char* v = getenv("DAMVS_ZSLIDE_ZC");
+    const int z = v ? atoi(v) : 16;  // measured: 16 beats 8 and 32 over stages 1-2 at B=4
+    return z > 0 ? z : 16;
+  }();
+  const int tx = (a.Wo + 16 * TXG - 1) / (16 * TXG), ty = (a.Ho + LTH - 1) / LTH, nzc = (a.Do + zc - 1) / zc;
+  const long long nt = (long long)tx * ty * nzc * a.B;
+  hipLaunchKernelGGL((conv3d_zslide_pair_kernel<CIN, TXG>), dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc,
+                     (int)nt);
+  return hipGetLastError();
+}
+
 template <typename T, int CIN>
 hipError_t launch_lds_pair_t(hipStream_t s, const ConvArgs& a) {
+  if constexpr (sizeof(T) == 2) {
+    if (!a.resid && !zslide_disabled()) {
+      if constexpr (CIN == 32) return launch_zslide_pair_t<CIN, 1>(s, a);
+      else return launch_zslide_pair_t<CIN, 2>(s, a);
+    }
+  }
   const size_t smem = lds_tile_bytes<T, CIN>();
   auto k = conv3d_lds_pair_kernel<T, CIN>;
   if (smem > 64 * 1024) {

@@ -409,6 +409,27 @@ def test_costreg_bf16_deterministic(s, D, B, H, W):
     assert torch.equal(d[1], d[0]) and torch.equal(d[2], d[0])
 
 
+@pytest.mark.parametrize("s,D,H,W", [(0, 48, 40, 72), (1, 24, 40, 72), (2, 8, 48, 96), (1, 32, 32, 80)])
+def test_conv0_zslide_matches_tile_kernel(s, D, H, W, monkeypatch):
+    """conv0's z-sliding ring-buffer kernel (bf16) against the 4x8x16-tile row-pair kernel: same K
+    order and accumulation chain, so the U-Net logits agree bitwise (partial x tiles included)."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine
+    C = (32, 16, 8)[s]
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    feats, P, hyps = depthnet_inputs(B=2, N=3, H=H, W=W, D=D, stage_idx=s, C=C)
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.bfloat16,
+                      torch.device(DEV))
+    nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats]
+    vol = eng.warp_aggregate(nhwc, cuda(P), cuda(hyps))
+    monkeypatch.setenv("DAMVS_CONV_NO_ZSLIDE", "0")
+    a = eng.costreg_logits(vol).clone()
+    monkeypatch.setenv("DAMVS_CONV_NO_ZSLIDE", "1")
+    b = eng.costreg_logits(vol).clone()
+    assert torch.equal(a, b)
+
+
 def test_forward_batch2_matches_batch1():
     """B=2 of the same sample equals B=1 (batch independence of the HIP path)."""
     torch.backends.cudnn.deterministic = True
