@@ -1,10 +1,14 @@
-"""Per-launch durations of the damvs kernels in the last timed step of a rocprofv3 kernel trace."""
+"""Per-launch durations of the damvs kernels in one forward of a rocprofv3 kernel trace
+(argv[2] = forward index, default the last).
+
+  python tools/prof_damvs_launches.py run_kernel_trace.csv [forward]
+"""
 import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-key = "prob_regress_kernel" if any("prob_regress_kernel" in r["Kernel_Name"] for r in rows) else "regress_kernel"
-reg = [i for i, r in enumerate(rows) if key in r["Kernel_Name"]]
+# one regression launch per stage (prob_mfma_kernel or prob_regress_kernel), 3 per forward
+reg = [i for i, r in enumerate(rows) if "regress_kernel" in r["Kernel_Name"] or "prob_mfma_kernel" in r["Kernel_Name"]]
 ends = reg[2::3]
 step = int(sys.argv[2]) if len(sys.argv) > 2 else len(ends) - 1
 sel = rows[ends[step - 1] + 1:ends[step] + 1]
