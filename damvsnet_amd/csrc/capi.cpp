@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -673,6 +674,7 @@ int damvs_hypotheses(void* stream, int B, int D, int H, int W, int scale, const 
 struct damvs_conv2d {
   damvs_conv2d_desc d;
   int dtype = 0, cout_pad = 0, cout_store = 0, MTtot = 0, nphase = 0, kchunk_k = 0;
+  int xpair = 0;  // x-parity-pair phases (build_phases_2d_xpair / pack_2d_xpair)
   Conv2dPhase ph[4];
   void* wpack = nullptr;
   float* wgeo = nullptr;
@@ -725,6 +727,49 @@ int build_phases_2d(damvs_conv2d* L) {
   return DAMVS_OK;
 }
 
+// ConvTranspose2d stride 2 with cout = 8 as 2 phases (output row parity ry): the 16 MFMA rows are
+// (output x parity px, channel), and the taps are (input row offsets of ry) x (the union of the input
+// x offsets of both parities). A row whose parity does not use an x offset gets zero weights. Per
+// output pixel pair this is |offs[ry]| * |union| taps instead of |offs[ry]| * (|offs[0]| + |offs[1]|)
+// over two phases with half the MFMA rows empty, and the 16 channels of an x pair are one 32-byte
+// store. wtap keeps the ky * K part; pack_2d_xpair resolves kx per row parity.
+int build_phases_2d_xpair(damvs_conv2d* L) {
+  const damvs_conv2d_desc& d = L->d;
+  const int K = d.kernel, p = d.padding;
+  std::memset(L->ph, 0, sizeof(L->ph));
+  std::vector<int> offs[2], ks[2];
+  for (int r = 0; r < 2; ++r)
+    for (int k = 0; k < K; ++k)
+      if (((r + p - k) % 2 + 2) % 2 == 0) { offs[r].push_back((r + p - k) / 2); ks[r].push_back(k); }
+  std::vector<int> xo;  // union of x offsets over both parities, ascending
+  for (int r = 0; r < 2; ++r)
+    for (int o : offs[r])
+      if (std::find(xo.begin(), xo.end(), o) == xo.end()) xo.push_back(o);
+  std::sort(xo.begin(), xo.end());
+  L->nphase = 2;
+  int w_off = 0;
+  for (int ry = 0; ry < 2; ++ry) {
+    Conv2dPhase& P = L->ph[ry];
+    P.py = ry;
+    P.px = 0;
+    int t = 0;
+    for (size_t a = 0; a < offs[ry].size(); ++a)
+      for (int dx : xo) {
+        if (t >= 25) return fail(DAMVS_E_SHAPE, "more than 25 taps per phase");
+        P.tap[t][0] = (signed char)offs[ry][a];
+        P.tap[t][1] = (signed char)dx;
+        P.wtap[t] = (signed char)(ks[ry][a] * K);
+        ++t;
+      }
+    P.ntaps = t;
+    P.kchunks = (t * (d.c0 + d.c1) + L->kchunk_k - 1) / L->kchunk_k;
+    P.gchunks = 0;
+    P.w_off = w_off;
+    w_off += P.kchunks;
+  }
+  return DAMVS_OK;
+}
+
 float wget(const damvs_conv2d_desc& d, const float* W, int co, int wc, int wt) {
   const int KK = d.kernel * d.kernel;
   return d.transposed ? W[((size_t)wc * d.cout + co) * KK + wt] : W[((size_t)co * d.cin + wc) * KK + wt];
@@ -754,6 +799,40 @@ void pack_2d(const damvs_conv2d* L, const float* W, std::vector<S>& out, S (*cvt
             out.push_back(cvt(v));
           }
   }
+}
+
+// A rows = (x parity px = row >> 3, channel co = row & 7); kx from the parity's tap list.
+template <typename S>
+void pack_2d_xpair(const damvs_conv2d* L, const float* W, std::vector<S>& out, S (*cvt)(float)) {
+  const damvs_conv2d_desc& d = L->d;
+  const int E = L->kchunk_k / 4, ctot = d.c0 + d.c1, K = d.kernel, p = d.padding;
+  auto kx_of = [&](int px, int dx) {
+    for (int k = 0; k < K; ++k)
+      if (((px + p - k) % 2 + 2) % 2 == 0 && (px + p - k) / 2 == dx) return k;
+    return -1;
+  };
+  for (int ph = 0; ph < L->nphase; ++ph) {
+    const Conv2dPhase& P = L->ph[ph];
+    for (int s = 0; s < P.kchunks; ++s)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int e = 0; e < E; ++e) {
+          const int row = lane & 15, px = row >> 3, co = row & 7;
+          const int k = s * L->kchunk_k + (lane >> 4) * E + e;
+          const int t = k / ctot, ci = k % ctot;
+          float v = 0.f;
+          if (co < d.cout && t < P.ntaps) {
+            const int kx = kx_of(px, P.tap[t][1]);
+            const int wc = ci < d.c0 ? d.c0_at + ci : d.c1_at + (ci - d.c0);
+            if (kx >= 0) v = wget(d, W, co, wc, (unsigned char)P.wtap[t] + kx);
+          }
+          out.push_back(cvt(v));
+        }
+  }
+}
+
+bool conv2d_xpair_disabled() {
+  const char* v = getenv("DAMVS_CONV2D_XPAIR");
+  return v && v[0] == '0';
 }
 
 void conv2d_out(const damvs_conv2d* L, int Hi, int Wi, int* Ho, int* Wo) {
@@ -794,15 +873,18 @@ int damvs_conv2d_create(const damvs_conv2d_desc* desc, const float* weight, cons
   L->MTtot = (d.cout + 15) / 16;
   L->cout_pad = L->MTtot * 16;
   L->cout_store = (d.cout + 3) / 4 * 4;
-  int rc = build_phases_2d(L);
+  L->xpair = d.transposed && d.stride == 2 && d.cout == 8 && d.ngeo == 0 && d.c0 + d.c1 > 0 && !conv2d_xpair_disabled();
+  int rc = L->xpair ? build_phases_2d_xpair(L) : build_phases_2d(L);
   if (rc == DAMVS_OK && d.c0 + d.c1 + d.ngeo > 0) {
     if (dtype == DAMVS_BF16) {
       std::vector<uint16_t> pk;
-      pack_2d<uint16_t>(L, weight, pk, cvt_bf16);
+      if (L->xpair) pack_2d_xpair<uint16_t>(L, weight, pk, cvt_bf16);
+      else pack_2d<uint16_t>(L, weight, pk, cvt_bf16);
       rc = upload(pk.data(), pk.size() * 2, &L->wpack);
     } else {
       std::vector<float> pk;
-      pack_2d<float>(L, weight, pk, cvt_f32);
+      if (L->xpair) pack_2d_xpair<float>(L, weight, pk, cvt_f32);
+      else pack_2d<float>(L, weight, pk, cvt_f32);
       rc = upload(pk.data(), pk.size() * 4, &L->wpack);
     }
   }
@@ -951,6 +1033,7 @@ int damvs_conv2d_forward(const damvs_conv2d* L, void* stream, int B, int Hi, int
   if (res_post && (a.Ho % a.post_up || a.Wo % a.post_up)) return fail(DAMVS_E_SHAPE, "bad upsample shape");
   a.relu = d.relu;
   a.nphase = L->nphase;
+  a.xpair = L->xpair;
   a.div_wq = make_fastdiv(a.Wq);
   a.div_hq = make_fastdiv(a.Hq);
   std::memcpy(a.ph, L->ph, sizeof(a.ph));

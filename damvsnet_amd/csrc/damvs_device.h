@@ -114,4 +114,39 @@ template <> struct BufIO<bf16_t> {
   }
 };
 
+// One whole 8-channel voxel / pixel record (16 B bf16 / 32 B f32): load into floats / store from floats.
+template <typename T> struct Vox8;
+template <> struct Vox8<bf16_t> {
+  __device__ __forceinline__ static void add(__amdgpu_buffer_rsrc_t r, uint32_t off, float* v) {
+    const uint4 q = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] += __uint_as_float(w[i] << 16);
+      v[2 * i + 1] += __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ __forceinline__ static void store(__amdgpu_buffer_rsrc_t r, uint32_t off, const float* v) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, make_uint4(w[0], w[1], w[2], w[3])), r, off, 0, 0);
+  }
+};
+template <> struct Vox8<float> {
+  __device__ __forceinline__ static void add(__amdgpu_buffer_rsrc_t r, uint32_t off, float* v) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 q = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * h, 0, 0));
+      v[4 * h] += q.x; v[4 * h + 1] += q.y; v[4 * h + 2] += q.z; v[4 * h + 3] += q.w;
+    }
+  }
+  __device__ __forceinline__ static void store(__amdgpu_buffer_rsrc_t r, uint32_t off, const float* v) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(v4u32_t, make_float4(v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3])), r, off + 16 * h, 0, 0);
+  }
+};
+
 }  // namespace damvs

@@ -111,6 +111,7 @@ struct Conv2dArgs {
   int cout, cout_pad, MTtot;
   int B, Hi, Wi, Hq, Wq, Ho, Wo, in_stride, out_stride, relu, nphase;
   FastDiv div_wq, div_hq;   // output-grid decomposition q -> (b, qy, qx)
+  int xpair;                // transposed stride 2, cout 8: both x parities in one phase's 16 MFMA rows
   Conv2dPhase ph[4];
 };
 

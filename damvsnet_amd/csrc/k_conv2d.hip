@@ -104,7 +104,10 @@ __device__ __forceinline__ void tail4(const Conv2dArgs& a, int b, int oy, int ox
 // tiles. K runs over (tap, concatenated channel) in chunks of KC = 4E, then over (tap, plane) for
 // the fp32 planes. Index arithmetic is 32-bit and incremental (no divisions in the K loop): the
 // kernel is otherwise VALU-bound on address math for the thin full-resolution layers.
-template <typename T, int MT, bool TWO>
+// XP (a.xpair layers: ConvTranspose stride 2, cout 8): MFMA row r = (x parity r >> 3, channel r & 7),
+// so lane group g holds channels (g & 1) * 4 of output x = 2 qx + (g >> 1); group g + 1 hands its 4
+// channels to group g (g even), which loads / stores the pixel's whole 8-channel record.
+template <typename T, int MT, bool TWO, bool XP = false>
 __global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, int nqblk) {
   typedef BufIO<T> IO;
   typedef typename IO::raw raw;
@@ -141,7 +144,7 @@ __global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, in
     ys[j] = qy * a.in_stride;
     xs[j] = qx * a.in_stride;
     pin[j] = (b * a.Hi + ys[j]) * a.Wi + xs[j];
-    const int oy = qy * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
+    const int oy = qy * a.out_stride + ph.py, ox = qx * a.out_stride + (XP ? (g >> 1) : ph.px);
     pout[j] = (b * a.Ho + oy) * a.Wo + ox;
     const int us = a.post_up >> 1;  // post_up is 1 or 2
     ppost[j] = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
@@ -267,6 +270,31 @@ __global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, in
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout * ES);
   const __amdgpu_buffer_rsrc_t rpre = make_rsrc(a.res_pre ? a.res_pre : a.out, a.res_pre ? nout * ES : 0);
   const __amdgpu_buffer_rsrc_t rpost = make_rsrc(a.res_post ? a.res_post : a.out, a.res_post ? nout / (up * up) * ES : 0);
+  if constexpr (XP) {
+    const bool lead = (g & 1) == 0;
+    float b8[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b8[i] = a.bias[i];
+#pragma unroll
+    for (int j = 0; j < kG2; ++j) {
+      float r[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        r[i] = acc[j][0][i] + b8[i];
+        r[4 + i] = __shfl_down(acc[j][0][i], 16) + b8[4 + i];
+      }
+      if (!lead) continue;
+      const bool ok = valid[j];
+      if (a.res_pre) Vox8<T>::add(rpre, ok ? (uint32_t)(pout[j] * 8) * ES : kOOB, r);
+      if (a.relu) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = fmaxf(r[i], 0.f);
+      }
+      if (a.res_post) Vox8<T>::add(rpost, ok ? (uint32_t)(ppost[j] * 8) * ES : kOOB, r);
+      Vox8<T>::store(ro, ok ? (uint32_t)(pout[j] * 8) * ES : kOOB, r);
+    }
+    return;
+  }
   float bias[MT][4];
   bool cok[MT];
 #pragma unroll
@@ -893,6 +921,17 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
     return hipGetLastError();
   }
   if (a.ngeo > 1) return hipErrorInvalidValue;  // the MFMA path takes at most one plane
+  if (a.xpair) {  // x-pair phases (built at layer creation): only the XP gather kernel runs them
+    if (a.cout != 8 || a.MTtot != 1 || a.ngeo != 0 || a.nphase != 2) return hipErrorInvalidValue;
+    const long long Qtot = (long long)a.B * a.Hq * a.Wq;
+    const int nq = (int)((Qtot + 4LL * kG2 * 16 - 1) / (4LL * kG2 * 16));
+    const dim3 grid((unsigned)(nq * a.nphase), 1);
+    if (a.c1 > 0)
+      hipLaunchKernelGGL((conv2d_mfma_kernel<T, 1, true, true>), grid, dim3(256), 0, s, a, nq);
+    else
+      hipLaunchKernelGGL((conv2d_mfma_kernel<T, 1, false, true>), grid, dim3(256), 0, s, a, nq);
+    return hipGetLastError();
+  }
   {
     hipError_t e = launch_lds2<T>(s, a);
     if (e != hipErrorNotSupported) return e;

@@ -90,41 +90,6 @@ __device__ __forceinline__ void finish4(const ConvArgs& a, __amdgpu_buffer_rsrc_
   (void)rr;
 }
 
-// One whole 8-channel voxel record (16 B bf16 / 32 B f32): load into floats / store from floats.
-template <typename T> struct Vox8;
-template <> struct Vox8<bf16_t> {
-  __device__ __forceinline__ static void add(__amdgpu_buffer_rsrc_t r, uint32_t off, float* v) {
-    const uint4 q = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[2 * i] += __uint_as_float(w[i] << 16);
-      v[2 * i + 1] += __uint_as_float(w[i] & 0xffff0000u);
-    }
-  }
-  __device__ __forceinline__ static void store(__amdgpu_buffer_rsrc_t r, uint32_t off, const float* v) {
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, make_uint4(w[0], w[1], w[2], w[3])), r, off, 0, 0);
-  }
-};
-template <> struct Vox8<float> {
-  __device__ __forceinline__ static void add(__amdgpu_buffer_rsrc_t r, uint32_t off, float* v) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const float4 q = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * h, 0, 0));
-      v[4 * h] += q.x; v[4 * h + 1] += q.y; v[4 * h + 2] += q.z; v[4 * h + 3] += q.w;
-    }
-  }
-  __device__ __forceinline__ static void store(__amdgpu_buffer_rsrc_t r, uint32_t off, const float* v) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-      __builtin_amdgcn_raw_buffer_store_b128(
-          __builtin_bit_cast(v4u32_t, make_float4(v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3])), r, off + 16 * h, 0, 0);
-  }
-};
-
 // Global-gather implicit GEMM (strided convs, deconv phases, and any layer the LDS variant does not
 // take). 32-bit incremental indexing: no divisions in the K loop, magic-number division for the
 // voxel decomposition, range-checked buffer loads for the zero padding.
@@ -180,6 +145,12 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int 
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * ES;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.resid ? a.resid : a.out, a.resid ? nout : 0);
+  constexpr bool kSkip16 = sizeof(T) == 2;
+  const bool skip16 = kSkip16 && a.resid && (a.Cout & 7) == 0;
+
   const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * a.Cin * ES);
   const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + (size_t)ph.w_off * 64 + lane;
   const int HW = a.Hi * a.Wi;
@@ -210,9 +181,6 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int 
     if (ci >= a.Cin) { ci -= a.Cin; ++t; }
   }
 
-  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * ES;
-  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
-  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.resid ? a.resid : a.out, a.resid ? nout : 0);
   if constexpr (XP) {
     // Cout = 8: lane group g + 1 hands its 4 channels to group g (g even), which then owns the whole
     // 8-channel record of output x = 2 qx + (g >> 1): one 16-byte (bf16) skip load and store per voxel.
@@ -240,8 +208,8 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int 
     }
     return;
   }
-  if constexpr (sizeof(T) == 2) {
-    if (a.resid && (a.Cout & 7) == 0) {
+  if constexpr (kSkip16) {
+    if (skip16) {
       // bf16 in-place skip: lane group g + 1 hands its 4 channels to group g (g even), which loads / stores the
       // 8 channels as one 16-byte access. (The 8-byte-per-lane form of this in-place skip epilogue
       // lost the skip term of lane group 3's even channels in a few hundred voxels per launch on
@@ -800,12 +768,161 @@ hipError_t launch_lds(hipStream_t s, const ConvArgs& a) {
   return hipErrorNotSupported;
 }
 
+// conv11 (ConvTranspose3d k3 s2 p1 op1, 16 -> 8 channels, bf16, in-place skip) streamed along z:
+// a block owns 8 x 16 input-grid columns (q) over DZ consecutive q-planes; input planes pass
+// through a 4-slot LDS ring ((8+1) x (16+1) x 16 channels: the deconv only reaches offsets 0 and
+// +1), loaded two planes ahead. Per q-plane each wave produces, for its 2 q-rows, the 4 (pz, py)
+// x-pair phases of build_phases_xpair (K chunk (a, b) = z offset a, y offset b, lane group g >> 1 =
+// x offset, g & 1 = channel half) with the 9 A fragments in registers, so the whole layer is the
+// skip read + output write + one pass over the input, with no per-lane tap decoding or bounds tests
+// in the K loop. Same K order and weights as the x-pair gather kernel: identical results.
+__global__ __launch_bounds__(256) void deconv_xpair_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y,
+                                                                  int nzc, int zc, int ntiles) {
+  typedef uint4 raw;
+  constexpr int CH = 2, QX = 16, QY = 8, PW = QX + 1, PH = QY + 1;
+  constexpr int PLANE = PH * PW * CH;
+  constexpr int NLD = (PLANE + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  raw* ring = reinterpret_cast<raw*>(smem);
+
+  const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
+  int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tx = tt % tiles_x; tt /= tiles_x;
+  const int ty = tt % tiles_y; tt /= tiles_y;
+  const int tz = tt % nzc;
+  const int b = tt / nzc;
+  const int qx0 = tx * QX, qy0 = ty * QY, zb = tz * zc;
+  const int zend = min(zb + zc, a.Di);
+
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 16 * 2);
+  auto load_plane = [&](int iz, raw* v) {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * 256;
+      const int row = c / (PW * CH), col = c - row * (PW * CH);
+      const int iy = qy0 + row, ix = qx0 + col / CH;
+      const bool ok = c < PLANE && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+                      (unsigned)ix < (unsigned)a.Wi;
+      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + qx0) * CH + col) * 16u;
+      v[i] = BufIO<bf16_t>::frag(rin, ok ? off : kOOB);
+    }
+  };
+  auto store_plane = [&](int iz, const raw* v) {
+    raw* dst = ring + (iz & 3) * PLANE;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * 256;
+      if (c < PLANE) dst[c] = v[i];
+    }
+  };
+  raw wreg[9];
+  {
+    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack) + (threadIdx.x & 63);
+#pragma unroll
+    for (int s = 0; s < 9; ++s) wreg[s] = wsrc[(size_t)s * 64];
+  }
+  raw pa[NLD], pb[NLD];
+  load_plane(zb, pa);
+  store_plane(zb, pa);
+  load_plane(zb + 1, pa);
+  store_plane(zb + 1, pa);
+  if (zb + 1 < zend) load_plane(zb + 2, pa);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const bool lead = (g & 1) == 0;
+  const int lbase = (2 * wave * PW + n + (g >> 1)) * CH + (g & 1);  // q-row 2w, column n, x offset g>>1
+  float b8[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b8[i] = a.bias[i];
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * 8 * 2;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.resid ? a.resid : a.out, a.resid ? nout : 0);
+  const int qx = qx0 + n;
+
+  auto step = [&](int qz, raw* cur, raw* nxt) {
+    if (qz + 2 < zend) load_plane(qz + 3, nxt);
+    // output offsets and the skip records of this plane's 8 outputs, loaded before the MFMAs
+    uint32_t off[8];
+    raw rq[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int pd = k >> 2, py = (k >> 1) & 1, r = k & 1;
+      const int qy = qy0 + 2 * wave + r;
+      const bool ok = lead && qy < a.Hi && qx < a.Wi;
+      const int oz = 2 * qz + pd, oy = 2 * qy + py, ox = 2 * qx + (g >> 1);
+      off[k] = ok ? (uint32_t)((((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * 8) * 2u : kOOB;
+      rq[k] = BufIO<bf16_t>::frag(rr, off[k]);  // zero when there is no skip tensor (empty range)
+    }
+    const raw* p0 = ring + (qz & 3) * PLANE + lbase;        // q-plane qz (z offset 0)
+    const raw* p1 = ring + ((qz + 1) & 3) * PLANE + lbase;  // q-plane qz + 1 (z offset +1)
+    f32x4_t acc[8];  // [pd][py][r]
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int pd = 0; pd < 2; ++pd)
+#pragma unroll
+      for (int py = 0; py < 2; ++py) {
+        const int na = pd ? 2 : 1, nb = py ? 2 : 1;
+        const int w0 = (pd * 2 + py) == 0 ? 0 : (pd * 2 + py) == 1 ? 1 : (pd * 2 + py) == 2 ? 3 : 5;
+#pragma unroll
+        for (int ca = 0; ca < na; ++ca)
+#pragma unroll
+          for (int cb = 0; cb < nb; ++cb) {
+            const int zo = pd ? (ca == 0 ? 1 : 0) : 0, yo = py ? (cb == 0 ? 1 : 0) : 0;
+            const raw w = wreg[w0 + ca * nb + cb];
+            const raw* src = (zo ? p1 : p0) + yo * PW * CH;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) Frag<bf16_t>::mma(w, src[r * PW * CH], acc[(pd * 2 + py) * 2 + r]);
+          }
+      }
+    // epilogue per output: partner channels, bias, ReLU, skip (after the ReLU), 16-byte store
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = acc[k][i];
+        v[4 + i] = __shfl_down(acc[k][i], 16);
+      }
+      const uint32_t q4[4] = {rq[k].x, rq[k].y, rq[k].z, rq[k].w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        v[i] += b8[i];
+        if (a.relu) v[i] = fmaxf(v[i], 0.f);
+        v[i] += __uint_as_float((i & 1) ? (q4[i >> 1] & 0xffff0000u) : (q4[i >> 1] << 16));
+      }
+      if (lead) Vox8<bf16_t>::store(ro, off[k], v);
+    }
+    if (qz + 1 < zend) store_plane(qz + 2, cur);  // slot of plane qz - 2, released by the last barrier
+    __syncthreads();
+  };
+  for (int qz = zb; qz < zend; qz += 2) {
+    step(qz, pa, pb);
+    if (qz + 1 < zend) step(qz + 1, pb, pa);
+  }
+}
+
+bool deconv_zslide_disabled() {  // read per call: tests flip it between launches
+  const char* v = getenv("DAMVS_DECONV_NO_ZSLIDE");
+  return v && v[0] == '1';
+}
+
 template <typename T>
 hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
   long long Qtot = (long long)a.B * a.Dq * a.Hq * a.Wq;
   long long per_block = 4LL * kGroups * 16;
   const int nq = (int)((Qtot + per_block - 1) / per_block);
   dim3 grid((unsigned)(nq * a.nphase));
+  if (sizeof(T) == 2 && a.xpair && a.Cin == 16 && a.Cout == 8 && a.nphase == 4 && !deconv_zslide_disabled()) {
+    constexpr int zc = 8;
+    const int tx = (a.Wi + 15) / 16, ty = (a.Hi + 7) / 8, nzc = (a.Di + zc - 1) / zc;
+    const long long nt = (long long)tx * ty * nzc * a.B;
+    const size_t smem = 4 * 9 * 17 * 2 * 16;
+    hipLaunchKernelGGL(deconv_xpair_zslide_kernel, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
+    return hipGetLastError();
+  }
   if (a.xpair) {
     if (a.MT != 1 || a.Cout != 8) return hipErrorInvalidValue;
     hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, true>), grid, dim3(256), 0, s, a, nq);

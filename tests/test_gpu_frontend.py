@@ -50,6 +50,9 @@ CASES = [
     (False, 3, 1, 1, 0, 32, 32, (64,), 64, True, True, 0),          # halo kernel: two inputs + plane
     (True, 5, 2, 2, 1, 128, 0, (), 32, True, False, 1),             # halo kernel: k5 s2 phases, cout 32
     (True, 3, 1, 1, 0, 64, 0, (), 128, True, True, 0),              # halo kernel: transposed k3 s1, MT 8
+    (True, 4, 2, 1, 0, 16, 0, (), 8, False, False, 0),              # x-pair phases: FPN top (k4 s2), cout 8
+    (True, 5, 2, 2, 1, 16, 0, (), 8, True, True, 2),                # x-pair + both residuals (post up 2)
+    (True, 3, 2, 1, 1, 16, 16, (), 8, True, False, 1),              # x-pair, two inputs
 ]
 
 

@@ -411,8 +411,10 @@ def test_costreg_bf16_deterministic(s, D, B, H, W):
 
 @pytest.mark.parametrize("s,D,H,W", [(0, 48, 40, 72), (1, 24, 40, 72), (2, 8, 48, 96), (1, 32, 32, 80)])
 def test_conv0_zslide_matches_tile_kernel(s, D, H, W, monkeypatch):
-    """conv0's z-sliding ring-buffer kernel (bf16) against the 4x8x16-tile row-pair kernel: same K
-    order and accumulation chain, so the U-Net logits agree bitwise (partial x tiles included)."""
+    """The z-streaming kernels (bf16) against the kernels they replace, each on the same U-Net:
+    conv0's ring-buffer row-pair kernel vs the 4x8x16-tile row-pair kernel, and conv11's z-streamed
+    x-pair deconv vs the x-pair gather kernel. Same K order and accumulation chains, so the logits
+    agree bitwise (partial tiles included)."""
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import StageEngine
     C = (32, 16, 8)[s]
@@ -423,11 +425,13 @@ def test_conv0_zslide_matches_tile_kernel(s, D, H, W, monkeypatch):
                       torch.device(DEV))
     nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats]
     vol = eng.warp_aggregate(nhwc, cuda(P), cuda(hyps))
-    monkeypatch.setenv("DAMVS_CONV_NO_ZSLIDE", "0")
-    a = eng.costreg_logits(vol).clone()
-    monkeypatch.setenv("DAMVS_CONV_NO_ZSLIDE", "1")
-    b = eng.costreg_logits(vol).clone()
-    assert torch.equal(a, b)
+    for knob in ("DAMVS_CONV_NO_ZSLIDE", "DAMVS_DECONV_NO_ZSLIDE"):
+        monkeypatch.setenv(knob, "0")
+        a = eng.costreg_logits(vol).clone()
+        monkeypatch.setenv(knob, "1")
+        b = eng.costreg_logits(vol).clone()
+        monkeypatch.setenv(knob, "0")
+        assert torch.equal(a, b), knob
 
 
 def test_forward_batch2_matches_batch1():
