@@ -1,0 +1,73 @@
+"""BASELINE.json's full size (DTU 1600x1184, 5 views): parity and invariants at the benchmark shape.
+
+* Stage-3 DepthNet at full resolution (1184 x 1600, 8 hypotheses, C = 8, ref + 4 sources, fp32):
+  the HIP path against the oracle (oracle/mvs_oracle.py, a restatement of models/cas_mvsnet.py:18-134)
+  on identical inputs, gated at the north-star tolerance: per-pixel |depth - ref| / ref <= 1e-3.
+  (About 10 s of oracle time on the host.)
+* The bf16 cascade at cfgC (48/32/8): size-independent properties of the regression
+  (models/cas_mvsnet.py:105-124) at every stage -- the depth of each pixel inside its hypothesis
+  range, probabilities summing to 1 over D, confidence in [0, 1] -- plus batch independence (two
+  copies of one sample give bitwise identical maps) and run-to-run bitwise reproducibility.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import pixel_rel
+from common import model_state, forward_inputs, depthnet_inputs
+from oracle import mvs_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+H, W = 1184, 1600
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from damvsnet_amd import _capi
+    _capi.load_library()
+
+
+def test_stage3_depthnet_fullres_vs_oracle():
+    from damvsnet_amd.cascade import CascadeMVSNet
+    sd = model_state("depthnet_cfgA_adaptive")
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(sd, strict=True)
+    net = net.to(DEV).eval()
+    feats, P, hyps = depthnet_inputs(B=1, N=5, H=H, W=W, D=8, stage_idx=2, C=8)
+    with torch.no_grad():
+        out = net.DepthNet(2, [f.to(DEV) for f in feats], P.to(DEV), hyps.to(DEV), 8, net.cost_regularization[2])
+        ref = O.depthnet_stage(2, feats, P, hyps, sd, "adaptive")
+    d, r = out["depth"].cpu().numpy(), ref["depth"].numpy()
+    assert d.shape == (1, H, W)
+    err = pixel_rel(d, r)
+    assert err.max() < 1e-3, (err.max(), err.mean())
+    assert np.abs(out["prob_volume"].cpu().numpy() - ref["prob_volume"].numpy()).max() < 1e-3
+
+
+def test_cascade_bf16_cfgC_invariants():
+    from damvsnet_amd.cascade import CascadeMVSNet
+    net = CascadeMVSNet(ndepths=[48, 32, 8], compute_dtype=torch.bfloat16, frontend_dtype=torch.bfloat16)
+    net.load_state_dict(model_state("forward_cfgB_640x512"), strict=True)
+    net = net.to(DEV).eval()
+    imgs, proj, dv, ins = forward_inputs(1, 5, H, W)
+    rep = lambda t: t.repeat(2, *([1] * (t.dim() - 1))).to(DEV)
+    imgs2, proj2, dv2, ins2 = rep(imgs), {k: rep(v) for k, v in proj.items()}, rep(dv), {k: rep(v) for k, v in ins.items()}
+    with torch.no_grad():
+        o1 = net(imgs2, proj2, dv2, ins2)
+        o2 = net(imgs2, proj2, dv2, ins2)
+    for s, (h, w, D) in zip(("stage1", "stage2", "stage3"), ((H // 4, W // 4, 48), (H // 2, W // 2, 32), (H, W, 8))):
+        st = o1[s]
+        depth, prob, hyp, conf = st["depth"], st["prob_volume"], st["depth_values"], st["photometric_confidence"]
+        assert depth.shape == (2, h, w) and prob.shape == (2, D, h, w) and hyp.shape == (2, D, h, w)
+        assert torch.isfinite(depth).all() and torch.isfinite(prob).all()
+        lo, hi = hyp.min(1).values, hyp.max(1).values
+        slack = 1e-5 * hi.abs()
+        assert bool(((depth >= lo - slack) & (depth <= hi + slack)).all()), s
+        assert float((prob.sum(1) - 1).abs().max()) < 1e-4, s
+        assert float(conf.min()) >= 0 and float(conf.max()) <= 1 + 1e-5, s
+        assert torch.equal(depth[0], depth[1]) and torch.equal(prob[0], prob[1]), s  # batch independence
+        assert torch.equal(depth, o2[s]["depth"]) and torch.equal(conf, o2[s]["photometric_confidence"]), s
+    assert torch.equal(o1["depth"], o1["stage3"]["depth"])
