@@ -31,6 +31,7 @@ CASES = {
     "K geo conv2 64+g->64 r4": (False, 3, 1, 1, 0, 64, 0, 1, 64, True, 1, 296, 400, True, 0),
     "L dec4 128->64 k3 r4": (True, 3, 1, 1, 0, 128, 0, 0, 64, True, 1, 296, 400, False, 0),
     "M dec5 64->32 k5s2 r2": (True, 5, 2, 2, 1, 64, 0, 0, 32, True, 1, 296, 400, False, 1),
+    "N geo conv2 128+g->128 r4 B=4": (False, 3, 1, 1, 0, 128, 0, 1, 128, True, 4, 296, 400, True, 0),
 }
 
 
