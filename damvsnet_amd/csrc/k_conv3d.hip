@@ -639,7 +639,7 @@ __global__ __launch_bounds__(256) void conv3d_zslide_pair_kernel(const ConvArgs 
   const int co = (g & 1) * 4, r = g >> 1;
   float bias[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) bias[i] = a.bias[co + i];
+  for (int i = 0; i < 4; ++i) bias[i] = co < a.Cout ? a.bias[co + i] : 0.f;  // (Cout 4 leaves group 1 idle)
   const int oy = y0 + 2 * wave + r;
 
   // one output plane: plane z + 2 (in `cur`, loaded one plane earlier) goes to the ring after the
