@@ -5,6 +5,8 @@
   the oracle (oracle/mvs_oracle.py, a restatement of models/cas_mvsnet.py:18-134)
   on identical inputs, gated at the north-star tolerance: per-pixel |depth - ref| / ref <= 1e-3.
   (About 10 s of oracle time per stage on the host.)
+* The bf16 stage path at the same sizes against the fp32 oracle on bf16-rounded features, at the
+  stated bf16 gate (mean <= 5e-3, p99 <= 2e-2 per-pixel relative depth).
 * The bf16 cascade at cfgC (48/32/8): size-independent properties of the regression
   (models/cas_mvsnet.py:105-124) at every stage -- the depth of each pixel inside its hypothesis
   range, probabilities summing to 1 over D, confidence in [0, 1] -- plus batch independence (two
@@ -51,6 +53,30 @@ def test_depthnet_fullres_vs_oracle(s, D, C):
     # probabilities: absolute 5e-3 (a fp32 logit difference of a few 1e-3 moves a sharp D = 48 softmax
     # peak by ~1.5e-3; measured max 1.45e-3 at stage 1), the gate stays on depth as north_star states
     assert np.abs(out["prob_volume"].cpu().numpy() - ref["prob_volume"].numpy()).max() < 5e-3
+
+
+@pytest.mark.parametrize("s,D,C", [(2, 8, 8), (1, 32, 16), (0, 48, 32)])
+def test_depthnet_bf16_fullres_stated_gate(s, D, C):
+    """The benchmark's bf16 stage path (z-streamed conv0 / conv11, banded-MFMA prob conv for D >= 32)
+    at each stage's cfgC resolution against the fp32 oracle on the same bf16-rounded features:
+    the stated bf16 gate of test_gpu_parity.py, mean <= 5e-3 and p99 <= 2e-2 per-pixel relative depth."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine
+    sd = model_state("depthnet_cfgA_adaptive")
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(sd, strict=True)
+    h, w = H >> (2 - s), W >> (2 - s)
+    feats, P, hyps = depthnet_inputs(B=1, N=5, H=h, W=w, D=D, stage_idx=s, C=C)
+    feats = [f.to(torch.bfloat16).float() for f in feats]
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.bfloat16,
+                      torch.device(DEV))
+    nhwc = [f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(DEV) for f in feats]
+    with torch.no_grad():
+        depth = eng.forward(nhwc, P.to(DEV), hyps.to(DEV))[0]
+        ref = O.depthnet_stage(s, feats, P, hyps, sd, "adaptive")["depth"].numpy()
+    pr = pixel_rel(depth.cpu().numpy(), ref)
+    print("bf16 full-size stage%d: mean %.3e p99 %.3e max %.3e" % (s + 1, pr.mean(), np.quantile(pr, 0.99), pr.max()))
+    assert pr.mean() < 5e-3 and np.quantile(pr, 0.99) < 2e-2
 
 
 def test_cascade_bf16_cfgC_invariants():
