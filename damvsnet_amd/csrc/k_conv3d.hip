@@ -904,6 +904,147 @@ __global__ __launch_bounds__(256) void deconv_xpair_zslide_kernel(const ConvArgs
   }
 }
 
+// conv9 (ConvTranspose3d k3 s2 p1 op1, 32 -> 16 channels, bf16, in-place skip) streamed along z like
+// deconv_xpair_zslide_kernel: 4-slot LDS ring of (8+1) x (16+1) x 32-channel input q-planes loaded
+// two ahead, the 27 A fragments (8 single-parity phases of build_phases, 1 tap per K chunk, lane
+// group g = channel block g) in registers; per q-plane and half (pd) each wave issues its 8 skip
+// records first, then the 4 (py, px) phases x 2 q-rows, then the 16-byte epilogue (lane group g + 1
+// hands its 4 channels to group g). Same K order and weights as the gather kernel.
+__global__ __launch_bounds__(256) void deconv_c16_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y, int nzc,
+                                                                int zc, int ntiles) {
+  typedef uint4 raw;
+  constexpr int CH = 4, QX = 16, QY = 8, PW = QX + 1, PH = QY + 1;
+  constexpr int PLANE = PH * PW * CH;
+  constexpr int NLD = (PLANE + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  raw* ring = reinterpret_cast<raw*>(smem);
+
+  const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
+  int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tx = tt % tiles_x; tt /= tiles_x;
+  const int ty = tt % tiles_y; tt /= tiles_y;
+  const int tz = tt % nzc;
+  const int b = tt / nzc;
+  const int qx0 = tx * QX, qy0 = ty * QY, zb = tz * zc;
+  const int zend = min(zb + zc, a.Di);
+
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 32 * 2);
+  auto load_plane = [&](int iz, raw* v) {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * 256;
+      const int row = c / (PW * CH), col = c - row * (PW * CH);
+      const int iy = qy0 + row, ix = qx0 + col / CH;
+      const bool ok = c < PLANE && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+                      (unsigned)ix < (unsigned)a.Wi;
+      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + qx0) * CH + col) * 16u;
+      v[i] = BufIO<bf16_t>::frag(rin, ok ? off : kOOB);
+    }
+  };
+  auto store_plane = [&](int iz, const raw* v) {
+    raw* dst = ring + (iz & 3) * PLANE;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * 256;
+      if (c < PLANE) dst[c] = v[i];
+    }
+  };
+  raw wreg[27];
+  {
+    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack) + (threadIdx.x & 63);
+#pragma unroll
+    for (int s = 0; s < 27; ++s) wreg[s] = wsrc[(size_t)s * 64];
+  }
+  raw pa[NLD], pb[NLD];
+  load_plane(zb, pa);
+  store_plane(zb, pa);
+  load_plane(zb + 1, pa);
+  store_plane(zb + 1, pa);
+  if (zb + 1 < zend) load_plane(zb + 2, pa);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const bool lead = (g & 1) == 0;
+  const int co = g * 4;                             // lead lanes own channels co .. co + 7
+  const int lbase = (2 * wave * PW + n) * CH + g;  // q-row 2w, column n, channel block g
+  float b8[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b8[i] = a.bias[(co & 8) + i];
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * 16 * 2;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.resid ? a.resid : a.out, a.resid ? nout : 0);
+  const int qx = qx0 + n;
+  constexpr int WOFF[8] = {0, 1, 3, 5, 9, 11, 15, 19};  // build_phases chunk offsets (Cin 32)
+
+  auto step = [&](int qz, raw* cur, raw* nxt) {
+    if (qz + 2 < zend) load_plane(qz + 3, nxt);
+    const raw* p0 = ring + (qz & 3) * PLANE + lbase;
+    const raw* p1 = ring + ((qz + 1) & 3) * PLANE + lbase;
+#pragma unroll
+    for (int pd = 0; pd < 2; ++pd) {
+      uint32_t off[8];
+      raw rq[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {  // k = (py, px, r)
+        const int py = k >> 2, px = (k >> 1) & 1, r = k & 1;
+        const int qy = qy0 + 2 * wave + r;
+        const bool ok = lead && qy < a.Hi && qx < a.Wi;
+        const int oz = 2 * qz + pd, oy = 2 * qy + py, ox = 2 * qx + px;
+        off[k] = ok ? (uint32_t)((((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * 16 + (co & 8)) * 2u : kOOB;
+        rq[k] = BufIO<bf16_t>::frag(rr, off[k]);
+      }
+      f32x4_t acc[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int py = 0; py < 2; ++py)
+#pragma unroll
+        for (int px = 0; px < 2; ++px) {
+          const int ph = pd * 4 + py * 2 + px;
+          const int na = pd ? 2 : 1, nb = py ? 2 : 1, nc = px ? 2 : 1;
+#pragma unroll
+          for (int ia = 0; ia < na; ++ia)
+#pragma unroll
+            for (int ib = 0; ib < nb; ++ib)
+#pragma unroll
+              for (int ic = 0; ic < nc; ++ic) {
+                const int zo = pd ? (ia == 0 ? 1 : 0) : 0, yo = py ? (ib == 0 ? 1 : 0) : 0;
+                const int xo = px ? (ic == 0 ? 1 : 0) : 0;
+                const raw w = wreg[WOFF[ph] + (ia * nb + ib) * nc + ic];
+                const raw* src = (zo ? p1 : p0) + (yo * PW + xo) * CH;
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+                  Frag<bf16_t>::mma(w, src[r * PW * CH], acc[(py * 2 + px) * 2 + r]);
+              }
+        }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = acc[k][i];
+          v[4 + i] = __shfl_down(acc[k][i], 16);
+        }
+        const uint32_t q4[4] = {rq[k].x, rq[k].y, rq[k].z, rq[k].w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          v[i] += b8[i];
+          if (a.relu) v[i] = fmaxf(v[i], 0.f);
+          v[i] += __uint_as_float((i & 1) ? (q4[i >> 1] & 0xffff0000u) : (q4[i >> 1] << 16));
+        }
+        if (lead) Vox8<bf16_t>::store(ro, off[k], v);
+      }
+    }
+    if (qz + 1 < zend) store_plane(qz + 2, cur);
+    __syncthreads();
+  };
+  for (int qz = zb; qz < zend; qz += 2) {
+    step(qz, pa, pb);
+    if (qz + 1 < zend) step(qz + 1, pb, pa);
+  }
+}
+
 bool deconv_zslide_disabled() {  // read per call: tests flip it between launches
   const char* v = getenv("DAMVS_DECONV_NO_ZSLIDE");
   return v && v[0] == '1';
@@ -921,6 +1062,15 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
     const long long nt = (long long)tx * ty * nzc * a.B;
     const size_t smem = 4 * 9 * 17 * 2 * 16;
     hipLaunchKernelGGL(deconv_xpair_zslide_kernel, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
+    return hipGetLastError();
+  }
+  if (sizeof(T) == 2 && !a.xpair && a.nphase == 8 && a.Cin == 32 && a.Cout == 16 && a.MT == 1 &&
+      !deconv_zslide_disabled()) {
+    constexpr int zc = 8;
+    const int tx = (a.Wi + 15) / 16, ty = (a.Hi + 7) / 8, nzc = (a.Di + zc - 1) / zc;
+    const long long nt = (long long)tx * ty * nzc * a.B;
+    const size_t smem = 4 * 9 * 17 * 4 * 16;
+    hipLaunchKernelGGL(deconv_c16_zslide_kernel, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
     return hipGetLastError();
   }
   if (a.xpair) {
