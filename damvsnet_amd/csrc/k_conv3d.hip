@@ -1045,6 +1045,124 @@ __global__ __launch_bounds__(256) void deconv_c16_zslide_kernel(const ConvArgs a
   }
 }
 
+// conv1 (Conv3d k3 s2 p1, 8 -> 16 channels, bf16) streamed along z: output plane z reads input planes
+// 2z-1 .. 2z+1, so a block keeps a 5-slot LDS ring of (2*8+1) x (2*16+1) x 8-channel input planes
+// and fetches the next two planes while it computes the current output plane. K = 27 taps x 8
+// channels in 7 chunks of 4 taps (lane group g = tap 4s + g; past tap 26 the weights are zero), the
+// 7 A fragments in registers. Same K order and weights as the gather kernel.
+__global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y, int nzc,
+                                                                int zc, int ntiles) {
+  typedef uint4 raw;
+  constexpr int QX = 16, QY = 8, PW = 2 * QX + 1, PH = 2 * QY + 1;
+  constexpr int PLANE = PH * PW;  // 16-byte (8-channel) pixels per halo plane
+  constexpr int NLD = (PLANE + 255) / 256;
+  constexpr int NS = 5;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  raw* ring = reinterpret_cast<raw*>(smem);
+
+  const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
+  int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tx = tt % tiles_x; tt /= tiles_x;
+  const int ty = tt % tiles_y; tt /= tiles_y;
+  const int tz = tt % nzc;
+  const int b = tt / nzc;
+  const int ox0 = tx * QX, oy0 = ty * QY, zb = tz * zc;
+  const int zend = min(zb + zc, a.Do);
+  const int ix0 = 2 * ox0 - 1, iy0 = 2 * oy0 - 1;
+
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 8 * 2);
+  auto load_plane = [&](int iz, raw* v) {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * 256;
+      const int row = c / PW, col = c - row * PW;
+      const int iy = iy0 + row, ix = ix0 + col;
+      const bool ok = c < PLANE && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+                      (unsigned)ix < (unsigned)a.Wi;
+      const uint32_t off = (uint32_t)(((b * a.Di + iz) * a.Hi + iy) * a.Wi + ix) * 16u;
+      v[i] = BufIO<bf16_t>::frag(rin, ok ? off : kOOB);
+    }
+  };
+  auto store_plane = [&](int iz, const raw* v) {
+    raw* dst = ring + ((iz + NS) % NS) * PLANE;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * 256;
+      if (c < PLANE) dst[c] = v[i];
+    }
+  };
+  raw wreg[7];
+  {
+    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack) + (threadIdx.x & 63);
+#pragma unroll
+    for (int s = 0; s < 7; ++s) wreg[s] = wsrc[(size_t)s * 64];
+  }
+  {
+    raw v[NLD];
+#pragma unroll
+    for (int p = -1; p <= 1; ++p) {
+      load_plane(2 * zb + p, v);
+      store_plane(2 * zb + p, v);
+    }
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const int lbase = (2 * (2 * wave) * PW + 2 * n);  // output row 2w (halo row 2*2w), column n
+  float bias[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias[i] = a.bias[g * 4 + i];
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * 16 * 2;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
+  const int ox = ox0 + n;
+
+  for (int z = zb; z < zend; ++z) {
+    const bool more = z + 1 < zend;
+    raw na[NLD], nb[NLD];
+    if (more) {
+      load_plane(2 * z + 2, na);
+      load_plane(2 * z + 3, nb);
+    }
+    const raw* pl[3] = {ring + ((2 * z - 1 + NS) % NS) * PLANE, ring + ((2 * z) % NS) * PLANE,
+                        ring + ((2 * z + 1) % NS) * PLANE};
+    f32x4_t acc[2] = {(f32x4_t){0.f, 0.f, 0.f, 0.f}, (f32x4_t){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const int t0 = 4 * s;
+      auto tap = [&](int t) {  // (plane, in-plane offset) of tap t (past 26: a valid pixel, zero weight)
+        const int tc = t < 27 ? t : 26;
+        return (tc / 9) * 65536 + (((tc / 3) % 3) * PW + tc % 3);
+      };
+      int code = tap(t0);
+      code = g == 1 ? tap(t0 + 1) : code;
+      code = g == 2 ? tap(t0 + 2) : code;
+      code = g == 3 ? tap(t0 + 3) : code;
+      const int dz = code >> 16, o = code & 0xffff;
+      const raw* src = (dz == 0 ? pl[0] : dz == 1 ? pl[1] : pl[2]) + lbase + o;
+#pragma unroll
+      for (int r = 0; r < 2; ++r) Frag<bf16_t>::mma(wreg[s], src[r * 2 * PW], acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int oy = oy0 + 2 * wave + r;
+      const bool ok = oy < a.Ho && ox < a.Wo;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = acc[r][i] + bias[i];
+        if (a.relu) v[i] = fmaxf(v[i], 0.f);
+      }
+      BufIO<bf16_t>::stq(ro, ok ? (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * 16 + g * 4) * 2u : kOOB, v);
+    }
+    if (more) {  // slots of planes 2z - 3 and 2z - 2, last read before the previous barrier
+      store_plane(2 * z + 2, na);
+      store_plane(2 * z + 3, nb);
+    }
+    __syncthreads();
+  }
+}
+
 bool deconv_zslide_disabled() {  // read per call: tests flip it between launches
   const char* v = getenv("DAMVS_DECONV_NO_ZSLIDE");
   return v && v[0] == '1';
@@ -1062,6 +1180,15 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
     const long long nt = (long long)tx * ty * nzc * a.B;
     const size_t smem = 4 * 9 * 17 * 2 * 16;
     hipLaunchKernelGGL(deconv_xpair_zslide_kernel, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
+    return hipGetLastError();
+  }
+  if (sizeof(T) == 2 && a.nphase == 1 && a.in_stride == 2 && a.Cin == 8 && a.Cout == 16 && a.MT == 1 && !a.resid &&
+      a.ph[0].ntaps == 27 && !deconv_zslide_disabled()) {
+    constexpr int zc = 8;
+    const int tx = (a.Wo + 15) / 16, ty = (a.Ho + 7) / 8, nzc = (a.Do + zc - 1) / zc;
+    const long long nt = (long long)tx * ty * nzc * a.B;
+    const size_t smem = 5 * 17 * 33 * 16;
+    hipLaunchKernelGGL(conv_s2_c8_zslide_kernel, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
     return hipGetLastError();
   }
   if (sizeof(T) == 2 && !a.xpair && a.nphase == 8 && a.Cin == 32 && a.Cout == 16 && a.MT == 1 &&
