@@ -746,6 +746,122 @@ hipError_t launch_lds_t(hipStream_t s, const ConvArgs& a) {
   return hipGetLastError();
 }
 
+// conv2 (Conv3d k3 s1 p1, 16 -> 16 channels, bf16) streamed along z on conv0's plan (4-slot ring of
+// (8+2) x (32+2) x 16-channel planes, two planes ahead), with 16 output channels as the MFMA rows
+// instead of conv0's row pairs: K = 27 taps x 16 channels in 14 chunks of 2 taps (lane group g:
+// tap 2s + (g >> 1), channel half g & 1; a chunk's two taps may sit in different planes), the 14 A
+// fragments in registers. Same K order and weights as conv3d_lds_kernel.
+__global__ __launch_bounds__(256) void conv_s1_c16_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y, int nzc,
+                                                                 int zc, int ntiles) {
+  typedef uint4 raw;
+  constexpr int CH = 2, TXG = 2, TX = 16 * TXG, PW = TX + 2, PH = LTH + 2;
+  constexpr int PLANE = PH * PW * CH;
+  constexpr int NLD = (PLANE + 255) / 256;
+  constexpr int KCH = 14;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  raw* ring = reinterpret_cast<raw*>(smem);
+
+  const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
+  int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tx = tt % tiles_x; tt /= tiles_x;
+  const int ty = tt % tiles_y; tt /= tiles_y;
+  const int tz = tt % nzc;
+  const int b = tt / nzc;
+  const int x0 = tx * TX, y0 = ty * LTH, zb = tz * zc;
+  const int zend = min(zb + zc, a.Do);
+
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 16 * 2);
+  auto load_plane = [&](int iz, raw* v) {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * 256;
+      const int row = c / (PW * CH), col = c - row * (PW * CH);
+      const int iy = y0 - 1 + row, ix = x0 - 1 + col / CH;
+      const bool ok = c < PLANE && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+                      (unsigned)ix < (unsigned)a.Wi;
+      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16u;
+      v[i] = BufIO<bf16_t>::frag(rin, ok ? off : kOOB);
+    }
+  };
+  auto store_plane = [&](int iz, const raw* v) {
+    raw* dst = ring + ((iz + 4) & 3) * PLANE;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * 256;
+      if (c < PLANE) dst[c] = v[i];
+    }
+  };
+  raw wreg[KCH];
+  {
+    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack) + (threadIdx.x & 63);
+#pragma unroll
+    for (int s = 0; s < KCH; ++s) wreg[s] = wsrc[(size_t)s * 64];
+  }
+  raw pa[NLD], pb[NLD];
+#pragma unroll
+  for (int p = -1; p <= 1; ++p) {
+    load_plane(zb + p, pa);
+    store_plane(zb + p, pa);
+  }
+  if (zb + 1 < zend) load_plane(zb + 2, pa);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const int gi = g >> 1, gc = g & 1;
+  const int lbase = (2 * wave * PW + n) * CH + gc;  // output row 2w (halo row 2w at dy = 0), column n
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * 16 * 2;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
+  float bias[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias[i] = a.bias[g * 4 + i];
+
+  auto step = [&](int z, raw* cur, raw* nxt) {
+    if (z + 2 < zend) load_plane(z + 3, nxt);
+    const raw* pl[3] = {ring + ((z + 3) & 3) * PLANE + lbase, ring + ((z + 4) & 3) * PLANE + lbase,
+                        ring + ((z + 5) & 3) * PLANE + lbase};
+    f32x4_t acc[2][TXG];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int xg = 0; xg < TXG; ++xg) acc[r][xg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KCH; ++s) {
+      auto tap = [&](int t) {  // (plane, in-plane offset); tap 27 (K padding) reads tap 26 against zero weights
+        const int tc = t < 27 ? t : 26;
+        return (tc / 9) * 65536 + (((tc / 3) % 3) * PW + tc % 3) * CH;
+      };
+      const int code = gi ? tap(2 * s + 1) : tap(2 * s);
+      const int dz = code >> 16, o = code & 0xffff;
+      const raw* src = (dz == 0 ? pl[0] : dz == 1 ? pl[1] : pl[2]) + o;
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int xg = 0; xg < TXG; ++xg) Frag<bf16_t>::mma(wreg[s], src[r * PW * CH + 16 * xg * CH], acc[r][xg]);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int xg = 0; xg < TXG; ++xg) {
+        const int oy = y0 + 2 * wave + r, ox = x0 + 16 * xg + n;
+        const bool ok = oy < a.Ho && ox < a.Wo;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = acc[r][xg][i] + bias[i];
+          if (a.relu) v[i] = fmaxf(v[i], 0.f);
+        }
+        BufIO<bf16_t>::stq(ro, ok ? (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * 16 + g * 4) * 2u : kOOB, v);
+      }
+    if (z + 1 < zend) store_plane(z + 2, cur);
+    __syncthreads();
+  };
+  for (int z = zb; z < zend; z += 2) {
+    step(z, pa, pb);
+    if (z + 1 < zend) step(z + 1, pb, pa);
+  }
+}
+
 // Returns hipErrorNotSupported when no LDS variant fits this layer (caller falls back).
 template <typename T>
 hipError_t launch_lds(hipStream_t s, const ConvArgs& a) {
@@ -759,6 +875,14 @@ hipError_t launch_lds(hipStream_t s, const ConvArgs& a) {
     if (a.Cin == 8) return launch_lds_pair_t<T, 8>(s, a);
     if (a.Cin == 16) return launch_lds_pair_t<T, 16>(s, a);
     if (a.Cin == 32 && sizeof(T) == 2) return launch_lds_pair_t<T, 32>(s, a);
+  }
+  if (sizeof(T) == 2 && a.Cin == 16 && a.Cout == 16 && MT == 1 && !a.resid && !zslide_disabled()) {
+    constexpr int zc = 16;
+    const int tx = (a.Wo + 31) / 32, ty = (a.Ho + LTH - 1) / LTH, nzc = (a.Do + zc - 1) / zc;
+    const long long nt = (long long)tx * ty * nzc * a.B;
+    const size_t smem = 4 * (LTH + 2) * 34 * 2 * 16;
+    hipLaunchKernelGGL(conv_s1_c16_zslide_kernel, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
+    return hipGetLastError();
   }
   if (a.Cin == 8 && MT == 1) return launch_lds_t<T, 8, 1>(s, a);
   if (a.Cin == 16 && MT == 1) return launch_lds_t<T, 16, 1>(s, a);
