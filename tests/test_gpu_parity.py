@@ -450,3 +450,30 @@ def test_forward_batch2_matches_batch1():
             assert pixel_rel(np_(o2["depth"][b]), np_(o1["depth"][0])).mean() < 1e-3
     finally:
         torch.backends.cudnn.deterministic = False
+
+
+@pytest.mark.parametrize("s,D,H,W", [(0, 24, 40, 72), (2, 8, 40, 56)])
+def test_stage_odd_batch_matches_per_sample(s, D, H, W):
+    """An odd batch (B=3, partial tiles; the U-Net needs multiples of 8) of distinct samples through the bf16 stage path equals
+    each sample run alone at B=1: warp volume, U-Net logits and depth are per-sample (the kernels'
+    batch index never enters a reduction)."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine
+    C = (32, 16, 8)[s]
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    feats, P, hyps = depthnet_inputs(B=3, N=3, H=H, W=W, D=D, stage_idx=s, C=C)
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.bfloat16,
+                      torch.device(DEV))
+    nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats]
+    vol = eng.warp_aggregate(nhwc, cuda(P), cuda(hyps)).clone()
+    logits = eng.costreg_logits(vol).clone()
+    depth = eng.forward(nhwc, cuda(P), cuda(hyps))[0].clone()
+    for b in range(3):
+        one = [f[b:b + 1].contiguous() for f in nhwc]
+        v1 = eng.warp_aggregate(one, cuda(P[b:b + 1]), cuda(hyps[b:b + 1]))
+        assert (v1.float() - vol[b:b + 1].float()).abs().max().item() <= 1e-2, b
+        l1 = eng.costreg_logits(vol[b:b + 1].contiguous())
+        assert (l1 - logits[b:b + 1]).abs().max().item() <= 1e-2, b
+        d1 = eng.forward(one, cuda(P[b:b + 1]), cuda(hyps[b:b + 1]))[0]
+        assert pixel_rel(np_(d1[0]), np_(depth[b])).max() < 1e-3, b
