@@ -74,5 +74,14 @@ def costreg_state(s):
     return sd
 
 
+def featurenet_unet_state():
+    """State of a bare FeatureNet(arch_mode="unet") (reference keys without the "feature." prefix, as the
+    fixture generator instantiated it) with the calibrated BN stats of tests/golden/featurenet_unet.npz."""
+    from damvsnet_amd.frontend import FeatureNet
+    net = FeatureNet(base_channels=8, stride=4, num_stage=3, arch_mode="unet")
+    sd = synthetic_state_dict(net.state_dict(), SEED)
+    return apply_bn_stats(sd, bn_from_golden(golden("featurenet_unet")))
+
+
 def checksum(*arrs):
     return np.array([float(np.asarray(a, dtype=np.float64).sum()) for a in arrs])

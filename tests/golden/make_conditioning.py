@@ -1,0 +1,71 @@
+"""Measure the reference forward's own fp32-vs-fp64 conditioning (CPU, the pinned oracle) and commit the
+fp64 depth maps the end-to-end GPU gates compare against.
+
+Run from the repo root:  ``python tests/golden/make_conditioning.py``  (a few minutes on 8 cores)
+
+For each end-to-end fixture case, the oracle (oracle/mvs_oracle.py, bit-exact against the reference's
+goldens in fp32, tests/test_oracle.py) runs the whole cascade twice on identical inputs and weights:
+once in float32 (what the reference computes) and once in float64. The per-stage per-pixel relative
+depth difference fp32-vs-fp64 (mean / p99 / max) is the reference's own rounding sensitivity with these
+random BN-calibrated weights: the cascade amplifies last-bit differences at stages 2-3 (uncertainty-
+aware sampling re-centres on the previous stage's depth). tests/test_gpu_parity.py gates the HIP fp32
+path against the float64 depths at a fixed multiple of these numbers.
+
+Writes ``tests/golden/conditioning.npz``: ``<case>::s<k>_depth64`` (float64 depth, stage k) and
+``<case>::s<k>_stats`` = [mean, p99, max] of the fp32-vs-fp64 per-pixel relative difference.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+from oracle import mvs_oracle as O  # noqa: E402
+from common import model_state, forward_inputs  # noqa: E402
+
+# (case, fixture whose BN statistics the weights use, H, W, N, ndepths, agg_mode)
+CASES = [
+    ("160x128_48_32_8", "forward_160x128_48_32_8", 128, 160, 5, (48, 32, 8), "adaptive"),
+    ("160x128_64_32_8_variance", "forward_160x128_64_32_8_variance", 128, 160, 3, (64, 32, 8), "variance"),
+    ("cfgB_640x512", "forward_cfgB_640x512", 512, 640, 5, (48, 32, 8), "adaptive"),
+]
+
+
+def run(sd, inputs, ndepths, mode, dtype):
+    imgs, proj, dv, _ = inputs
+    cast = lambda t: t.to(dtype)
+    sdd = {k: (v.to(dtype) if torch.is_floating_point(v) else v) for k, v in sd.items()}
+    with torch.no_grad():
+        out = O.cascade_forward(sdd, cast(imgs), {k: cast(v) for k, v in proj.items()}, cast(dv), ndepths, mode)
+    return [out["stage%d" % s]["depth"].double().numpy() for s in (1, 2, 3)]
+
+
+def main():
+    torch.set_num_threads(os.cpu_count() or 8)
+    res = {}
+    for case, fixture, H, W, N, nd, mode in CASES:
+        t0 = time.time()
+        sd = model_state(fixture)
+        inputs = forward_inputs(1, N, H, W)
+        d32 = run(sd, inputs, nd, mode, torch.float32)
+        d64 = run(sd, inputs, nd, mode, torch.float64)
+        for s in range(3):
+            pr = np.abs(d32[s] - d64[s]) / np.maximum(np.abs(d64[s]), 1e-12)
+            st = np.array([pr.mean(), np.quantile(pr, 0.99), pr.max()])
+            res["%s::s%d_depth64" % (case, s + 1)] = d64[s]
+            res["%s::s%d_stats" % (case, s + 1)] = st
+            print("%-26s stage%d fp32 vs fp64: mean %.3e p99 %.3e max %.3e" % (case, s + 1, *st))
+        print("  (%.1f s)" % (time.time() - t0))
+    np.savez_compressed(os.path.join(HERE, "conditioning.npz"), **res)
+
+
+if __name__ == "__main__":
+    main()

@@ -158,6 +158,19 @@ def fixture_forward(origin, tag, B, N, H, W, ndepths, mode="adaptive", keep_prob
     save("forward_" + tag, **arrays)
 
 
+def fixture_featurenet_unet(mod):
+    """FeatureNet(arch_mode="unet") (models/module.py:355-462, DeConv2dFuse :334-352): two seeded 128x96
+    views as one batch, calibrated BN, the three stage outputs."""
+    net = mod.FeatureNet(base_channels=8, num_stage=3, stride=4, arch_mode="unet")
+    sd = synthetic_state_dict(net.state_dict(), seed=SEED)
+    net.load_state_dict(sd, strict=True)
+    x = torch.from_numpy(synth.images(1, 2, 96, 128, seed=SEED)[0])
+    calibrate(net, lambda: net(x))
+    with torch.no_grad():
+        out = net(x)
+    save("featurenet_unet", **{k: to_np(v) for k, v in out.items()}, chk=checksum(x), **bn_stats(net))
+
+
 def fixture_state_dict_keys(active):
     """Key -> shape of the reference CascadeMVSNet state_dict (fpn and unet arch modes)."""
     import json
@@ -171,10 +184,14 @@ def fixture_state_dict_keys(active):
     print("wrote", path)
 
 
-def main():
+def main(only=()):
     torch.manual_seed(0)
     torch.set_num_threads(8)
     mod, active, origin = import_reference()
+    if "featurenet_unet" in only or not only:
+        fixture_featurenet_unet(mod)
+    if only:
+        return
     fixture_state_dict_keys(active)
     fixture_homo_warping(mod)
     fixture_costreg(mod)
@@ -186,4 +203,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))  # e.g. "featurenet_unet" to write just that fixture

@@ -172,6 +172,28 @@ def test_featurenet_hip_vs_oracle(dtype, tol):
         assert err < tol, (k, err)
 
 
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 5e-2)])
+def test_featurenet_unet_hip_vs_reference(dtype, tol):
+    """arch_mode="unet" FeatureNet (models/module.py:385-399,430-441; DeConv2dFuse :334-352) on the HIP
+    front-end against the reference's own outputs (tests/golden/featurenet_unet.npz) and the oracle."""
+    from common import featurenet_unet_state
+    from conftest import golden
+    from damvsnet_amd import synth
+    from damvsnet_amd.frontend import FeatureNet
+    from damvsnet_amd.frontend_fold import fold_frontend
+    from damvsnet_amd.frontend_hip import HipFeatureNet
+    sd = featurenet_unet_state()
+    net = FeatureNet(base_channels=8, stride=4, num_stage=3, arch_mode="unet")
+    net.load_state_dict(sd, strict=True)
+    x = torch.from_numpy(synth.images(1, 2, 96, 128, seed=0)[0])
+    g = golden("featurenet_unet")
+    ref = O.feature_net(x, {"feature." + k: v for k, v in sd.items()}, arch_mode="unet")
+    got = HipFeatureNet(fold_frontend(net, torch.float32).to(DEV), dtype)(x.to(DEV))
+    for k in ("stage1", "stage2", "stage3"):
+        y = got[k].float().cpu().permute(0, 3, 1, 2).numpy()
+        assert rel_max(y, g[k]) < tol and rel_max(y, ref[k].numpy()) < tol, k
+
+
 @pytest.mark.parametrize("stage_idx", [1, 2])
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 8e-2)])
 def test_geofusion_hip_vs_oracle(stage_idx, dtype, tol):

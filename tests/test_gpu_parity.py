@@ -339,15 +339,25 @@ def test_stage_isolated_bf16_stated_gate():
         assert pr.mean() < 5e-3 and np.quantile(pr, 0.99) < 2e-2, s
 
 
-def _check_forward_e2e(out, g):
-    stats = []
+COND_K = 2.5  # HIP fp32 vs fp64 may be this many times the reference's own fp32-vs-fp64 difference
+
+
+def _check_forward_e2e(out, case):
+    """End-to-end gate grounded in the reference's measured conditioning (tests/golden/make_conditioning.py):
+    per stage, the HIP fp32 depth against the float64 oracle depth on identical inputs must stay within
+    COND_K x the oracle-fp32-vs-fp64 mean, p99 and max per-pixel relative difference. Stage 1 also holds the
+    north-star 1e-3 per pixel end to end."""
+    g = golden("conditioning")
     for s in (1, 2, 3):
-        pr = pixel_rel(np_(out["stage%d" % s]["depth"]), g["s%d_depth" % s])
-        stats.append((pr.mean(), np.quantile(pr, 0.99), pr.max()))
-        print("e2e stage%d depth: mean %.3e p99 %.3e max %.3e" % ((s,) + stats[-1]))
-    assert stats[0][2] < 1e-3                      # stage 1: the gate holds end to end
-    assert stats[1][0] < 2e-4 and stats[1][2] < 1e-2
-    assert stats[2][0] < 2e-2
+        ref = g["%s::s%d_depth64" % (case, s)]
+        rm, rp, rx = g["%s::s%d_stats" % (case, s)]
+        pr = pixel_rel(np_(out["stage%d" % s]["depth"]), ref)
+        m, p, x = pr.mean(), np.quantile(pr, 0.99), pr.max()
+        print("e2e %s stage%d vs fp64: mean %.3e (%.2fx ref) p99 %.3e (%.2fx) max %.3e (%.2fx)"
+              % (case, s, m, m / rm, p, p / rp, x, x / rx))
+        assert m <= COND_K * rm and p <= COND_K * rp and x <= COND_K * rx, (s, m / rm, p / rp, x / rx)
+        if s == 1:
+            assert x < 1e-3
 
 
 @pytest.mark.parametrize("tag,N,ndepths,mode", [("160x128_48_32_8", 5, (48, 32, 8), "adaptive"),
@@ -357,19 +367,23 @@ def test_forward_small_golden(tag, N, ndepths, mode):
     imgs, proj, dv, ins = forward_inputs(1, N, 128, 160)
     with torch.no_grad():
         out = net(cuda(imgs), cuda(proj), cuda(dv), cuda(ins))
-    _check_forward_e2e(out, golden("forward_" + tag))
+    _check_forward_e2e(out, tag)
+    g = golden("forward_" + tag)  # the reference's own fp32 outputs: stage 1 within the north-star gate
+    assert pixel_rel(np_(out["stage1"]["depth"]), g["s1_depth"]).max() < 1e-3
     assert set(out) >= {"stage1", "stage2", "stage3", "depth", "photometric_confidence", "variance", "prob_volume",
                         "depth_values"}
     assert torch.equal(out["depth"], out["stage3"]["depth"])
 
 
 def test_forward_cfgB_golden_fp32():
-    """BASELINE.json configs[1]: 640x512, 5 views, 48/32/8, fp32, end to end vs the reference goldens."""
+    """BASELINE.json configs[1]: 640x512, 5 views, 48/32/8, fp32, end to end vs the float64 oracle."""
     net = make_model("forward_cfgB_640x512", (48, 32, 8))
     imgs, proj, dv, ins = forward_inputs(1, 5, 512, 640)
     with torch.no_grad():
         out = net(cuda(imgs), cuda(proj), cuda(dv), cuda(ins))
-    _check_forward_e2e(out, golden("forward_cfgB_640x512"))
+    _check_forward_e2e(out, "cfgB_640x512")
+    g = golden("forward_cfgB_640x512")
+    assert pixel_rel(np_(out["stage1"]["depth"]), g["s1_depth"]).max() < 1e-3
 
 
 def test_depthnet_deterministic():
@@ -452,28 +466,46 @@ def test_forward_batch2_matches_batch1():
         torch.backends.cudnn.deterministic = False
 
 
+def _distinct_samples(P, hyps):
+    """Give every batch element its own cameras and hypotheses (synth broadcasts one sample): source
+    translations scaled by 1 + 0.15 b and a small extra yaw, hypotheses scaled by 1 + 0.02 b. A kernel
+    that reads the wrong batch slice of rt / hyps then produces a different volume."""
+    P, hyps = P.clone(), hyps.clone()
+    for b in range(P.shape[0]):
+        a = 0.01 * b
+        R = torch.tensor([[np.cos(a), 0.0, np.sin(a)], [0.0, 1.0, 0.0], [-np.sin(a), 0.0, np.cos(a)]],
+                         dtype=torch.float32)
+        P[b, 1:, 0, :3, 3] *= 1.0 + 0.15 * b
+        P[b, 1:, 0, :3, :3] = R @ P[b, 1:, 0, :3, :3]
+        hyps[b] *= 1.0 + 0.02 * b
+    return P, hyps
+
+
 @pytest.mark.parametrize("s,D,H,W", [(0, 24, 40, 72), (2, 8, 40, 56)])
 def test_stage_odd_batch_matches_per_sample(s, D, H, W):
-    """An odd batch (B=3, partial tiles; the U-Net needs multiples of 8) of distinct samples through the bf16 stage path equals
-    each sample run alone at B=1: warp volume, U-Net logits and depth are per-sample (the kernels'
-    batch index never enters a reduction)."""
+    """An odd batch (B=3, partial tiles; the U-Net needs multiples of 8) of distinct samples -- own
+    features, cameras and hypotheses per element -- through the bf16 stage path equals each sample run
+    alone at B=1, bitwise: warp volume, U-Net logits and depth are per-sample (the kernels' batch index
+    never enters a reduction, and no kernel choice depends on B at these sizes)."""
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import StageEngine
     C = (32, 16, 8)[s]
     net = CascadeMVSNet(ndepths=[48, 32, 8])
     net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
     feats, P, hyps = depthnet_inputs(B=3, N=3, H=H, W=W, D=D, stage_idx=s, C=C)
+    P, hyps = _distinct_samples(P, hyps)
     eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.bfloat16,
                       torch.device(DEV))
     nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats]
     vol = eng.warp_aggregate(nhwc, cuda(P), cuda(hyps)).clone()
     logits = eng.costreg_logits(vol).clone()
     depth = eng.forward(nhwc, cuda(P), cuda(hyps))[0].clone()
+    assert not torch.equal(depth[0], depth[1])  # the samples really differ
     for b in range(3):
         one = [f[b:b + 1].contiguous() for f in nhwc]
         v1 = eng.warp_aggregate(one, cuda(P[b:b + 1]), cuda(hyps[b:b + 1]))
-        assert (v1.float() - vol[b:b + 1].float()).abs().max().item() <= 1e-2, b
+        assert torch.equal(v1, vol[b:b + 1]), b
         l1 = eng.costreg_logits(vol[b:b + 1].contiguous())
-        assert (l1 - logits[b:b + 1]).abs().max().item() <= 1e-2, b
+        assert torch.equal(l1, logits[b:b + 1]), b
         d1 = eng.forward(one, cuda(P[b:b + 1]), cuda(hyps[b:b + 1]))[0]
-        assert pixel_rel(np_(d1[0]), np_(depth[b])).max() < 1e-3, b
+        assert torch.equal(d1[0], depth[b]), b

@@ -63,6 +63,35 @@ def test_depthnet_cfgA_golden(mode):
     assert rel_max(out["prob_volume"], g["prob"]) < 1e-5
 
 
+def test_featurenet_unet_golden():
+    """FeatureNet arch_mode="unet" (models/module.py:385-399,430-441; DeConv2dFuse :334-352) vs the reference."""
+    from common import featurenet_unet_state
+    from damvsnet_amd import synth
+    g = golden("featurenet_unet")
+    x = torch.from_numpy(synth.images(1, 2, 96, 128, seed=0)[0])
+    np.testing.assert_allclose(checksum(x), g["chk"], rtol=1e-12)
+    sd = {"feature." + k: v for k, v in featurenet_unet_state().items()}
+    with torch.no_grad():
+        out = O.feature_net(x, sd, arch_mode="unet")
+    for k in ("stage1", "stage2", "stage3"):
+        assert rel_max(out[k], g[k]) < 1e-5, k
+
+
+def test_conditioning_fixture_reproduces():
+    """tests/golden/conditioning.npz: the oracle's fp32 cascade at 160x128 against the committed float64
+    depths reproduces the committed fp32-vs-fp64 statistics (the e2e GPU gates are multiples of them)."""
+    from conftest import pixel_rel
+    g = golden("conditioning")
+    sd = model_state("forward_160x128_48_32_8")
+    imgs, proj, dv, _ = forward_inputs(1, 5, 128, 160)
+    with torch.no_grad():
+        out = O.cascade_forward(sd, imgs, proj, dv, (48, 32, 8), "adaptive")
+    for s in (1, 2, 3):
+        pr = pixel_rel(out["stage%d" % s]["depth"].numpy(), g["160x128_48_32_8::s%d_depth64" % s])
+        st = np.array([pr.mean(), np.quantile(pr, 0.99), pr.max()])
+        np.testing.assert_allclose(st, g["160x128_48_32_8::s%d_stats" % s], rtol=1e-6)
+
+
 def test_regression_one_hot_known_answer():
     """Softmax/regression KAT: a dominant logit -> depth = that hypothesis, confidence 1, variance 0."""
     D = 8
