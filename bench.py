@@ -2,13 +2,23 @@
 roofline of the dominant kernel and the CPU baseline — one JSON line on rank 0.
 
   python bench.py [--gpus N --steps K --warmup W] [--config cfgC] [--batch B] [--no-cpu-baseline]
+                  [--shard depth|rows [--emulate P]] [--no-shard-latency]
 
 Workload (BASELINE.json configs[2]): DTU 1600x1184, 5 views, 3-stage 48/32/8 hypotheses, bf16 storage
 on 1x MI355X; synthetic seeded images/cameras, synthetic weights with calibrated BN statistics
 (no checkpoints or datasets exist offline). One step = one full CascadeMVSNet forward
 (front-end + 3 x (hypotheses, [GeoFeatureFusion], DepthNet)) over one batch per GPU, inputs resident
 in HBM. Multi-GPU: one process per GPU, each processing its own batch (reference views are
-independent units: weak scaling, no collective in the data path); timing = max over ranks.
+independent units: weak scaling, no collective in the data path); timing = max over ranks. With N > 1 the
+depth-sharded latency mode (damvsnet_amd/sharded.py: one map's cost volumes over all N GPUs) is timed
+after the throughput steps and reported as "depth_sharded"; ``--shard`` makes it the measured mode
+(``--emulate P``: P ranks as threads on one GPU, a functional rehearsal, not a speed figure).
+
+Roofline (damvsnet_amd/costmodel.py): HIP events recorded inside damvs_stage_forward
+(damvs_stage_forward_probed) around the warp, the U-Net and the regression of every stage of the timed
+steps give the in-pipeline kernel-group times; the headline roofline kernel is the stage-2 warp as the
+product runs it. MFMA utilisation of the U-Net / front-end conv kernels comes from the committed
+rocprofv3 PMC summary (tools/pmc_mfma.py) when present.
 """
 from __future__ import annotations
 
@@ -78,6 +88,107 @@ class StageTimer:
         for (n0, e0), (_, e1) in zip(self.marks, self.marks[1:]):
             out.setdefault(n0, []).append(e0.elapsed_time(e1))
         return out
+
+
+class ProbeRecorder:
+    """DepthNet.probe: 4 events per stage call (before / after the warp, after the U-Net, after the
+    regression), recorded by the library on the launch stream (damvs_stage_forward_probed)."""
+
+    def __init__(self):
+        self.calls = []
+
+    def __call__(self, stage_idx):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        self.calls.append((stage_idx, ev))
+        return ev
+
+    def per_stage_ms(self):
+        out = {}
+        for s, ev in self.calls:
+            d = out.setdefault(s, {"warp": [], "unet": [], "regress": []})
+            d["warp"].append(ev[0].elapsed_time(ev[1]))
+            d["unet"].append(ev[1].elapsed_time(ev[2]))
+            d["regress"].append(ev[2].elapsed_time(ev[3]))
+        return {s: {k: statistics.mean(v) for k, v in d.items()} for s, d in sorted(out.items())}
+
+
+def hot_path_roofline(per_stage_ms, H, W, N, nd, B, dtype_name):
+    """Per stage and per map: algorithmic bytes / FLOPs (costmodel) against the in-pipeline times."""
+    from damvsnet_amd import costmodel as CM
+    e = 2 if dtype_name == "bf16" else 4
+    cost = CM.cascade_cost(H, W, N, nd, e)
+    stages, t_meas, t_roof = {}, 0.0, 0.0
+    for s, ms in per_stage_ms.items():
+        groups = {}
+        for g in ("warp", "unet", "regress"):
+            nbytes, flops = (B * x for x in cost[s][g])
+            t = ms[g] * 1e-3
+            groups[g] = {"ms": round(ms[g], 4), "GB/s": round(nbytes / t / 1e9, 1), "TFLOP/s": round(flops / t / 1e12, 2),
+                         "hbm_frac": round(nbytes / t / CM.HBM_PEAK, 4),
+                         "mfma_frac": round(flops / t / CM.MFMA_PEAK[dtype_name], 4),
+                         "roofline_frac": round(CM.roofline_time(nbytes, flops, dtype_name) / t, 4)}
+        sb = sum(B * cost[s][g][0] for g in groups)
+        sf = sum(B * cost[s][g][1] for g in groups)
+        ts = sum(ms[g] for g in groups) * 1e-3
+        tr = CM.roofline_time(sb, sf, dtype_name)
+        stages["stage%d" % (s + 1)] = {"ms": round(ts * 1e3, 4), "roofline_ms": round(tr * 1e3, 4),
+                                        "roofline_frac": round(tr / ts, 4), "kernels": groups}
+        t_meas += ts
+        t_roof += tr
+    return {"per_stage": stages, "per_map": {"ms": round(t_meas * 1e3 / B, 4), "roofline_ms": round(t_roof * 1e3 / B, 4),
+                                              "roofline_frac": round(t_roof / t_meas, 4)}}
+
+
+def pmc_mfma(config, batch):
+    """MFMA utilisation per kernel family from the committed rocprofv3 PMC summary
+    (profiles/<round>/pmc_mfma_<config>_b<batch>.json, tools/pmc_mfma.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_mfma_%s_b%d.json" % (config, batch))))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return {"source": os.path.relpath(files[-1], REPO), "kernels": d.get("summary", d)}
+
+
+def sharded_latency(net, H, W, N, device, comm=None, emulate=1, warp="depth", steps=5, warmup=2):
+    """One depth map (B=1) with every stage's DepthNet over the ranks (damvsnet_amd/sharded.py): ms per map
+    (max over ranks) and rank 0's per-phase times of the last step."""
+    from damvsnet_amd.sharded import DepthShardedDepthNet, ThreadGroup
+    imgs, proj, dv, ins = make_inputs(1, N, H, W, device, seed=0)  # every rank: the same map
+    world = comm.world if comm is not None else emulate
+
+    def step(c, hook=None):
+        return net(imgs, proj, dv, ins, depthnet=DepthShardedDepthNet(net, c, warp=warp, hook=hook))
+
+    def run_all(hook=None):
+        if comm is not None:
+            step(comm, hook)
+        else:
+            ThreadGroup(emulate).run(lambda c: step(c, hook if c.rank == 0 else None))
+
+    with torch.no_grad():
+        net(imgs, proj, dv, ins)  # folded front-end and stage engines exist before any rank thread starts
+        for _ in range(warmup):
+            run_all()
+        torch.cuda.synchronize()
+        if comm is not None:
+            torch.distributed.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run_all()
+        torch.cuda.synchronize()
+        if comm is not None:
+            torch.distributed.barrier()
+        el = time.perf_counter() - t0
+        timer = StageTimer()
+        run_all(timer)
+        torch.cuda.synchronize()
+    from damvsnet_amd.dist import max_over_ranks
+    el = max_over_ranks(el, device=device) if comm is not None else el
+    return {"ms_per_map": round(el / steps * 1e3, 3), "ranks": world, "warp": warp,
+            "transport": "rccl" if comm is not None else "threads on one GPU (rehearsal)",
+            "phases_rank0_ms": {k: round(sum(v), 3) for k, v in timer.per_phase_ms().items()}}
 
 
 def latency_b1(net, imgs, proj, dv, ins, steps=10):
@@ -192,6 +303,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--frontend", default="hip", choices=["hip", "torch"], help="2D front-end implementation")
     ap.add_argument("--cpu-budget", type=float, default=60.0)
+    ap.add_argument("--shard", choices=["depth", "rows"], default=None,
+                    help="measure the depth-sharded latency mode (one map over all ranks) instead of replicas")
+    ap.add_argument("--emulate", type=int, default=1, help="with --shard on one GPU: P ranks as threads")
+    ap.add_argument("--no-shard-latency", action="store_true",
+                    help="N > 1: skip the depth-sharded latency block after the throughput steps")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -204,7 +320,26 @@ def main():
     torch.cuda.set_device(device)
 
     H, W, N, nd, dtype, desc = CONFIGS[args.config]
+    dname = "bf16" if dtype == torch.bfloat16 else "f32"
     net, _ = build_model(nd, dtype, device, args.frontend)
+    if args.shard:
+        from damvsnet_amd.sharded import TorchComm
+        res = sharded_latency(net, H, W, N, device, comm=TorchComm() if world > 1 else None, emulate=args.emulate,
+                              warp=args.shard, steps=args.steps, warmup=args.warmup)
+        if rank == 0:
+            ms = res["ms_per_map"]
+            print(json.dumps({
+                "metric": "depth maps/sec (full CascadeMVSNet forward, one map over all ranks)",
+                "value": round(1e3 / ms, 4), "unit": "depth maps/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "strong",
+                "vs_baseline": None, "dtype": dname, "data": "synthetic",
+                "config": {"workload": "%s: %s" % (args.config, desc), "batch_per_gpu": 1, "global_batch": 1,
+                           "height": H, "width": W, "views": N, "ndepths": list(nd),
+                           "parallelism": "depth-sharded x%d (%s warp)" % (res["ranks"], args.shard)},
+                "depth_sharded": res}), flush=True)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
     imgs, proj, dv, ins = make_inputs(args.batch, N, H, W, device, seed=rank)
 
     def barrier():
@@ -218,6 +353,8 @@ def main():
         barrier()
         torch.cuda.synchronize()
         timer = StageTimer()
+        probes = ProbeRecorder()
+        net.DepthNet.probe = probes
         t0 = time.perf_counter()
         for _ in range(args.steps):
             net(imgs, proj, dv, ins, stage_hook=timer)
@@ -225,16 +362,28 @@ def main():
         barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        net.DepthNet.probe = None
     from damvsnet_amd.dist import max_over_ranks
     elapsed = max_over_ranks(elapsed, device=device)
     maps = args.steps * args.batch * world
     phases = {k: round(statistics.mean(v), 3) for k, v in timer.per_phase_ms().items()}
 
+    shard_block = None
+    if world > 1 and not args.no_shard_latency:  # every rank takes part
+        from damvsnet_amd.sharded import TorchComm
+        try:
+            shard_block = sharded_latency(net, H, W, N, device, comm=TorchComm())
+        except Exception as ex:  # reported, never fatal for the throughput line
+            shard_block = {"error": repr(ex)[:300]}
+
     result = None
     if rank == 0:
         lat = latency_b1(net, imgs, proj, dv, ins)
-        ms, alg = warp_roofline(net, imgs, proj, dv, 1, dtype)
-        achieved = alg / (ms * 1e-3) / 1e9
+        per_stage = probes.per_stage_ms()
+        hp = hot_path_roofline(per_stage, H, W, N, nd, args.batch, dname)
+        iso_ms, alg = warp_roofline(net, imgs, proj, dv, 1, dtype)
+        pipe_ms = per_stage[1]["warp"]
+        achieved = alg / (pipe_ms * 1e-3) / 1e9
         tr = pmc_traffic(args.config, args.batch)
         result = {
             "metric": "depth maps/sec (full CascadeMVSNet forward)",
@@ -247,7 +396,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
+            "dtype": dname,
             "data": "synthetic (seeded DTU-like images/cameras, synthetic weights with calibrated BN stats)",
             "config": {"workload": "%s: %s" % (args.config, desc), "batch_per_gpu": args.batch,
                        "frontend": args.frontend,
@@ -255,12 +404,19 @@ def main():
                        "ndepths": list(nd), "parallelism": "replicas x%d (reference views sharded over ranks)" % world},
             "ms_per_stage": phases,
             "latency_b1": lat,
-            "roofline": {"kernel": "warp_aggregate stage2 (fused homography warp + adaptive aggregation)",
+            "roofline": {"kernel": "warp_aggregate stage2 (fused homography warp + adaptive aggregation), "
+                                   "in-pipeline launch time (HIP events inside damvs_stage_forward_probed)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr["bytes"] if tr else None,
-                         "traffic_source": tr["source"] if tr else None,
-                         "ms_per_launch": round(ms, 4), "algorithmic_bytes": int(alg)},
+                         "traffic_source": ("committed PMC profile " + tr["source"]) if tr else None,
+                         "ms_per_launch": round(pipe_ms, 4), "algorithmic_bytes": int(alg),
+                         "isolated_ms_per_launch": round(iso_ms, 4),
+                         "isolated_frac": round(alg / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "hot_path_roofline": hp,
+            "mfma_utilisation": pmc_mfma(args.config, args.batch),
         }
+        if shard_block is not None:
+            result["depth_sharded"] = shard_block
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)
         print(json.dumps(result), flush=True)

@@ -65,6 +65,9 @@ SIGNATURES = (
     ("damvs_stage_forward", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_void_p),
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
                                     c_void_p)),
+    ("damvs_stage_forward_probed", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                           ctypes.POINTER(c_void_p), c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_void_p))),
     ("damvs_proj_prepare", c_int, (c_void_p, c_int, c_int, c_void_p, c_void_p)),
     ("damvs_homo_warp", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                 c_void_p)),
@@ -74,6 +77,11 @@ SIGNATURES = (
                                      ctypes.POINTER(c_void_p))),
     ("damvs_costreg_logits", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t,
                                      c_void_p)),
+    ("damvs_warp_aggregate_rows", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                          c_int, ctypes.POINTER(c_void_p), c_int, c_void_p, c_void_p, c_void_p)),
+    ("damvs_costreg_layer", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p)),
+    ("damvs_stage_regress", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p)),
     ("damvs_regress", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p)),
     ("damvs_hypotheses", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,

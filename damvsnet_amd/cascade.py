@@ -110,7 +110,9 @@ class CascadeMVSNet(nn.Module):
         f = feat(x)
         return [{k: v.reshape(B, N, *v.shape[1:])[:, i] for k, v in f.items()} for i in range(N)]
 
-    def forward(self, imgs, proj_matrices, depth_values, intrinsics_matrices=None, stage_hook=None):
+    def forward(self, imgs, proj_matrices, depth_values, intrinsics_matrices=None, stage_hook=None, depthnet=None):
+        """``depthnet``: optional stage runner (stage_idx, NHWC features, proj, hyps, cost_regularization) -> dict,
+        e.g. sharded.DepthShardedDepthNet (one depth map over several GPUs); default: this model's DepthNet."""
         if self.refine:
             raise NotImplementedError("refine=True: the reference RefineNet forward is not runnable "
                                       "(models/module.py:602 calls F.cat)")
@@ -142,7 +144,11 @@ class CascadeMVSNet(nn.Module):
             hyps = hypotheses(depth_values, self.ndepths[s], H, W, scale, depth, exp_var)
             hook(name + ".depthnet")
             cr = self.cost_regularization if self.share_cr else self.cost_regularization[s]
-            if self.frontend_impl == "hip":
+            if depthnet is not None:
+                if self.frontend_impl != "hip":
+                    raise ValueError("a custom stage runner takes the HIP front-end's NHWC features")
+                out = depthnet(s, fs, proj_matrices[name], hyps, cr)
+            elif self.frontend_impl == "hip":
                 out = self.DepthNet.forward_nhwc(s, fs, proj_matrices[name], hyps, cr)
             else:
                 out = self.DepthNet(s, fs, proj_matrices[name], hyps, self.ndepths[s], cr)

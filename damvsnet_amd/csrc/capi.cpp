@@ -362,12 +362,38 @@ WarpArgs warp_args(const damvs_stage* st, int B, int N, int C, int D, int h, int
   a.hyps = hyps;
   a.out = out;
   a.B = B; a.N = N; a.C = C; a.D = D; a.h = h; a.w = w;
+  a.y0 = 0;
+  a.rows = h;
+  a.out_rows = h;
+  a.out_y = 0;
   if (st) {
     std::memcpy(a.k1, st->k1, sizeof(a.k1));
     a.s1 = st->s1; a.t1 = st->t1; a.s2 = st->s2; a.t2 = st->t2;
   }
   return a;
 }
+
+// Prob conv (models/module.py:541) + softmax regression, confidence and exp-variance
+// (models/cas_mvsnet.py:105-124) on the U-Net output c0 [B][D][h][w][base].
+int regress_tail(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, const void* feat, const float* hyps,
+                 const float* prob_init, float* logits, float* depth, float* conf, float* var, float* prob) {
+  // banded MFMA prob conv + regression: TA-bound on its per-tap B loads, it beats the LDS-tiled VALU
+  // kernel only with >= 2 plane groups (measured at cfgC: stage 2 -26 us, stage 3 +50 us)
+  if (st->prob_pack && D >= 32 && D <= 64 && !prob_mfma_disabled())
+    return hip_check(launch_prob_mfma(s, B, D, h, w, feat, st->prob_pack, prob_init, hyps, depth, conf, var, prob),
+                     "prob_mfma launch");
+  if (prob_regress_smem_bytes(st->dtype, st->base, D) <= 160 * 1024)  // fused: logits stay in LDS
+    return hip_check(launch_prob_regress(s, st->dtype, B, st->base, D, h, w, feat, st->prob_w, prob_init, hyps, depth,
+                                         conf, var, prob),
+                     "prob_regress launch");
+  if (!logits) return fail(DAMVS_E_WORKSPACE, "this D needs the logits scratch buffer");
+  DAMVS_TRY(hip_check(launch_prob_conv(s, st->dtype, B, st->base, D, h, w, feat, st->prob_w, prob_init, logits),
+                      "prob conv launch"));
+  return hip_check(launch_regress(s, B, D, h, w, logits, hyps, depth, conf, var, prob), "regress launch");
+}
+
+// U-Net layer i (conv0..conv6, conv7, conv9, conv11): (input level, output level)
+constexpr int kLayerLevels[10][2] = {{0, 0}, {0, 1}, {1, 1}, {1, 2}, {2, 2}, {2, 3}, {3, 3}, {3, 2}, {2, 1}, {1, 0}};
 
 }  // namespace
 
@@ -537,6 +563,14 @@ int damvs_stage_forward(const damvs_stage* st, void* stream, int B, int N, int D
                         const void* const* feats, const float* proj, const float* hyps, const float* prob_init,
                         void* workspace, size_t workspace_bytes, float* depth, float* conf, float* var,
                         float* prob) {
+  return damvs_stage_forward_probed(st, stream, B, N, D, h, w, feats, proj, hyps, prob_init, workspace, workspace_bytes,
+                                    depth, conf, var, prob, nullptr);
+}
+
+int damvs_stage_forward_probed(const damvs_stage* st, void* stream, int B, int N, int D, int h, int w,
+                               const void* const* feats, const float* proj, const float* hyps, const float* prob_init,
+                               void* workspace, size_t workspace_bytes, float* depth, float* conf, float* var,
+                               float* prob, void* const* events) {
   if (!st || !feats || !proj || !hyps || !workspace || !depth || !conf || !var) return fail(DAMVS_E_ARG, "null argument");
   DAMVS_TRY(check_stage_shape(st, B, N, D, h, w));
   for (int v = 0; v < N; ++v)
@@ -560,28 +594,19 @@ int damvs_stage_forward(const damvs_stage* st, void* stream, int B, int N, int D
     }
     DAMVS_TRY(hip_check(launch_block_channels(s, st->dtype, src, dst, N, B, h * w, st->C), "block_channels launch"));
   }
+  auto mark = [&](int i) {
+    return events && events[i] ? hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(events[i]), s), "hipEventRecord")
+                               : DAMVS_OK;
+  };
   WarpArgs wa = warp_args(st, B, N, st->C, D, h, w, fv, rt, hyps, ws + W.vol);
+  DAMVS_TRY(mark(0));
   DAMVS_TRY(hip_check(launch_warp_aggregate(s, st->dtype, st->mode, wa, blk), "warp_aggregate launch"));
+  DAMVS_TRY(mark(1));
   DAMVS_TRY(run_unet(st, s, B, D, h, w, ws + W.vol, ws, W));
-  const void* feat = ws + W.c[0];
-  // banded MFMA prob conv + regression: TA-bound on its per-tap B loads, it beats the LDS-tiled VALU
-  // kernel only with >= 2 plane groups (measured at cfgC: stage 2 -26 us, stage 3 +50 us)
-  if (st->prob_pack && D >= 32 && D <= 64 && !prob_mfma_disabled()) {
-    DAMVS_TRY(hip_check(launch_prob_mfma(s, B, D, h, w, feat, st->prob_pack, prob_init, hyps, depth, conf, var, prob),
-                        "prob_mfma launch"));
-    return DAMVS_OK;
-  }
-  if (prob_regress_smem_bytes(st->dtype, st->base, D) <= 160 * 1024) {  // fused: logits stay in LDS
-    DAMVS_TRY(hip_check(launch_prob_regress(s, st->dtype, B, st->base, D, h, w, feat, st->prob_w, prob_init, hyps,
-                                            depth, conf, var, prob),
-                        "prob_regress launch"));
-    return DAMVS_OK;
-  }
-  float* logits = reinterpret_cast<float*>(ws + W.logits);
-  DAMVS_TRY(hip_check(launch_prob_conv(s, st->dtype, B, st->base, D, h, w, feat, st->prob_w, prob_init, logits),
-                      "prob conv launch"));
-  DAMVS_TRY(hip_check(launch_regress(s, B, D, h, w, logits, hyps, depth, conf, var, prob), "regress launch"));
-  return DAMVS_OK;
+  DAMVS_TRY(mark(2));
+  DAMVS_TRY(regress_tail(st, s, B, D, h, w, ws + W.c[0], hyps, prob_init, reinterpret_cast<float*>(ws + W.logits), depth,
+                         conf, var, prob));
+  return mark(3);
 }
 
 int damvs_proj_prepare(void* stream, int B, int N, const float* proj, float* rt) {
@@ -641,6 +666,45 @@ int damvs_costreg_logits(const damvs_stage* st, void* stream, int B, int D, int 
   DAMVS_TRY(run_unet(st, s, B, D, h, w, volume, ws, W));
   return hip_check(launch_prob_conv(s, st->dtype, B, st->base, D, h, w, ws + W.c[0], st->prob_w, nullptr, logits),
                    "prob conv launch");
+}
+
+int damvs_costreg_layer(const damvs_stage* st, void* stream, int layer, int B, int D, int h, int w, const void* in,
+                        void* out) {
+  if (!st || !in || !out) return fail(DAMVS_E_ARG, "null argument");
+  if (layer < 0 || layer > 9) return fail(DAMVS_E_ARG, "layer %d not in 0..9", layer);
+  DAMVS_TRY(check_stage_shape(st, B, 2, D, h, w));
+  const Shapes S = level_shapes(D, h, w);
+  const bool deconv = layer >= 7;  // conv7 / conv9 / conv11: relu(deconv) + skip, in place on `out`
+  ConvArgs a = conv_args(st, layer, B, S, kLayerLevels[layer][0], kLayerLevels[layer][1], in, out, deconv ? out : nullptr);
+  return hip_check(launch_conv3d(reinterpret_cast<hipStream_t>(stream), st->dtype, a), "conv3d launch");
+}
+
+int damvs_stage_regress(const damvs_stage* st, void* stream, int B, int D, int h, int w, const void* c0,
+                        const float* hyps, const float* prob_init, float* scratch, float* depth, float* conf, float* var,
+                        float* prob) {
+  if (!st || !c0 || !hyps || !depth || !conf || !var) return fail(DAMVS_E_ARG, "null argument");
+  DAMVS_TRY(check_stage_shape(st, B, 2, D, h, w));
+  return regress_tail(st, reinterpret_cast<hipStream_t>(stream), B, D, h, w, c0, hyps, prob_init, scratch, depth, conf,
+                      var, prob);
+}
+
+int damvs_warp_aggregate_rows(const damvs_stage* st, void* stream, int B, int N, int D, int h, int w, int y0, int rows,
+                              int out_rows, int out_y, const void* const* feats, int layout, const float* rt,
+                              const float* hyps, void* volume) {
+  if (!st || !feats || !rt || !hyps || !volume) return fail(DAMVS_E_ARG, "null argument");
+  if (B < 1 || N < 2 || N > kMaxViews || D < 1 || h < 2 || w < 2) return fail(DAMVS_E_SHAPE, "bad shape");
+  if (y0 < 0 || rows < 1 || y0 + rows > h) return fail(DAMVS_E_SHAPE, "rows [%d, %d) outside 0..%d", y0, y0 + rows, h);
+  if (out_y < 0 || out_y + rows > out_rows)
+    return fail(DAMVS_E_SHAPE, "rows [%d, %d) outside the %d-row output planes", out_y, out_y + rows, out_rows);
+  if (layout != DAMVS_LAYOUT_NHWC && layout != DAMVS_LAYOUT_CBLOCK) return fail(DAMVS_E_ARG, "layout %d", layout);
+  WarpArgs a = warp_args(st, B, N, st->C, D, h, w, feats, rt, hyps, volume);
+  a.y0 = y0;
+  a.rows = rows;
+  a.out_rows = out_rows;
+  a.out_y = out_y;
+  return hip_check(launch_warp_aggregate(reinterpret_cast<hipStream_t>(stream), st->dtype, st->mode, a,
+                                         layout == DAMVS_LAYOUT_CBLOCK),
+                   "warp_aggregate launch");
 }
 
 int damvs_regress(void* stream, int B, int D, int h, int w, const float* logits, const float* hyps,

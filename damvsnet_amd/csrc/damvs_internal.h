@@ -25,9 +25,11 @@ constexpr int kMaxPhases = 8;
 struct WarpArgs {
   const void* feats[kMaxViews];  // N views, view 0 = reference
   const float* rt;               // [B][N-1][12]
-  const float* hyps;             // [B][D][h][w]
-  void* out;                     // [B][D][h][w][C]
-  int B, N, C, D, h, w;
+  const float* hyps;             // [B][D][out_rows][w]
+  void* out;                     // [B][D][out_rows][w][C]
+  int B, N, C, D, h, w;          // h x w: the feature maps (and the full reference image grid)
+  int y0, rows;                  // computed: reference rows [y0, y0 + rows) (0, h: the whole image) ...
+  int out_rows, out_y;           // ... at rows [out_y, out_y + rows) of the hyps / out planes
   // adaptive weight net, BN folded: a = relu(sum_c k1[c] x_c * s1 + t1); wt = relu(a * s2 + t2)
   float k1[32];
   float s1, t1, s2, t2;

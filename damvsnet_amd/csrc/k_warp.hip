@@ -66,7 +66,7 @@ __device__ __forceinline__ void sample_bilinear(const T* __restrict__ src, int h
 template <typename T, int C, int MODE, bool BLK, int NVC>
 __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, int npix_blocks, int dchunk,
                                                              int ndchunks) {
-  const int hw = a.h * a.w;
+  const int hw = a.h * a.w, ohw = a.rows * a.w;  // feature-map plane, computed rows (y0 .. y0 + rows - 1)
   const int nblk = npix_blocks * ndchunks * a.B;
   const int bid = blockIdx.x, q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
   int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;  // bijective XCD remap
@@ -80,8 +80,9 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
   __syncthreads();
   const float4* s_rt = reinterpret_cast<const float4*>(s_rtf);
   const int p = pb * 256 + threadIdx.x;
-  if (p >= hw) return;
-  const int y = p / a.w, x = p - y * a.w;
+  if (p >= ohw) return;
+  const int yl = p / a.w, x = p - yl * a.w;
+  const int y = a.y0 + yl, pg = y * a.w + x;  // reference-image row and pixel
   const float fx = (float)x, fy = (float)y;
   const float kx = (float)a.w / (float)(a.w - 1), ky = (float)a.h / (float)(a.h - 1);
 
@@ -91,13 +92,13 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
     constexpr int E = Stor<T>::E;
 #pragma unroll
     for (int q = 0; q < C / E; ++q)
-      Stor<T>::load16(BLK ? f0 + ((size_t)q * hw + p) * E : f0 + (size_t)p * C + q * E, ref + q * E);
+      Stor<T>::load16(BLK ? f0 + ((size_t)q * hw + pg) * E : f0 + (size_t)pg * C + q * E, ref + q * E);
   }
 
   const float inv_n = 1.f / (float)a.N, inv_n1 = 1.f / (float)(a.N - 1);  // exact for N = 5 (the default)
   const int d0 = dc * dchunk, d1 = min(a.D, d0 + dchunk);
   for (int d = d0; d < d1; ++d) {
-    const size_t vox = ((size_t)b * a.D + d) * hw + p;
+    const size_t vox = (((size_t)b * a.D + d) * a.out_rows + a.out_y) * a.w + p;
     const float hyp = a.hyps[vox];
     float acc[C], sq[C];
 #pragma unroll
@@ -172,7 +173,7 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
 
 template <typename T, int MODE, bool BLK>
 hipError_t launch_c(hipStream_t s, const WarpArgs& a) {
-  const int npb = (a.h * a.w + 255) / 256;
+  const int npb = (a.rows * a.w + 255) / 256;
   // depth chunk: as long as possible (locality) while keeping >= ~4 blocks per CU in flight
   int dchunk = a.D;
   static const long long minblk = [] {

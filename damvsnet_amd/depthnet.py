@@ -45,6 +45,7 @@ class DepthNet(nn.Module):
             self.weight_net = nn.ModuleList([AggWeightNetVolume(c) for c in in_channels])
         self.compute_dtype = compute_dtype
         self._engines = {}
+        self.probe = None  # optional callable(stage_idx) -> 4 torch.cuda.Event (bench.py in-pipeline timing)
 
     def engine(self, stage_idx, cost_regularization, device):
         aggw = self.weight_net[stage_idx] if self.mode == "adaptive" else None
@@ -84,7 +85,8 @@ class DepthNet(nn.Module):
         hyps = depth_values.float().contiguous()
         pinit = prob_volume_init.float().contiguous() if prob_volume_init is not None else None
         depth, conf, var, prob = eng.forward(feats, proj_matrices.float().contiguous(), hyps, pinit,
-                                             want_prob=return_prob_volume)
+                                             want_prob=return_prob_volume,
+                                             probe=self.probe(stage_idx) if self.probe is not None else None)
         return {"depth": depth, "photometric_confidence": conf, "variance": var, "prob_volume": prob,
                 "depth_values": depth_values}
 

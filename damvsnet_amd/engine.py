@@ -31,7 +31,7 @@ class StageEngine:
         lib = _capi.load_library()
         if dtype not in DTYPES:
             raise TypeError("compute dtype must be float32 or bfloat16, got %r" % (dtype,))
-        self.dtype, self.device, self.C = dtype, device, costreg.in_channels
+        self.dtype, self.device, self.C, self.base = dtype, device, costreg.in_channels, costreg.base_channels
         self.mode = _capi.DAMVS_AGG_ADAPTIVE if agg_mode == "adaptive" else _capi.DAMVS_AGG_VARIANCE
         keep = []  # host tensors must outlive the create call
 
@@ -78,8 +78,9 @@ class StageEngine:
             self._ws = torch.empty(n.value, dtype=torch.uint8, device=self.device)
         return self._ws
 
-    def forward(self, feats_nhwc, proj, hyps, prob_init=None, want_prob=True):
-        """feats_nhwc: list of N (B,h,w,C) tensors of self.dtype; proj (B,N,2,4,4); hyps (B,D,h,w) float32."""
+    def forward(self, feats_nhwc, proj, hyps, prob_init=None, want_prob=True, probe=None):
+        """feats_nhwc: list of N (B,h,w,C) tensors of self.dtype; proj (B,N,2,4,4); hyps (B,D,h,w) float32.
+        probe: None or 4 torch.cuda.Event recorded before / after the warp, after the U-Net, after the regression."""
         N = len(feats_nhwc)
         B, h, w, C = feats_nhwc[0].shape
         D = hyps.shape[1]
@@ -90,9 +91,17 @@ class StageEngine:
         var = torch.empty_like(depth)
         prob = torch.empty(B, D, h, w, device=dev, dtype=torch.float32) if want_prob else None
         fptrs = (ctypes.c_void_p * N)(*[f.data_ptr() for f in feats_nhwc])
-        check(self._lib.damvs_stage_forward(self.handle, _capi.stream_ptr(dev), B, N, D, h, w, fptrs, ptr(proj),
-                                            ptr(hyps), ptr(prob_init), ptr(ws), ws.numel(), ptr(depth), ptr(conf),
-                                            ptr(var), ptr(prob)))
+        if probe is None:
+            check(self._lib.damvs_stage_forward(self.handle, _capi.stream_ptr(dev), B, N, D, h, w, fptrs, ptr(proj),
+                                                ptr(hyps), ptr(prob_init), ptr(ws), ws.numel(), ptr(depth), ptr(conf),
+                                                ptr(var), ptr(prob)))
+        else:
+            for e in probe:  # torch creates the HIP event at its first record
+                e.record()
+            evs = (ctypes.c_void_p * 4)(*[e.cuda_event for e in probe])
+            check(self._lib.damvs_stage_forward_probed(self.handle, _capi.stream_ptr(dev), B, N, D, h, w, fptrs,
+                                                       ptr(proj), ptr(hyps), ptr(prob_init), ptr(ws), ws.numel(),
+                                                       ptr(depth), ptr(conf), ptr(var), ptr(prob), evs))
         return depth, conf, var, prob
 
     # ---- split entry points (parity tests / sharded execution)
@@ -109,6 +118,44 @@ class StageEngine:
         check(self._lib.damvs_warp_aggregate(self.handle, _capi.stream_ptr(self.device), B, N, D, h, w, fptrs, layout,
                                              ptr(rt), ptr(hyps), ptr(vol)))
         return vol
+
+    def warp_aggregate_rows(self, feats, rt, hyps, h, y0, rows, out_y, out, layout=_capi.DAMVS_LAYOUT_NHWC):
+        """Aggregated volume of reference rows [y0, y0 + rows) from the whole feature maps (h rows), read from
+        hyps [B][D][R][w] and written to out [B][D][R][w][C] at rows [out_y, out_y + rows) (R = hyps.shape[2]);
+        bitwise the same voxels as warp_aggregate."""
+        N = len(feats)
+        B, D, R, w = hyps.shape
+        fptrs = (ctypes.c_void_p * N)(*[f.data_ptr() for f in feats])
+        check(self._lib.damvs_warp_aggregate_rows(self.handle, _capi.stream_ptr(self.device), B, N, D, h, w, y0, rows,
+                                                  R, out_y, fptrs, layout, ptr(rt), ptr(hyps), ptr(out)))
+        return out
+
+    def unet_layer(self, layer, D, h, w, inp, out):
+        """CostRegNet layer ``layer`` (0..9 = conv0..conv6, conv7, conv9, conv11) of a level-0 volume of
+        D x h x w; deconvs add into ``out`` in place (it holds the skip tensor)."""
+        B = inp.shape[0]
+        check(self._lib.damvs_costreg_layer(self.handle, _capi.stream_ptr(self.device), layer, B, D, h, w, ptr(inp),
+                                            ptr(out)))
+        return out
+
+    def unet_buffers(self, B, D, h, w):
+        """Level tensors c0..c6 (conv0..conv6 outputs, NDHWC) of a D x h x w volume."""
+        b = self.base
+        spec = ((0, b), (1, 2 * b), (1, 2 * b), (2, 4 * b), (2, 4 * b), (3, 8 * b), (3, 8 * b))
+        return [torch.empty(B, D >> l, h >> l, w >> l, c, device=self.device, dtype=self.dtype) for l, c in spec]
+
+    def regress_c0(self, c0, hyps, prob_init=None, want_prob=True, scratch=None):
+        """Prob conv + softmax regression on the U-Net output c0 [B][D][h][w][base] (damvs_stage_regress)."""
+        B, D, h, w, _ = c0.shape
+        dev = self.device
+        depth = torch.empty(B, h, w, device=dev, dtype=torch.float32)
+        conf, var = torch.empty_like(depth), torch.empty_like(depth)
+        prob = torch.empty(B, D, h, w, device=dev, dtype=torch.float32) if want_prob else None
+        if scratch is None:
+            scratch = torch.empty(B, D, h, w, device=dev, dtype=torch.float32)
+        check(self._lib.damvs_stage_regress(self.handle, _capi.stream_ptr(dev), B, D, h, w, ptr(c0), ptr(hyps),
+                                            ptr(prob_init), ptr(scratch), ptr(depth), ptr(conf), ptr(var), ptr(prob)))
+        return depth, conf, var, prob
 
     def costreg_logits(self, vol):
         B, D, h, w, C = vol.shape

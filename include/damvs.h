@@ -100,6 +100,14 @@ int damvs_stage_forward(const damvs_stage* st, void* stream, int B, int N, int D
                         void* workspace, size_t workspace_bytes, float* depth, float* conf, float* var,
                         float* prob);
 
+/* damvs_stage_forward with in-pipeline timing probes: events (NULL, or 4 hipEvent_t, any may be NULL) are
+ * recorded on `stream` before the warp + aggregation launch, after it, after the U-Net and after the
+ * regression -- the per-kernel-group durations of the stage as the product runs it (bench.py roofline). */
+int damvs_stage_forward_probed(const damvs_stage* st, void* stream, int B, int N, int D, int h, int w,
+                               const void* const* feats, const float* proj, const float* hyps, const float* prob_init,
+                               void* workspace, size_t workspace_bytes, float* depth, float* conf, float* var,
+                               float* prob, void* const* events);
+
 /* ---- split entry points (used by the parity tests and by sharded execution) ---- */
 
 /* Per (b, src view): 3x4 [R|t] of P_src * inv(P_ref) with P = [K E[:3,:4]; E[3]]
@@ -128,6 +136,32 @@ int damvs_block_channels(void* stream, int dtype, int N, int B, int h, int w, in
 /* CostRegNet forward incl. the final prob conv (models/module.py:532-541): logits [B][D][h][w]. */
 int damvs_costreg_logits(const damvs_stage* st, void* stream, int B, int D, int h, int w, const void* volume,
                          void* workspace, size_t workspace_bytes, float* logits);
+
+/* ---- pieces of one stage for sharded execution (damvsnet_amd/sharded.py: one depth map over P GPUs) ---- */
+
+/* The aggregated volume of reference rows [y0, y0 + rows) only (models/cas_mvsnet.py:26-87 restricted to
+ * those rows; the feature maps stay whole: [B][h][w][C] or channel-blocked per `layout`), read from / written
+ * to rows [out_y, out_y + rows) of planes of out_rows rows: hyps [B][D][out_rows][w], volume
+ * [B][D][out_rows][w][C] (a haloed H-slab; other rows untouched). Voxels are bitwise those of
+ * damvs_warp_aggregate. */
+int damvs_warp_aggregate_rows(const damvs_stage* st, void* stream, int B, int N, int D, int h, int w, int y0, int rows,
+                              int out_rows, int out_y, const void* const* feats, int layout, const float* rt,
+                              const float* hyps, void* volume);
+
+/* One CostRegNet layer (models/module.py:532-540; Conv3d / Deconv3d wrappers :117-202): layer 0..9 =
+ * conv0..conv6, conv7, conv9, conv11. D, h, w are the level-0 volume dims (multiples of 8); level l has
+ * D>>l, h>>l, w>>l. in: the layer input at its level ([B][Dl][hl][wl][cin]); out: its output. For
+ * conv7 / conv9 / conv11, `out` holds the skip tensor (conv4 / conv2 / conv0 output) on entry and
+ * relu(deconv(in)) + skip on exit (models/module.py:537-539). Zero padding at every tensor edge. */
+int damvs_costreg_layer(const damvs_stage* st, void* stream, int layer, int B, int D, int h, int w, const void* in,
+                        void* out);
+
+/* The tail of damvs_stage_forward: prob conv (models/module.py:541) + softmax regression, confidence and
+ * exp-variance (models/cas_mvsnet.py:105-124) on the U-Net output c0 [B][D][h][w][base].
+ * scratch: [B][D][h][w] float (used only when the fused kernels cannot hold a pixel's logits). */
+int damvs_stage_regress(const damvs_stage* st, void* stream, int B, int D, int h, int w, const void* c0,
+                        const float* hyps, const float* prob_init, float* scratch, float* depth, float* conf, float* var,
+                        float* prob);
 
 /* Softmax regression on logits (models/cas_mvsnet.py:105-124). prob_init / prob may be NULL. */
 int damvs_regress(void* stream, int B, int D, int h, int w, const float* logits, const float* hyps,
