@@ -86,6 +86,9 @@ template <> struct BufIO<float> {
   __device__ __forceinline__ static quad ldq(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
   }
+  __device__ __forceinline__ static quad ldq_dev(__amdgpu_buffer_rsrc_t r, uint32_t off) {  // device scope (sc1)
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+  }
   __device__ __forceinline__ static void addq(const quad& q, float* v) { v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w; }
   __device__ __forceinline__ static void stq(__amdgpu_buffer_rsrc_t r, uint32_t off, const float* v) {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, make_float4(v[0], v[1], v[2], v[3])), r, off, 0, 0);
@@ -102,6 +105,9 @@ template <> struct BufIO<bf16_t> {
   }
   __device__ __forceinline__ static quad ldq(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+  }
+  __device__ __forceinline__ static quad ldq_dev(__amdgpu_buffer_rsrc_t r, uint32_t off) {  // device scope (sc1)
+    return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16));
   }
   __device__ __forceinline__ static void addq(const quad& q, float* v) {
     v[0] += __uint_as_float(q.x << 16); v[1] += __uint_as_float(q.x & 0xffff0000u);

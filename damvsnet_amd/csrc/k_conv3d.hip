@@ -74,6 +74,16 @@ __device__ __forceinline__ void load4<bf16_t>(const bf16_t* p, float* r) {
 
 constexpr int kGroups = 4;  // 16-voxel column groups per wave (64 output voxels per wave)
 
+// DAMVS_DIAG_SKIP_EPI selects the bf16 in-place skip epilogue of conv3d_mfma_kernel in DIAGNOSTIC builds only
+// (tools/diag_skip_epilogue.py; the product is always 0): 0 = 16-byte records (lane group g+1 hands its 4
+// channels to g); 1 = the former 8-byte-per-lane form (skip loaded through the `rr` descriptor, stored through
+// `ro`); 2 = form 1 with one descriptor for both; 3 = form 1 with device-scope (sc1) skip loads, which miss the
+// CU's L1; 4 = form 1 with every skip load of the wave issued before its first store. Forms 1-4 also run the
+// x-pair deconv (XP) through the 8-byte path, as round 1 did before the 16-byte records.
+#ifndef DAMVS_DIAG_SKIP_EPI
+#define DAMVS_DIAG_SKIP_EPI 0
+#endif
+
 // Epilogue for 4 channels: bias, ReLU, skip add (after the ReLU, models/module.py:537-539), store.
 template <typename T>
 __device__ __forceinline__ void finish4(const ConvArgs& a, __amdgpu_buffer_rsrc_t ro, __amdgpu_buffer_rsrc_t rr,
@@ -148,7 +158,7 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int 
   const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * ES;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.resid ? a.resid : a.out, a.resid ? nout : 0);
-  constexpr bool kSkip16 = sizeof(T) == 2;
+  constexpr bool kSkip16 = sizeof(T) == 2 && DAMVS_DIAG_SKIP_EPI == 0;
   const bool skip16 = kSkip16 && a.resid && (a.Cout & 7) == 0;
 
   const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * a.Cin * ES);
@@ -181,7 +191,7 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int 
     if (ci >= a.Cin) { ci -= a.Cin; ++t; }
   }
 
-  if constexpr (XP) {
+  if constexpr (XP && DAMVS_DIAG_SKIP_EPI == 0) {
     // Cout = 8: lane group g + 1 hands its 4 channels to group g (g even), which then owns the whole
     // 8-channel record of output x = 2 qx + (g >> 1): one 16-byte (bf16) skip load and store per voxel.
     const bool lead = (g & 1) == 0;
@@ -250,18 +260,26 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int 
 #pragma unroll
     for (int i = 0; i < 4; ++i) bias[m][i] = cok[m] ? a.bias[co + i] : 0.f;
   }
+  const __amdgpu_buffer_rsrc_t rq = DAMVS_DIAG_SKIP_EPI == 2 ? ro : rr;
+  typename IO::quad q[kGroups][MT];
+  auto load_skip = [&](int j) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const uint32_t off = valid[j] && cok[m] ? (uint32_t)(pout[j] * a.Cout + m * 16 + cg) * ES : kOOB;
+      if (a.resid) q[j][m] = DAMVS_DIAG_SKIP_EPI == 3 ? IO::ldq_dev(rq, off) : IO::ldq(rq, off);
+    }
+  };
+  if (DAMVS_DIAG_SKIP_EPI == 4) {
+#pragma unroll
+    for (int j = 0; j < kGroups; ++j) load_skip(j);
+  }
 #pragma unroll
   for (int j = 0; j < kGroups; ++j) {
-    typename IO::quad q[MT];
+    if (DAMVS_DIAG_SKIP_EPI != 4) load_skip(j);
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const uint32_t off = (uint32_t)(pout[j] * a.Cout + m * 16 + cg) * ES;
-      if (a.resid) q[m] = IO::ldq(rr, valid[j] && cok[m] ? off : kOOB);
-    }
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const uint32_t off = (uint32_t)(pout[j] * a.Cout + m * 16 + cg) * ES;
-      finish4<T>(a, ro, rr, q[m], a.resid != nullptr, off, valid[j] && cok[m], bias[m], acc[j][m]);
+      finish4<T>(a, ro, rr, q[j][m], a.resid != nullptr, off, valid[j] && cok[m], bias[m], acc[j][m]);
     }
   }
 }
