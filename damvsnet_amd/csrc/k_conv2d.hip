@@ -719,6 +719,290 @@ hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a) {
   return hipErrorNotSupported;
 }
 
+// Wide-layer implicit GEMM (bf16; 128-channel cout blocks; Cin slices of 32; in_stride 1): the stride-1
+// GeoBlock convs at 128-256 channels and the k5 s2 transposed decoders' phases of GeoFeatureFusion
+// (models/geometry.py:381-433,475-480). A block owns 128 output channels x a 2-row x 64-column tile of
+// one phase's q-grid; its 4 waves form a 2 x 2 grid (wave (wm, wn): 4 cout tiles x q-row wn = 64 pixels,
+// 4 MFMA N-groups). Both MFMA operands come from LDS:
+//  * A: the block's 8 cout tiles of one K chunk (tap, 32-channel slice) = 8 KB of packed fragments, copied
+//    once per block (buffer loads at a wave-uniform SGPR offset, two chunks ahead, into alternating
+//    register pairs; written one chunk ahead) and read by the two waves of each cout half (the gather
+//    kernel streams 8 KB per wave per chunk through L1);
+//  * B: the slice's input halo ((2 + span - 1) x (64 + span - 1) pixels x 64 B), staged once per slice and
+//    read at every tap's offset; a pixel's 16-byte chunk sits at position chunk ^ ((pixel >> 2) & 3) so the
+//    16 lanes of a quarter-wave (16 consecutive pixels, one chunk) hit distinct banks.
+// One barrier per K chunk. (An LDS-DMA variant measured slower: hipcc drains every outstanding DMA before
+// each LDS read it cannot prove disjoint.)
+constexpr int WC = 64;   // q-tile columns; rows WR = 2 * RW (RW q-rows per wave)
+constexpr int WPER = 7;  // halo pieces per thread: up to 448 pixels
+
+template <bool TWO, int RW>
+__global__ __launch_bounds__(256) void conv2d_wide_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int nsl,
+                                                          int dmin, int span) {
+  typedef uint4 raw;
+  typedef BufIO<bf16_t> IO;
+  constexpr uint32_t ES = 2;
+  constexpr int WR = 2 * RW, NG = 4 * RW;  // q-tile rows; N-groups (16 pixels) per wave
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  raw* abuf = reinterpret_cast<raw*>(smem);  // 2 x 512 raws (8 KB per chunk)
+  const int HC = WC + span - 1, HP = (WR + span - 1) * HC;
+  raw* hbuf = abuf + 2 * 512;                // 2 x HP * 4 raws
+
+  // logical block = (tile, phase), phase fastest, XCD-contiguous
+  const int ntile = tiles_x * tiles_y * a.B;
+  const int nblk = ntile * a.nphase;
+  const int bid = blockIdx.x, q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tl = L / a.nphase;
+  const Conv2dPhase& ph = a.ph[L - tl * a.nphase];
+  const int tx = tl % tiles_x, ty = (tl / tiles_x) % tiles_y, b = tl / (tiles_x * tiles_y);
+  const int qy0 = ty * WR, qx0 = tx * WC;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int n = lane & 15, g = lane >> 4;
+  const int mt0 = blockIdx.y * 8;
+
+  __shared__ int s_toff[32];  // tap offset inside the halo, in pixels
+  if (tid < 25) s_toff[tid] = tid < ph.ntaps ? (ph.tap[tid][0] - dmin) * HC + (ph.tap[tid][1] - dmin) : 0;
+
+  const int nt = ph.ntaps;  // loop order (slice, tap); packed order chunk = tap * nsl + slice
+  const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack) + ((size_t)ph.w_off * a.MTtot + mt0) * 64;
+  const size_t cstride = (size_t)a.MTtot * 64;  // raws between consecutive packed chunks
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.wpack, 0x7fffffffLL);
+  const uint32_t wbase = (uint32_t)(((size_t)ph.w_off * a.MTtot + mt0) * 64 * 16);
+  const uint32_t cbytes = (uint32_t)a.MTtot * 64 * 16;  // bytes between consecutive packed chunks
+  const int npix = a.B * a.Hi * a.Wi;
+  const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.in0, (long long)npix * a.c0 * ES);
+  const __amdgpu_buffer_rsrc_t r1 = make_rsrc(TWO ? a.in1 : a.in0, TWO ? (long long)npix * a.c1 * ES : 0);
+  const int iy0 = qy0 + dmin, ix0 = qx0 + dmin, pb = b * a.Hi * a.Wi;
+  // this thread's halo pieces: input pixel index (-1: outside the image or past the halo) and the 16-byte
+  // chunk it fetches, the same for every slice
+  int hpix[WPER], hch[WPER];
+#pragma unroll
+  for (int k = 0; k < WPER; ++k) {
+    const int i = tid + k * 256;
+    const int p = i >> 2, slot = i & 3;
+    const int row = p / HC, col = p - row * HC;
+    const int iy = iy0 + row, ix = ix0 + col;
+    const bool ok = p < HP && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+    hpix[k] = ok ? pb + iy * a.Wi + ix : -1;
+    hch[k] = (slot ^ ((p >> 2) & 3)) * 8;
+  }
+  raw hreg[WPER];
+  auto hload = [&](int c) {
+    const bool second = TWO && c * 32 >= a.c0;
+    const int cs = second ? a.c1 : a.c0, cb = second ? c * 32 - a.c0 : c * 32;
+#pragma unroll
+    for (int k = 0; k < WPER; ++k) {
+      const uint32_t off = hpix[k] >= 0 ? (uint32_t)(hpix[k] * cs + cb + hch[k]) * ES : kOOB;
+      hreg[k] = (TWO && second) ? IO::frag(r1, off) : IO::frag(r0, off);
+    }
+  };
+  auto hstore = [&](int bi) {
+#pragma unroll
+    for (int k = 0; k < WPER; ++k) {
+      const int i = tid + k * 256;
+      if ((i >> 2) < HP) hbuf[bi * HP * 4 + i] = hreg[k];
+    }
+  };
+
+  f32x4_t acc[4][NG];  // [cout tile][N-group: q-row j / 4 of the wave, 16 columns j % 4]
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int j = 0; j < NG; ++j) acc[m][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  // One K chunk per barrier, slices outer and taps inner. A: chunk k + 2 is loaded (scalar offset: no
+  // per-chunk VGPR address math) into one register pair while the other pair (chunk k + 1) goes to LDS
+  // after chunk k's MFMAs; loads past the last chunk re-read it (unconditional: exact vmcnt counting).
+  // Halo of slice c + 1: loaded after tap 0's A store of slice c (hipcc counts the vmcnt in front of that
+  // store as if no halo load were pending, so issuing them later keeps them out of it), stored after the
+  // slice's last tap.
+  raw p0, p1, q0, q1;
+  int lc = 0, lt = 0;  // (slice, tap) of the next chunk to load, two ahead of the chunk computed
+  auto next = [&](int& cc, int& tt) {
+    if (++tt == nt) {
+      tt = 0;
+      cc = cc + 1 < nsl ? cc + 1 : cc;  // past the end: stays on the last slice (clamped re-read)
+    }
+  };
+  auto wld = [&](raw& x0, raw& x1) {
+    const uint32_t so = wbase + (uint32_t)(lt * nsl + lc) * cbytes;
+    x0 = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)tid * 16u, so, 0));
+    x1 = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(tid + 256) * 16u, so, 0));
+    if (!(lc == nsl - 1 && lt == nt - 1)) next(lc, lt);
+  };
+  wld(p0, p1);
+  wld(q0, q1);
+  hload(0);
+  abuf[tid] = p0;
+  abuf[tid + 256] = p1;
+  hstore(0);
+  __syncthreads();
+  const int lanepix = wn * RW * HC + n;
+  int k = 0;
+  auto step = [&](int c, int t, raw& ld0, raw& ld1, const raw& st0, const raw& st1) {
+    wld(ld0, ld1);
+    const raw* ab = abuf + (k & 1) * 512 + wm * 256 + lane;
+    raw af[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) af[m] = ab[m * 64];
+    // 16 pixels apart keeps (p >> 2) & 3: one swizzled address, the 4 N-groups at immediate offsets
+    raw bf[NG];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {  // one swizzled address per q-row (HC is not a multiple of 16)
+      const int px = s_toff[t] + lanepix + r * HC;
+      const raw* hb = hbuf + (c & 1) * HP * 4 + px * 4 + (g ^ ((px >> 2) & 3));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[r * 4 + j] = hb[j * 64];
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int j = 0; j < NG; ++j) Frag2<bf16_t>::mma(af[m], bf[j], acc[m][j]);
+    abuf[((k + 1) & 1) * 512 + tid] = st0;  // past the last chunk: a harmless copy
+    abuf[((k + 1) & 1) * 512 + tid + 256] = st1;
+    if (t == 0 && c + 1 < nsl) hload(c + 1);
+    if (t == nt - 1 && c + 1 < nsl) hstore((c + 1) & 1);
+    __syncthreads();
+    ++k;
+  };
+  int c = 0, t = 0;
+  const int nk = nt * nsl;
+  for (int kk = 0; kk < nk; kk += 2) {  // unrolled by two: the register pairs alternate statically
+    step(c, t, p0, p1, q0, q1);
+    if (++t == nt) { t = 0; ++c; }
+    if (kk + 1 < nk) {
+      step(c, t, q0, q1, p0, p1);
+      if (++t == nt) { t = 0; ++c; }
+    }
+  }
+
+  const int qyw = qy0 + wn * RW;  // the wave's first q-row
+  // the fp32 plane as trailing K chunks (tap x plane), as in conv2d_mfma_kernel
+  if (ph.gchunks > 0) {
+    const raw* __restrict__ wg = wsrc + (size_t)ph.kchunks * cstride + wm * 256 + lane;
+    const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.geo[0], ((long long)(a.B - 1) * a.geo_bstride[0] + a.Hi * a.Wi) * 4);
+    const int pg0 = b * (int)a.geo_bstride[0];
+    for (int s = 0; s < ph.gchunks; ++s) {
+      raw af[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) af[m] = wg[(size_t)s * cstride + m * 64];
+      float v[NG][8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int tt = s * 32 + g * 8 + e;
+        const bool tv = tt < nt;
+        const int dy = tv ? ph.tap[tt][0] : 0, dx = tv ? ph.tap[tt][1] : 0;
+#pragma unroll
+        for (int j = 0; j < NG; ++j) {
+          const int iy = qyw + (j >> 2) + dy, ix = qx0 + (j & 3) * 16 + n + dx;
+          const bool ok = tv && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+          v[j][e] = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(rg, ok ? (uint32_t)(pg0 + iy * a.Wi + ix) * 4u : kOOB, 0, 0));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NG; ++j) {
+        const raw xf = pack_vals<bf16_t>(v[j]);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) Frag2<bf16_t>::mma(af[m], xf, acc[m][j]);
+      }
+    }
+  }
+
+  // epilogue (as conv2d_mfma_kernel): residual before ReLU, ReLU, (upsampled) residual after, store
+  typedef typename IO::quad quad;
+  const int up = a.post_up, us = a.post_up >> 1;
+  const long long nout = (long long)a.B * a.Ho * a.Wo * a.cout;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout * ES);
+  const __amdgpu_buffer_rsrc_t rpre = make_rsrc(a.res_pre ? a.res_pre : a.out, a.res_pre ? nout * ES : 0);
+  const __amdgpu_buffer_rsrc_t rpost = make_rsrc(a.res_post ? a.res_post : a.out, a.res_post ? nout / (up * up) * ES : 0);
+  float bias[4][4];
+  bool cok[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int co = (mt0 + wm * 4 + m) * 16 + g * 4;
+    cok[m] = co < a.cout;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[m][i] = a.bias[co + i];  // padded to cout_pad
+  }
+#pragma unroll
+  for (int j = 0; j < NG; ++j) {
+    const int qy = qyw + (j >> 2), qx = qx0 + (j & 3) * 16 + n;
+    const int oy = qy * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
+    const bool vok = qy < a.Hq && qx < a.Wq;
+    const int pout = (b * a.Ho + oy) * a.Wo + ox;
+    const int ppost = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
+    quad qpre[4], qpost[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const bool ok = vok && cok[m];
+      const int co = (mt0 + wm * 4 + m) * 16 + g * 4;
+      if (a.res_pre) qpre[m] = IO::ldq(rpre, ok ? (uint32_t)(pout * a.cout + co) * ES : kOOB);
+      if (a.res_post) qpost[m] = IO::ldq(rpost, ok ? (uint32_t)(ppost * a.cout + co) * ES : kOOB);
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      float r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = acc[m][j][i] + bias[m][i];
+      if (a.res_pre) IO::addq(qpre[m], r);
+      if (a.relu) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = fmaxf(r[i], 0.f);
+      }
+      if (a.res_post) IO::addq(qpost[m], r);
+      const int co = (mt0 + wm * 4 + m) * 16 + g * 4;
+      IO::stq(ro, vok && cok[m] ? (uint32_t)(pout * a.cout + co) * ES : kOOB, r);
+    }
+  }
+}
+
+// Returns hipErrorNotSupported when the wide kernel does not take the layer (bf16 callers only).
+hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
+  static const bool off = [] {
+    const char* v = getenv("DAMVS_CONV2D_WIDE");
+    return v && v[0] == '0';
+  }();
+  if (off || a.in_stride != 1 || a.xpair || a.ngeo > 1 || a.MTtot % 8 || a.c0 % 32 || a.c1 % 32 || a.c0 + a.c1 < 64)
+    return hipErrorNotSupported;
+  int dmin = 0, dmax = 0;
+  for (int p = 0; p < a.nphase; ++p)
+    for (int t = 0; t < a.ph[p].ntaps; ++t)
+      for (int d = 0; d < 2; ++d) {
+        dmin = a.ph[p].tap[t][d] < dmin ? a.ph[p].tap[t][d] : dmin;
+        dmax = a.ph[p].tap[t][d] > dmax ? a.ph[p].tap[t][d] : dmax;
+      }
+  const int span = dmax - dmin + 1;
+  static const int rw_env = [] {
+    const char* v = getenv("DAMVS_CONV2D_WIDE_RW");
+    return v ? atoi(v) : 1;
+  }();
+  // DAMVS_CONV2D_WIDE_RW=2: two q-rows per wave (32 MFMAs a chunk) when the taller halo fits the pieces.
+  // Off by default: 182 VGPRs + 128 AGPRs leave one wave per SIMD (case N 318 us vs 270-278 us at RW=1).
+  const int RW = rw_env == 2 && (4 + span - 1) * (WC + span - 1) * 4 <= WPER * 256 ? 2 : 1;
+  const int WR = 2 * RW;
+  const int HP = (WR + span - 1) * (WC + span - 1);
+  if (HP * 4 > WPER * 256) return hipErrorNotSupported;
+  for (int p = 0; p < a.nphase; ++p)  // geo taps beyond one K chunk; fewer than 4 taps (halo schedule)
+    if (a.ph[p].gchunks > 1 || a.ph[p].ntaps < 4) return hipErrorNotSupported;
+  const int tx = (a.Wq + WC - 1) / WC, ty = (a.Hq + WR - 1) / WR;
+  const int nsl = (a.c0 + a.c1) / 32;
+  const size_t smem = 2 * 512 * 16 + 2 * (size_t)HP * 64;
+  const long long nblk = (long long)tx * ty * a.B * a.nphase;
+  const dim3 grid((unsigned)nblk, (unsigned)(a.MTtot / 8));
+  auto k = RW == 2 ? (a.c1 > 0 ? conv2d_wide_kernel<true, 2> : conv2d_wide_kernel<false, 2>)
+                   : (a.c1 > 0 ? conv2d_wide_kernel<true, 1> : conv2d_wide_kernel<false, 1>);
+  if (smem > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)smem);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, grid, dim3(256), smem, s, a, tx, ty, nsl, dmin, span);
+  return hipGetLastError();
+}
+
 // True when the layer is a plain 3x3 stride-1 padding-1 conv with dense row-major taps.
 bool lds3_ok(const Conv2dArgs& a) {
   if (a.nphase != 1 || a.out_stride != 1 || a.in_stride != 1 || a.ph[0].ntaps != 9 || a.ngeo != 0 || a.c1 != 0 ||
@@ -937,6 +1221,10 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
     if (e != hipErrorNotSupported) return e;
     e = launch_halo<T>(s, a);
     if (e != hipErrorNotSupported) return e;
+    if constexpr (T_is_bf16<T>::value) {
+      e = launch_wide(s, a);
+      if (e != hipErrorNotSupported) return e;
+    }
   }
   // Widest cout tile (each loaded input fragment feeds MT MFMAs) that still puts about one wave on
   // every SIMD: the low-resolution GeoFeatureFusion layers have few pixels and many channels.

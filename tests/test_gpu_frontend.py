@@ -53,6 +53,10 @@ CASES = [
     (True, 4, 2, 1, 0, 16, 0, (), 8, False, False, 0),              # x-pair phases: FPN top (k4 s2), cout 8
     (True, 5, 2, 2, 1, 16, 0, (), 8, True, True, 2),                # x-pair + both residuals (post up 2)
     (True, 3, 2, 1, 1, 16, 16, (), 8, True, False, 1),              # x-pair, two inputs
+    (False, 3, 1, 1, 0, 128, 0, (0,), 128, True, True, 0),          # wide kernel: GeoBlock conv2 (plane first)
+    (False, 3, 1, 1, 0, 128, 128, (256,), 256, True, True, 2),      # wide: two inputs + plane, both residuals
+    (True, 5, 2, 2, 1, 256, 0, (), 128, True, False, 1),            # wide: k5 s2 transposed decoder + skip
+    (False, 1, 1, 0, 0, 64, 0, (64,), 128, False, False, 0),        # wide: 1x1 (GeoBlock downsample)
 ]
 
 
