@@ -103,11 +103,15 @@ __global__ __launch_bounds__(256) void regress_kernel(int B, int D, int hw, cons
 }
 
 // Fused prob conv + regression. One 256-thread block owns an 8 x 32 pixel tile for all D planes:
-// each input plane's (8+2) x (32+2) x Cb halo tile is staged once in LDS (double-buffered, one
-// barrier per plane, next plane's global loads issued before this plane's FMAs), every thread slides
-// its 3x3x3 window over the planes keeping the two open logits in registers, completed logits go to
-// an LDS column [D][256] and the regression runs from there. Logits never reach HBM.
+// each input plane's (8+2) x (32+2) x Cb halo tile is staged once in LDS as fp32 (double-buffered, one
+// barrier per plane, next plane's global loads issued before this plane's FMAs; bf16 is widened once
+// per voxel at staging, not once per tap), every thread slides its 3x3x3 window over the planes keeping
+// the two open logits in registers, completed logits go to an LDS column [D][256] and the regression
+// runs from there. Logits never reach HBM. The channel sums run as packed fp32 FMAs (even / odd channel
+// partial sums, added at the end of the plane) with the 72 weights of one kernel row as scalar operands
+// (the ky loop is not unrolled: all 216 weights at once would spill to VGPR lanes).
 constexpr int kTY = 8, kTX = 32, kHY = kTY + 2, kHX = kTX + 2;
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 // TWO: first pass of the two-pass form — the same LDS-tiled prob conv, logits (+prob_init) written
 // to HBM ([B][D][h][w], argument `prob`) for regress_kernel; LDS then holds only the plane tiles, so
@@ -120,13 +124,16 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
                                                            float* __restrict__ conf, float* __restrict__ var,
                                                            float* __restrict__ prob) {
   constexpr int E = Stor<T>::E;
-  constexpr int CH = CB / E;                 // 16-byte chunks per voxel
-  constexpr int TILE_CHUNKS = kHY * kHX * CH;
+  constexpr int CH = CB / E;                 // 16-byte storage chunks per voxel
+  constexpr int NVOX = kHY * kHX;
+  constexpr int TILE_CHUNKS = NVOX * CH;
   constexpr int PER_T = (TILE_CHUNKS + 255) / 256;
+  constexpr int FQ = CB / 4;                 // fp32 quads per voxel in LDS, quad-major ([FQ][NVOX]):
+                                             // 16 consecutive pixels read 16 consecutive quads
   typedef typename std::conditional<sizeof(T) == 4, float4, uint4>::type raw;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  raw* tile = reinterpret_cast<raw*>(smem);                      // 2 x TILE_CHUNKS (double buffer)
-  float* lg = reinterpret_cast<float*>(tile + 2 * TILE_CHUNKS);  // [D][256] logits, column per thread
+  float4* tile = reinterpret_cast<float4*>(smem);               // 2 x FQ x NVOX (double buffer)
+  float* lg = reinterpret_cast<float*>(tile + 2 * FQ * NVOX);   // [D][256] logits, column per thread
 
   const int tid = threadIdx.x;
   const int ty = tid / kTX, tx = tid % kTX;
@@ -153,7 +160,19 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
 #pragma unroll
     for (int k = 0; k < PER_T; ++k) {
       const int c = tid + k * 256;
-      if (c < TILE_CHUNKS) tile[buf * TILE_CHUNKS + c] = regs[k];
+      if (c < TILE_CHUNKS) {
+        const int vox = c / CH, part = c % CH;
+        float4* dst = tile + buf * FQ * NVOX + part * (E / 4) * NVOX + vox;
+        if constexpr (sizeof(T) == 4) {
+          dst[0] = regs[k];
+        } else {
+          const uint4 r = regs[k];
+          dst[0] = make_float4(__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u),
+                               __uint_as_float(r.y << 16), __uint_as_float(r.y & 0xffff0000u));
+          dst[NVOX] = make_float4(__uint_as_float(r.z << 16), __uint_as_float(r.z & 0xffff0000u),
+                                  __uint_as_float(r.w << 16), __uint_as_float(r.w & 0xffff0000u));
+        }
+      }
     }
   };
 
@@ -163,50 +182,44 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
   float am1 = 0.f, a0 = 0.f;
   for (int pl = 0; pl < D; ++pl) {
     if (pl + 1 < D) gload(pl + 1);
-    const raw* tb = tile + (pl & 1) * TILE_CHUNKS;
-    float c0 = 0.f, c1 = 0.f, c2 = 0.f;
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+    const float4* tb = tile + (pl & 1) * FQ * NVOX + ty * kHX + tx;
+    f32x2_t c0 = {0.f, 0.f}, c1 = {0.f, 0.f}, c2 = {0.f, 0.f};
+#pragma unroll 1
+    for (int ky = 0; ky < 3; ++ky) {
+      // wave-uniform weights through the scalar cache (SGPR operands), one kernel row per iteration
+      const float* wr = wprob + ky * 3 * CB;
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         float v[CB];
-        const raw* src = tb + ((ty + ky) * kHX + tx + kx) * CH;
 #pragma unroll
-        for (int q = 0; q < CH; ++q) {
-          raw r = src[q];
-          if constexpr (sizeof(T) == 4) {
-            v[q * 4 + 0] = r.x; v[q * 4 + 1] = r.y; v[q * 4 + 2] = r.z; v[q * 4 + 3] = r.w;
-          } else {
-            const uint32_t u[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              v[q * 8 + 2 * i] = __uint_as_float(u[i] << 16);
-              v[q * 8 + 2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
-            }
-          }
+        for (int q = 0; q < FQ; ++q) {
+          const float4 f = tb[q * NVOX + ky * kHX + kx];
+          v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
         }
-        // wave-uniform weights through the scalar cache (SGPR operands of v_fmac)
-        const float* w0 = wprob + ((0 * 3 + ky) * 3 + kx) * CB;
-        const float* w1 = wprob + ((1 * 3 + ky) * 3 + kx) * CB;
-        const float* w2 = wprob + ((2 * 3 + ky) * 3 + kx) * CB;
+        const float* w0 = wr + kx * CB;           // dz = 0: w[((dz * 3 + ky) * 3 + kx) * CB + c]
+        const float* w1 = wr + 9 * CB + kx * CB;  // dz = 1
+        const float* w2 = wr + 18 * CB + kx * CB; // dz = 2
 #pragma unroll
-        for (int c = 0; c < CB; ++c) {
-          c0 += w0[c] * v[c];
-          c1 += w1[c] * v[c];
-          c2 += w2[c] * v[c];
+        for (int c = 0; c < CB; c += 2) {
+          const f32x2_t x = {v[c], v[c + 1]};
+          c0 += (f32x2_t){w0[c], w0[c + 1]} * x;
+          c1 += (f32x2_t){w1[c], w1[c + 1]} * x;
+          c2 += (f32x2_t){w2[c], w2[c + 1]} * x;
         }
       }
+    }
+    const float s0 = c0.x + c0.y, s1 = c1.x + c1.y, s2 = c2.x + c2.y;
     if (TWO) {
       const int y = y0 + ty, x = x0 + tx;
       if (pl >= 1 && y < h && x < w) {
         const size_t o = (((size_t)b * D + pl - 1) * h + y) * w + x;
-        prob[o] = am1 + c2 + (prob_init ? prob_init[o] : 0.f);
+        prob[o] = am1 + s2 + (prob_init ? prob_init[o] : 0.f);
       }
     } else if (pl >= 1) {
-      lg[(pl - 1) * 256 + tid] = am1 + c2;
+      lg[(pl - 1) * 256 + tid] = am1 + s2;
     }
-    am1 = a0 + c1;
-    a0 = c0;
+    am1 = a0 + s1;
+    a0 = s0;
     if (pl + 1 < D) lstore((pl + 1) & 1);
     __syncthreads();
   }
@@ -375,8 +388,7 @@ __global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int
 
 template <typename T, int CB>
 size_t prob_regress_smem(int D) {
-  constexpr int CH = CB / Stor<T>::E;
-  return 2 * (size_t)kHY * kHX * CH * 16 + (size_t)D * 256 * 4;
+  return 2 * (size_t)kHY * kHX * CB * 4 + (size_t)D * 256 * 4;  // fp32 plane tiles + logit column
 }
 
 template <typename T, int CB>

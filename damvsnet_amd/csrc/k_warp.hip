@@ -22,39 +22,52 @@ namespace damvs {
 
 namespace {
 
-// Bilinear sample of C channels at (ix, iy), zero padding. Branch-free: invalid taps load from a
-// clamped in-bounds address with weight 0 (all four loads issue back to back). BLK selects the
-// channel-blocked layout [C/E][h][w][E] (one contiguous 16-byte plane per chunk: a wave's gather
-// touches half the cache lines of plain NHWC for C > E).
-template <typename T, int C, bool BLK>
-__device__ __forceinline__ void sample_bilinear(const T* __restrict__ src, int h, int w, float ix, float iy, float* s) {
-  constexpr int E = Stor<T>::E;
+// One 16-byte storage record -> E floats.
+template <typename T> struct Rec16;
+template <> struct Rec16<float> {
+  __device__ __forceinline__ static void unpack(const uint4& q, float* v) {
+    v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y); v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
+  }
+};
+template <> struct Rec16<bf16_t> {
+  __device__ __forceinline__ static void unpack(const uint4& q, float* v) {
+    const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(u[i] << 16);
+      v[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+  }
+};
+
+// Bilinear footprint of one sample at (ix, iy): byte offsets of the nw, ne, sw, se pixel records inside one
+// batch element's map (rec bytes per record) and their weights. A corner outside the map gets the offset
+// kOOB, so its buffer load returns 0: grid_sample's zero padding without a weight select. Samples far
+// outside (or NaN) are moved to (-4, -4), where all four corners are outside.
+struct Taps {
+  uint32_t off[4];
+  float wt[4];
+};
+__device__ __forceinline__ Taps bilinear_taps(int h, int w, uint32_t rec, float ix, float iy) {
   const bool inside = ix > -2.f && ix < (float)w + 1.f && iy > -2.f && iy < (float)h + 1.f;  // false for NaN
   const float cx = inside ? ix : -4.f, cy = inside ? iy : -4.f;
   const float x0f = floorf(cx), y0f = floorf(cy);
   const int x0 = (int)x0f, y0 = (int)y0f;
   const float wx1 = cx - x0f, wx0 = (x0f + 1.f) - cx;
   const float wy1 = cy - y0f, wy0 = (y0f + 1.f) - cy;
-  float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};  // nw, ne, sw, se
-  int idx[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int xx = x0 + (k & 1), yy = y0 + (k >> 1);
-    const bool ok = xx >= 0 && xx < w && yy >= 0 && yy < h;
-    idx[k] = ok ? yy * w + xx : 0;
-    wt[k] = ok ? wt[k] : 0.f;
-  }
-  const size_t plane = (size_t)h * w * E;
-#pragma unroll
-  for (int q = 0; q < C / E; ++q) {
-    float v[4][E];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      Stor<T>::load16(BLK ? src + q * plane + (size_t)idx[k] * E : src + (size_t)idx[k] * C + q * E, v[k]);
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-      s[q * E + e] = ((v[0][e] * wt[0] + v[1][e] * wt[1]) + v[2][e] * wt[2]) + v[3][e] * wt[3];
-  }
+  Taps t;
+  t.wt[0] = wx0 * wy0;
+  t.wt[1] = wx1 * wy0;
+  t.wt[2] = wx0 * wy1;
+  t.wt[3] = wx1 * wy1;
+  const bool vx0 = (unsigned)x0 < (unsigned)w, vx1 = (unsigned)(x0 + 1) < (unsigned)w;
+  const bool vy0 = (unsigned)y0 < (unsigned)h, vy1 = (unsigned)(y0 + 1) < (unsigned)h;
+  const uint32_t o = (uint32_t)(y0 * w + x0) * rec, ow = (uint32_t)w * rec;  // wraps for x0 / y0 = -1: fine
+  t.off[0] = vx0 && vy0 ? o : kOOB;
+  t.off[1] = vx1 && vy0 ? o + rec : kOOB;
+  t.off[2] = vx0 && vy1 ? o + ow : kOOB;
+  t.off[3] = vx1 && vy1 ? o + ow + rec : kOOB;
+  return t;
 }
 
 // Work decomposition (locality): a block owns 256 consecutive pixels of one image row band and a
@@ -63,9 +76,20 @@ __device__ __forceinline__ void sample_bilinear(const T* __restrict__ src, int h
 // inside a narrow band of each source image; blocks are dealt so that each XCD gets a contiguous
 // range of (pixel-chunk, depth-chunk) work and its L2 holds that band (the naive (pixels, D) grid
 // spreads every depth slice over all 8 XCDs and serves the gathers from the Infinity Cache).
+//
+// Per thread the depth-independent part of each view's homography (the ray R [x y 1]^T) is computed
+// once; the cameras' translations are block-uniform. Gathers are buffer loads with 32-bit offsets (the
+// batch element and channel chunk in the scalar offset), so a tap costs one select instead of 64-bit
+// address arithmetic and a weight select. With NVC > 0 (the source-view count a compile-time constant)
+// the (depth, view) sequence is software-pipelined one view deep: the 4 x C/E records of the next view
+// (across the depth boundary too, from a hypothesis loaded a plane ahead) are in flight while the
+// current view is reduced, and the loads are unconditional (the last plane re-reads its own last
+// view) so the vmcnt waits count exactly.
 template <typename T, int C, int MODE, bool BLK, int NVC>
 __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, int npix_blocks, int dchunk,
                                                              int ndchunks) {
+  constexpr int E = Stor<T>::E, NQ = C / E;
+  static_assert(NVC % 2 == 0, "the view pipeline alternates two register sets");
   const int hw = a.h * a.w, ohw = a.rows * a.w;  // feature-map plane, computed rows (y0 .. y0 + rows - 1)
   const int nblk = npix_blocks * ndchunks * a.B;
   const int bid = blockIdx.x, q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
@@ -73,12 +97,10 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
   const int dc = L % ndchunks; L /= ndchunks;
   const int pb = L % npix_blocks;
   const int b = L / npix_blocks;
-  // this batch element's [N-1][12] source cameras in LDS: the per-plane reads below are broadcast
-  // ds_reads instead of 12 vector-memory loads per view per plane through the (gather-bound) TA
+  // this batch element's [N-1][12] source cameras in LDS (broadcast reads)
   __shared__ __attribute__((aligned(16))) float s_rtf[(kMaxViews - 1) * 12];
   if (threadIdx.x < (a.N - 1) * 12) s_rtf[threadIdx.x] = a.rt[(size_t)b * (a.N - 1) * 12 + threadIdx.x];
   __syncthreads();
-  const float4* s_rt = reinterpret_cast<const float4*>(s_rtf);
   const int p = pb * 256 + threadIdx.x;
   if (p >= ohw) return;
   const int yl = p / a.w, x = p - yl * a.w;
@@ -86,65 +108,60 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
   const float fx = (float)x, fy = (float)y;
   const float kx = (float)a.w / (float)(a.w - 1), ky = (float)a.h / (float)(a.h - 1);
 
+  // byte geometry of a feature map: record = one pixel (NHWC) or one pixel's chunk (blocked)
+  const uint32_t bbytes = (uint32_t)hw * C * sizeof(T);
+  const uint32_t rec = BLK ? 16u : (uint32_t)(C * sizeof(T));
+  const uint32_t qstep = BLK ? (uint32_t)hw * 16u : 16u;  // bytes between a record's channel chunks
+  const uint32_t sb = (uint32_t)b * bbytes;
+  const long long fbytes = (long long)a.B * bbytes;
+
   float ref[C];
   if (MODE != AGG_WARP_ONLY) {
-    const T* f0 = reinterpret_cast<const T*>(a.feats[0]) + (size_t)b * hw * C;
-    constexpr int E = Stor<T>::E;
+    const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.feats[0], fbytes);
 #pragma unroll
-    for (int q = 0; q < C / E; ++q)
-      Stor<T>::load16(BLK ? f0 + ((size_t)q * hw + pg) * E : f0 + (size_t)pg * C + q * E, ref + q * E);
+    for (int q = 0; q < NQ; ++q)
+      Rec16<T>::unpack(__builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r0, (uint32_t)pg * rec, sb + q * qstep, 0)),
+                       ref + q * E);
   }
-
   const float inv_n = 1.f / (float)a.N, inv_n1 = 1.f / (float)(a.N - 1);  // exact for N = 5 (the default)
   const int d0 = dc * dchunk, d1 = min(a.D, d0 + dchunk);
-  for (int d = d0; d < d1; ++d) {
-    const size_t vox = (((size_t)b * a.D + d) * a.out_rows + a.out_y) * a.w + p;
-    const float hyp = a.hyps[vox];
-    float acc[C], sq[C];
+  auto vox_of = [&](int d) { return (((size_t)b * a.D + d) * a.out_rows + a.out_y) * a.w + p; };
+
+  // per-channel reduction of one view's sample into the running aggregate
+  auto reduce = [&](const uint4* rv, const float* wt, float* acc, float* sq) {
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      acc[c] = (MODE == AGG_VARIANCE) ? ref[c] : 0.f;
-      sq[c] = (MODE == AGG_VARIANCE) ? ref[c] * ref[c] : 0.f;
-    }
-    // NVC > 0: the source-view count is a compile-time constant and the view loop unrolls, so the
-    // gathers of several views are in flight together
-    const int nviews = NVC > 0 ? NVC + 1 : a.N;
-    constexpr int kUnrollV = NVC > 0 ? NVC : 1;
-#pragma unroll kUnrollV
-    for (int v = 1; v < nviews; ++v) {
-      const float4 m0 = s_rt[(v - 1) * 3], m1 = s_rt[(v - 1) * 3 + 1], m2 = s_rt[(v - 1) * 3 + 2];
-      const float m[12] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w, m2.x, m2.y, m2.z, m2.w};
-      const float rx = m[0] * fx + m[1] * fy + m[2];
-      const float ry = m[3] * fx + m[4] * fy + m[5];
-      const float rz = m[6] * fx + m[7] * fy + m[8];
-      const float qx = rx * hyp + m[9], qy = ry * hyp + m[10], qz = rz * hyp + m[11];
-      // g = (q/qz) / ((W-1)/2) - 1 and ix = ((g + 1) W - 1) / 2 fold to ix = (q/qz) W/(W-1) - 1/2:
-      // one reciprocal instead of four IEEE divisions (coordinates agree to ~1 ulp)
-      const float iz = __builtin_amdgcn_rcpf(qz);
-      const float ix = qx * iz * kx - 0.5f;
-      const float iy = qy * iz * ky - 0.5f;
-      float s[C];
-      sample_bilinear<T, C, BLK>(reinterpret_cast<const T*>(a.feats[v]) + (size_t)b * hw * C, a.h, a.w, ix, iy, s);
+    for (int q = 0; q < NQ; ++q) {
+      float v[4][E];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) Rec16<T>::unpack(rv[q * 4 + k], v[k]);
+      float s[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) s[e] = ((v[0][e] * wt[0] + v[1][e] * wt[1]) + v[2][e] * wt[2]) + v[3][e] * wt[3];
       if (MODE == AGG_WARP_ONLY) {
 #pragma unroll
-        for (int c = 0; c < C; ++c) acc[c] = s[c];
+        for (int e = 0; e < E; ++e) acc[q * E + e] = s[e];
       } else if (MODE == AGG_VARIANCE) {
 #pragma unroll
-        for (int c = 0; c < C; ++c) { acc[c] += s[c]; sq[c] += s[c] * s[c]; }
+        for (int e = 0; e < E; ++e) { acc[q * E + e] += s[e]; sq[q * E + e] += s[e] * s[e]; }
       } else {
-        float dot = 0.f;
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-          const float df = ref[c] - s[c];
-          s[c] = df * df;
-          dot += a.k1[c] * s[c];
+        for (int e = 0; e < E; ++e) {
+          const float df = ref[q * E + e] - s[e];
+          sq[q * E + e] = df * df;  // adaptive: the squared difference, weighted below
         }
-        const float a1 = fmaxf(dot * a.s1 + a.t1, 0.f);
-        const float wt = fmaxf(a1 * a.s2 + a.t2, 0.f) + 1.f;
-#pragma unroll
-        for (int c = 0; c < C; ++c) acc[c] += wt * s[c];
       }
     }
+    if (MODE == AGG_ADAPTIVE) {
+      float dot = 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) dot += a.k1[c] * sq[c];
+      const float a1 = fmaxf(dot * a.s1 + a.t1, 0.f);
+      const float wv = fmaxf(a1 * a.s2 + a.t2, 0.f) + 1.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] += wv * sq[c];
+    }
+  };
+  auto finish = [&](int d, float* acc, float* sq) {
     float o[C];
     if (MODE == AGG_VARIANCE) {
 #pragma unroll
@@ -159,13 +176,107 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
 #pragma unroll
       for (int c = 0; c < C; ++c) o[c] = acc[c];
     }
-    store_vec<T, C>(reinterpret_cast<T*>(a.out) + vox * C, o);
+    store_vec<T, C>(reinterpret_cast<T*>(a.out) + vox_of(d) * C, o);
+  };
+  auto init = [&](float* acc, float* sq) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      acc[c] = (MODE == AGG_VARIANCE) ? ref[c] : 0.f;
+      sq[c] = (MODE == AGG_VARIANCE) ? ref[c] * ref[c] : 0.f;
+    }
+  };
+
+  if constexpr (NVC > 0) {
+    // source view j = 1 + v: ray (per lane), translation (block-uniform) and descriptor
+    float rx[NVC], ry[NVC], rz[NVC], tx[NVC], ty[NVC], tz[NVC];
+    __amdgpu_buffer_rsrc_t rs[NVC];
+    auto uniform = [](float f) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(f))); };
+#pragma unroll
+    for (int v = 0; v < NVC; ++v) {
+      const float* m = s_rtf + v * 12;
+      rx[v] = m[0] * fx + m[1] * fy + m[2];
+      ry[v] = m[3] * fx + m[4] * fy + m[5];
+      rz[v] = m[6] * fx + m[7] * fy + m[8];
+      tx[v] = uniform(m[9]);
+      ty[v] = uniform(m[10]);
+      tz[v] = uniform(m[11]);
+      rs[v] = make_rsrc(a.feats[v + 1], fbytes);
+    }
+    auto taps = [&](int v, float hyp) {
+      const float qx = rx[v] * hyp + tx[v], qy = ry[v] * hyp + ty[v], qz = rz[v] * hyp + tz[v];
+      // g = (q/qz) / ((W-1)/2) - 1 and ix = ((g + 1) W - 1) / 2 fold to ix = (q/qz) W/(W-1) - 1/2:
+      // one reciprocal instead of four IEEE divisions (coordinates agree to ~1 ulp)
+      const float iz = __builtin_amdgcn_rcpf(qz);
+      return bilinear_taps(a.h, a.w, rec, qx * iz * kx - 0.5f, qy * iz * ky - 0.5f);
+    };
+    auto issue = [&](int v, const Taps& t, uint4* rv, float* wt) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          rv[q * 4 + k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs[v], t.off[k], sb + q * qstep, 0));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wt[k] = t.wt[k];
+    };
+    uint4 ra[4 * NQ], rb[4 * NQ];
+    float wa[4], wb[4];
+    float hyp = a.hyps[vox_of(d0)];
+    float hyp_n = a.hyps[vox_of(min(d0 + 1, d1 - 1))];
+    issue(0, taps(0, hyp), ra, wa);
+    for (int d = d0; d < d1; ++d) {
+      const float hyp_nn = a.hyps[vox_of(min(d + 2, d1 - 1))];  // two planes ahead, first in the plane's loads
+      float acc[C], sq[C];
+      init(acc, sq);
+      // view v's records are in (cur, wcur); the next (view, plane)'s go to (nxt, wnxt) before v is reduced
+      auto step = [&](int v, const uint4* cur, const float* wcur, uint4* nxt, float* wnxt) {
+        if (v + 1 < NVC) issue(v + 1, taps(v + 1, hyp), nxt, wnxt);
+        else issue(0, taps(0, hyp_n), nxt, wnxt);  // next plane's first view (the last plane: a re-read)
+        reduce(cur, wcur, acc, sq);
+      };
+#pragma unroll
+      for (int v = 0; v < NVC; v += 2) {
+        step(v, ra, wa, rb, wb);
+        step(v + 1, rb, wb, ra, wa);
+      }
+      hyp = hyp_n;
+      hyp_n = hyp_nn;
+      finish(d, acc, sq);
+    }
+  } else {
+    const int nviews = a.N;
+    for (int d = d0; d < d1; ++d) {
+      const float hyp = a.hyps[vox_of(d)];
+      float acc[C], sq[C];
+      init(acc, sq);
+      for (int j = 1; j < nviews; ++j) {
+        const float* m = s_rtf + (j - 1) * 12;
+        const float rx = m[0] * fx + m[1] * fy + m[2];
+        const float ry = m[3] * fx + m[4] * fy + m[5];
+        const float rz = m[6] * fx + m[7] * fy + m[8];
+        const float qx = rx * hyp + m[9], qy = ry * hyp + m[10], qz = rz * hyp + m[11];
+        const float iz = __builtin_amdgcn_rcpf(qz);
+        const Taps t = bilinear_taps(a.h, a.w, rec, qx * iz * kx - 0.5f, qy * iz * ky - 0.5f);
+        const __amdgpu_buffer_rsrc_t r = make_rsrc(a.feats[j], fbytes);
+        uint4 rv[4 * NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            rv[q * 4 + k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, t.off[k], sb + q * qstep, 0));
+        reduce(rv, t.wt, acc, sq);
+      }
+      finish(d, acc, sq);
+    }
   }
 }
 
 template <typename T, int C, int MODE, bool BLK>
 void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, int ndc) {
-  if (a.N == 5 && C <= 16)  // C = 32: the unrolled views cost more registers than they hide
+  static const bool no_pipe = [] {
+    const char* v = getenv("DAMVS_WARP_NO_PIPE");
+    return v && v[0] == '1';
+  }();
+  if (a.N == 5 && C <= 16 && !no_pipe)
     hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 4>), grid, dim3(256), 0, s, a, npb, dchunk, ndc);
   else
     hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 0>), grid, dim3(256), 0, s, a, npb, dchunk, ndc);
@@ -173,6 +284,8 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
 
 template <typename T, int MODE, bool BLK>
 hipError_t launch_c(hipStream_t s, const WarpArgs& a) {
+  // 32-bit buffer offsets: each view's feature tensor must stay below 2 GiB
+  if ((long long)a.B * a.h * a.w * a.C * (long long)sizeof(T) >= (1LL << 31)) return hipErrorInvalidValue;
   const int npb = (a.rows * a.w + 255) / 256;
   // depth chunk: as long as possible (locality) while keeping >= ~4 blocks per CU in flight
   int dchunk = a.D;
