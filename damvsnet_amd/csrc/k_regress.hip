@@ -488,12 +488,12 @@ hipError_t launch_prob_mfma(hipStream_t s, int B, int D, int h, int w, const voi
   return hipGetLastError();
 }
 
+// The banded-MFMA prob conv runs only with DAMVS_PROB_MFMA=1 (read per call: tests flip it): since the
+// VALU prob_regress widens its tiles once per voxel and runs packed FMAs it is as fast at D = 32-48
+// (stage-1/2 forwards 2.93 / 4.92 ms against 2.99 / 5.01 at B=4) and keeps the exact fp32 weights.
 bool prob_mfma_disabled() {
-  static const bool off = [] {
-    const char* v = getenv("DAMVS_PROB_MFMA");
-    return v && v[0] == '0';
-  }();
-  return off;
+  const char* v = getenv("DAMVS_PROB_MFMA");
+  return !(v && v[0] == '1');
 }
 
 }  // namespace damvs

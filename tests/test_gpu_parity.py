@@ -140,10 +140,12 @@ def test_warp_aggregate_channel_blocked_layout(C, dtype):
 
 
 @pytest.mark.parametrize("s,D", [(0, 48), (1, 32), (0, 64)])
-def test_prob_mfma_vs_split_path(s, D):
-    """bf16 stage forward (banded-MFMA prob conv + regression, k_regress.hip) against the split path on
-    the same U-Net output (damvs_costreg_logits: fp32-weight VALU prob conv, then damvs_regress):
-    they differ only in the prob conv's weight split (bf16 hi + lo) and summation order."""
+def test_prob_mfma_vs_split_path(s, D, monkeypatch):
+    """bf16 stage forward (banded-MFMA prob conv + regression, k_regress.hip; opt-in DAMVS_PROB_MFMA=1)
+    against the split path on the same U-Net output (damvs_costreg_logits: fp32-weight VALU prob conv,
+    then damvs_regress): they differ only in the prob conv's weight split (bf16 hi + lo) and summation
+    order."""
+    monkeypatch.setenv("DAMVS_PROB_MFMA", "1")
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import StageEngine, regress
     C = (32, 16, 8)[s]
