@@ -731,18 +731,23 @@ hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a) {
 //  * B: the slice's input halo ((2 + span - 1) x (64 + span - 1) pixels x 64 B), staged once per slice and
 //    read at every tap's offset; a pixel's 16-byte chunk sits at position chunk ^ ((pixel >> 2) & 3) so the
 //    16 lanes of a quarter-wave (16 consecutive pixels, one chunk) hit distinct banks.
-// One barrier per K chunk. (An LDS-DMA variant measured slower: hipcc drains every outstanding DMA before
-// each LDS read it cannot prove disjoint.)
-constexpr int WC = 64;   // q-tile columns; rows WR = 2 * RW (RW q-rows per wave)
-constexpr int WPER = 7;  // halo pieces per thread: up to 448 pixels
+// One barrier per K chunk. The depth plane's halo is staged once per block; the plane chunk's weights and
+// the epilogue's residuals are requested together after the K loop. (Reading chunk k + 1's fragments
+// during chunk k's MFMAs measured no faster: 271 against 268 us on case N. An LDS-DMA variant measured slower: hipcc drains every outstanding DMA before each LDS read it cannot
+// prove disjoint. Two q-rows per wave, 32 MFMAs a chunk, needed 182 VGPRs + 128 AGPRs: one wave per SIMD,
+// 318 against 270 us on case N.)
+#ifndef DAMVS_WIDE_DIAG
+#define DAMVS_WIDE_DIAG 0  // diagnostic builds only (tools/build_diag_wide.sh): skip parts of the K loop
+#endif
+constexpr int WC = 64, WR = 2;  // q-tile columns x rows
+constexpr int WPER = 7;         // halo pieces per thread: up to 448 pixels
 
-template <bool TWO, int RW>
+template <bool TWO>
 __global__ __launch_bounds__(256) void conv2d_wide_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int nsl,
                                                           int dmin, int span) {
   typedef uint4 raw;
   typedef BufIO<bf16_t> IO;
   constexpr uint32_t ES = 2;
-  constexpr int WR = 2 * RW, NG = 4 * RW;  // q-tile rows; N-groups (16 pixels) per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   raw* abuf = reinterpret_cast<raw*>(smem);  // 2 x 512 raws (8 KB per chunk)
   const int HC = WC + span - 1, HP = (WR + span - 1) * HC;
@@ -806,11 +811,24 @@ __global__ __launch_bounds__(256) void conv2d_wide_kernel(const Conv2dArgs a, in
     }
   };
 
-  f32x4_t acc[4][NG];  // [cout tile][N-group: q-row j / 4 of the wave, 16 columns j % 4]
+  f32x4_t acc[4][4];  // [cout tile][N-group: 16 columns of the wave's q-row]
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int j = 0; j < NG; ++j) acc[m][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) acc[m][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  // the fp32 depth plane's halo (zero outside the image) for the trailing plane chunk, staged once
+  float* gbuf = reinterpret_cast<float*>(hbuf + 2 * HP * 4);  // HP floats
+  if (ph.gchunks > 0) {
+    const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.geo[0], ((long long)(a.B - 1) * a.geo_bstride[0] + a.Hi * a.Wi) * 4);
+    const int pg0 = b * (int)a.geo_bstride[0];
+    for (int p = tid; p < HP; p += 256) {
+      const int row = p / HC, col = p - row * HC;
+      const int iy = iy0 + row, ix = ix0 + col;
+      const bool ok = (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+      gbuf[p] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, ok ? (uint32_t)(pg0 + iy * a.Wi + ix) * 4u : kOOB, 0, 0));
+    }
+  }
 
   // One K chunk per barrier, slices outer and taps inner. A: chunk k + 2 is loaded (scalar offset: no
   // per-chunk VGPR address math) into one register pair while the other pair (chunk k + 1) goes to LDS
@@ -839,32 +857,35 @@ __global__ __launch_bounds__(256) void conv2d_wide_kernel(const Conv2dArgs a, in
   abuf[tid + 256] = p1;
   hstore(0);
   __syncthreads();
-  const int lanepix = wn * RW * HC + n;
+  const int lanepix = wn * HC + n;
   int k = 0;
   auto step = [&](int c, int t, raw& ld0, raw& ld1, const raw& st0, const raw& st1) {
-    wld(ld0, ld1);
+    if (!(DAMVS_WIDE_DIAG & 8)) wld(ld0, ld1);
     const raw* ab = abuf + (k & 1) * 512 + wm * 256 + lane;
     raw af[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) af[m] = ab[m * 64];
     // 16 pixels apart keeps (p >> 2) & 3: one swizzled address, the 4 N-groups at immediate offsets
-    raw bf[NG];
+    const int p0x = s_toff[t] + lanepix;
+    const raw* hb = hbuf + (c & 1) * HP * 4 + p0x * 4 + (g ^ ((p0x >> 2) & 3));
+    raw bf[4];
 #pragma unroll
-    for (int r = 0; r < RW; ++r) {  // one swizzled address per q-row (HC is not a multiple of 16)
-      const int px = s_toff[t] + lanepix + r * HC;
-      const raw* hb = hbuf + (c & 1) * HP * 4 + px * 4 + (g ^ ((px >> 2) & 3));
+    for (int j = 0; j < 4; ++j) bf[j] = hb[j * 64];
+    if (!(DAMVS_WIDE_DIAG & 1)) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bf[r * 4 + j] = hb[j * 64];
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Frag2<bf16_t>::mma(af[m], bf[j], acc[m][j]);
+    } else {
+      acc[0][0][0] += __uint_as_float(af[0].x ^ bf[0].y);
     }
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int j = 0; j < NG; ++j) Frag2<bf16_t>::mma(af[m], bf[j], acc[m][j]);
     abuf[((k + 1) & 1) * 512 + tid] = st0;  // past the last chunk: a harmless copy
     abuf[((k + 1) & 1) * 512 + tid + 256] = st1;
-    if (t == 0 && c + 1 < nsl) hload(c + 1);
-    if (t == nt - 1 && c + 1 < nsl) hstore((c + 1) & 1);
-    __syncthreads();
+    if (!(DAMVS_WIDE_DIAG & 4)) {
+      if (t == 0 && c + 1 < nsl) hload(c + 1);
+      if (t == nt - 1 && c + 1 < nsl) hstore((c + 1) & 1);
+    }
+    if (!(DAMVS_WIDE_DIAG & 2)) __syncthreads();
     ++k;
   };
   int c = 0, t = 0;
@@ -878,81 +899,97 @@ __global__ __launch_bounds__(256) void conv2d_wide_kernel(const Conv2dArgs a, in
     }
   }
 
-  const int qyw = qy0 + wn * RW;  // the wave's first q-row
-  // the fp32 plane as trailing K chunks (tap x plane), as in conv2d_mfma_kernel
+  // tail: the plane chunk's A fragments and the epilogue's residual records are requested together, so
+  // their latencies overlap the plane chunk's LDS reads and MFMAs instead of following one another
+  typedef typename IO::quad quad;
+  const int qyw = qy0 + wn;  // the wave's q-row
+  raw ag[4];
   if (ph.gchunks > 0) {
     const raw* __restrict__ wg = wsrc + (size_t)ph.kchunks * cstride + wm * 256 + lane;
-    const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.geo[0], ((long long)(a.B - 1) * a.geo_bstride[0] + a.Hi * a.Wi) * 4);
-    const int pg0 = b * (int)a.geo_bstride[0];
-    for (int s = 0; s < ph.gchunks; ++s) {
-      raw af[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) af[m] = wg[(size_t)s * cstride + m * 64];
-      float v[NG][8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int tt = s * 32 + g * 8 + e;
-        const bool tv = tt < nt;
-        const int dy = tv ? ph.tap[tt][0] : 0, dx = tv ? ph.tap[tt][1] : 0;
-#pragma unroll
-        for (int j = 0; j < NG; ++j) {
-          const int iy = qyw + (j >> 2) + dy, ix = qx0 + (j & 3) * 16 + n + dx;
-          const bool ok = tv && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
-          v[j][e] = __uint_as_float(
-              __builtin_amdgcn_raw_buffer_load_b32(rg, ok ? (uint32_t)(pg0 + iy * a.Wi + ix) * 4u : kOOB, 0, 0));
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < NG; ++j) {
-        const raw xf = pack_vals<bf16_t>(v[j]);
-#pragma unroll
-        for (int m = 0; m < 4; ++m) Frag2<bf16_t>::mma(af[m], xf, acc[m][j]);
-      }
-    }
+    for (int m = 0; m < 4; ++m) ag[m] = wg[m * 64];
   }
-
-  // epilogue (as conv2d_mfma_kernel): residual before ReLU, ReLU, (upsampled) residual after, store
-  typedef typename IO::quad quad;
   const int up = a.post_up, us = a.post_up >> 1;
   const long long nout = (long long)a.B * a.Ho * a.Wo * a.cout;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout * ES);
   const __amdgpu_buffer_rsrc_t rpre = make_rsrc(a.res_pre ? a.res_pre : a.out, a.res_pre ? nout * ES : 0);
   const __amdgpu_buffer_rsrc_t rpost = make_rsrc(a.res_post ? a.res_post : a.out, a.res_post ? nout / (up * up) * ES : 0);
-  float bias[4][4];
   bool cok[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) cok[m] = (mt0 + wm * 4 + m) * 16 + g * 4 < a.cout;
+  auto out_px = [&](int j, int& pout, int& ppost) {
+    const int qx = qx0 + j * 16 + n;
+    const int oy = qyw * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
+    pout = (b * a.Ho + oy) * a.Wo + ox;
+    ppost = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
+    return qyw < a.Hq && qx < a.Wq;
+  };
+  quad qres[4][4];  // res_pre, else res_post (a layer with both reads res_post in the epilogue)
+  const bool pre_first = a.res_pre != nullptr, any_res = a.res_pre || a.res_post;
+  if (any_res) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int pout, ppost;
+      const bool vok = out_px(j, pout, ppost);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int co = (mt0 + wm * 4 + m) * 16 + g * 4;
+        const bool ok = vok && cok[m];
+        qres[j][m] = pre_first ? IO::ldq(rpre, ok ? (uint32_t)(pout * a.cout + co) * ES : kOOB)
+                               : IO::ldq(rpost, ok ? (uint32_t)(ppost * a.cout + co) * ES : kOOB);
+      }
+    }
+  }
+  // the fp32 plane as a trailing K chunk (tap x plane), B from the staged plane halo
+  if (ph.gchunks > 0) {
+    float v[4][8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int tt = g * 8 + e;
+      const bool tv = tt < nt;
+      const int po = s_toff[tv ? tt : 0] + lanepix;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j][e] = tv ? gbuf[po + j * 16] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const raw xf = pack_vals<bf16_t>(v[j]);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) Frag2<bf16_t>::mma(ag[m], xf, acc[m][j]);
+    }
+  }
+
+  // epilogue (as conv2d_mfma_kernel): residual before ReLU, ReLU, (upsampled) residual after, store
+  float bias[4][4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const int co = (mt0 + wm * 4 + m) * 16 + g * 4;
-    cok[m] = co < a.cout;
 #pragma unroll
     for (int i = 0; i < 4; ++i) bias[m][i] = a.bias[co + i];  // padded to cout_pad
   }
 #pragma unroll
-  for (int j = 0; j < NG; ++j) {
-    const int qy = qyw + (j >> 2), qx = qx0 + (j & 3) * 16 + n;
-    const int oy = qy * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
-    const bool vok = qy < a.Hq && qx < a.Wq;
-    const int pout = (b * a.Ho + oy) * a.Wo + ox;
-    const int ppost = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
-    quad qpre[4], qpost[4];
+  for (int j = 0; j < 4; ++j) {
+    int pout, ppost;
+    const bool vok = out_px(j, pout, ppost);
+    quad qpost[4];
+    if (a.res_pre && a.res_post) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const bool ok = vok && cok[m];
-      const int co = (mt0 + wm * 4 + m) * 16 + g * 4;
-      if (a.res_pre) qpre[m] = IO::ldq(rpre, ok ? (uint32_t)(pout * a.cout + co) * ES : kOOB);
-      if (a.res_post) qpost[m] = IO::ldq(rpost, ok ? (uint32_t)(ppost * a.cout + co) * ES : kOOB);
+      for (int m = 0; m < 4; ++m) {
+        const int co = (mt0 + wm * 4 + m) * 16 + g * 4;
+        qpost[m] = IO::ldq(rpost, vok && cok[m] ? (uint32_t)(ppost * a.cout + co) * ES : kOOB);
+      }
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       float r[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) r[i] = acc[m][j][i] + bias[m][i];
-      if (a.res_pre) IO::addq(qpre[m], r);
+      if (a.res_pre) IO::addq(qres[j][m], r);
       if (a.relu) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) r[i] = fmaxf(r[i], 0.f);
       }
-      if (a.res_post) IO::addq(qpost[m], r);
+      if (a.res_post) IO::addq(a.res_pre ? qpost[m] : qres[j][m], r);
       const int co = (mt0 + wm * 4 + m) * 16 + g * 4;
       IO::stq(ro, vok && cok[m] ? (uint32_t)(pout * a.cout + co) * ES : kOOB, r);
     }
@@ -975,25 +1012,16 @@ hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
         dmax = a.ph[p].tap[t][d] > dmax ? a.ph[p].tap[t][d] : dmax;
       }
   const int span = dmax - dmin + 1;
-  static const int rw_env = [] {
-    const char* v = getenv("DAMVS_CONV2D_WIDE_RW");
-    return v ? atoi(v) : 1;
-  }();
-  // DAMVS_CONV2D_WIDE_RW=2: two q-rows per wave (32 MFMAs a chunk) when the taller halo fits the pieces.
-  // Off by default: 182 VGPRs + 128 AGPRs leave one wave per SIMD (case N 318 us vs 270-278 us at RW=1).
-  const int RW = rw_env == 2 && (4 + span - 1) * (WC + span - 1) * 4 <= WPER * 256 ? 2 : 1;
-  const int WR = 2 * RW;
   const int HP = (WR + span - 1) * (WC + span - 1);
   if (HP * 4 > WPER * 256) return hipErrorNotSupported;
   for (int p = 0; p < a.nphase; ++p)  // geo taps beyond one K chunk; fewer than 4 taps (halo schedule)
     if (a.ph[p].gchunks > 1 || a.ph[p].ntaps < 4) return hipErrorNotSupported;
   const int tx = (a.Wq + WC - 1) / WC, ty = (a.Hq + WR - 1) / WR;
   const int nsl = (a.c0 + a.c1) / 32;
-  const size_t smem = 2 * 512 * 16 + 2 * (size_t)HP * 64;
+  const size_t smem = 2 * 512 * 16 + 2 * (size_t)HP * 64 + (size_t)HP * 4;  // A chunks, halo slices, plane halo
   const long long nblk = (long long)tx * ty * a.B * a.nphase;
   const dim3 grid((unsigned)nblk, (unsigned)(a.MTtot / 8));
-  auto k = RW == 2 ? (a.c1 > 0 ? conv2d_wide_kernel<true, 2> : conv2d_wide_kernel<false, 2>)
-                   : (a.c1 > 0 ? conv2d_wide_kernel<true, 1> : conv2d_wide_kernel<false, 1>);
+  auto k = a.c1 > 0 ? conv2d_wide_kernel<true> : conv2d_wide_kernel<false>;
   if (smem > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)smem);
