@@ -300,6 +300,9 @@ def main():
     ap.add_argument("--batch", type=int, default=4,
                     help="depth maps (reference views) per GPU per step; default 4 = the reference's own "
                          "test batch (scripts/test.sh:25 --batch_size=4), SURVEY.md 8(d) 'B=4 for throughput'")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="sub-batches of the per-GPU batch on concurrent HIP streams in the timed steps "
+                         "(bitwise the one-stream result; ms_per_stage / rooflines come from a one-stream pass)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--frontend", default="hip", choices=["hip", "torch"], help="2D front-end implementation")
     ap.add_argument("--cpu-budget", type=float, default=60.0)
@@ -348,20 +351,25 @@ def main():
 
     with torch.no_grad():
         for _ in range(args.warmup):
-            net(imgs, proj, dv, ins)
+            net(imgs, proj, dv, ins, streams=args.streams)
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
-        timer = StageTimer()
-        probes = ProbeRecorder()
-        net.DepthNet.probe = probes
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            net(imgs, proj, dv, ins, stage_hook=timer)
+            net(imgs, proj, dv, ins, streams=args.streams)
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        # attribution pass, one stream (per-phase and per-kernel-group times are not separable when sub-batches
+        # overlap): HIP events at the phase boundaries and inside damvs_stage_forward_probed
+        timer = StageTimer()
+        probes = ProbeRecorder()
+        net.DepthNet.probe = probes
+        for _ in range(min(args.steps, 5)):
+            net(imgs, proj, dv, ins, stage_hook=timer)
+        torch.cuda.synchronize()
         net.DepthNet.probe = None
     from damvsnet_amd.dist import max_over_ranks
     elapsed = max_over_ranks(elapsed, device=device)
@@ -401,7 +409,8 @@ def main():
             "config": {"workload": "%s: %s" % (args.config, desc), "batch_per_gpu": args.batch,
                        "frontend": args.frontend,
                        "global_batch": args.batch * world, "height": H, "width": W, "views": N,
-                       "ndepths": list(nd), "parallelism": "replicas x%d (reference views sharded over ranks)" % world},
+                       "ndepths": list(nd), "streams": args.streams,
+                       "parallelism": "replicas x%d (reference views sharded over ranks)" % world},
             "ms_per_stage": phases,
             "latency_b1": lat,
             "roofline": {"kernel": "warp_aggregate stage2 (fused homography warp + adaptive aggregation), "

@@ -110,9 +110,76 @@ class CascadeMVSNet(nn.Module):
         f = feat(x)
         return [{k: v.reshape(B, N, *v.shape[1:])[:, i] for k, v in f.items()} for i in range(N)]
 
-    def forward(self, imgs, proj_matrices, depth_values, intrinsics_matrices=None, stage_hook=None, depthnet=None):
+    def _side_streams(self, n, device):
+        pool = getattr(self, "_streams", None)
+        if pool is None or len(pool) < n or pool[0].device != device:
+            pool = self._streams = [torch.cuda.Stream(device) for _ in range(n)]
+        return pool[:n]
+
+    def _forward_streams(self, imgs, proj_matrices, depth_values, intrinsics_matrices, nstreams):
+        """The batch as ``nstreams`` sub-batches of reference views on concurrent HIP streams, merged along the
+        batch. Per sample every kernel sees the same inputs as in one batch, so the outputs are bitwise those of
+        the single-stream forward (tests/test_gpu_streams.py); the gain is overlap between kernels with different
+        bounds (one sub-batch's TA-bound warp beside another's HBM / MFMA-bound U-Net or front-end)."""
+        B = imgs.shape[0]
+        cut = [B * i // nstreams for i in range(nstreams + 1)]
+        main = torch.cuda.current_stream(imgs.device)
+
+        def part(x, a, b):
+            if isinstance(x, dict):
+                return {k: part(v, a, b) for k, v in x.items()}
+            return x[a:b] if isinstance(x, torch.Tensor) else x
+
+        pool = self._side_streams(nstreams, imgs.device)
+        outs = []
+        for st, a, b in zip(pool, cut[:-1], cut[1:]):
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                outs.append(self.forward(part(imgs, a, b), part(proj_matrices, a, b), part(depth_values, a, b),
+                                         part(intrinsics_matrices, a, b)))
+
+        # batch-sized outputs allocated on the main stream, each stream copying its rows right after its own
+        # forward (the copies overlap the other sub-batches' kernels instead of following all of them)
+        memo = {}  # the top-level keys alias the last stage's tensors: one batch tensor (and copy) each
+
+        def alloc(v):
+            if isinstance(v, dict):
+                return {k: alloc(x) for k, x in v.items()}
+            if isinstance(v, torch.Tensor):
+                if id(v) not in memo:
+                    memo[id(v)] = torch.empty((B,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
+                return memo[id(v)]
+            return v
+
+        full = alloc(outs[0])
+
+        def fill(dst, src, a, b, st, done):
+            if isinstance(dst, dict):
+                for k in dst:
+                    fill(dst[k], src[k], a, b, st, done)
+            elif isinstance(dst, torch.Tensor) and id(dst) not in done:
+                done.add(id(dst))
+                dst[a:b].copy_(src)
+                dst.record_stream(st)
+
+        for i, (st, a, b) in enumerate(zip(pool, cut[:-1], cut[1:])):
+            st.wait_stream(main)  # after the allocations (their blocks may come from pending main-stream work)
+            with torch.cuda.stream(st):
+                fill(full, outs[i], a, b, st, set())
+        for st in pool:
+            main.wait_stream(st)
+        return full
+
+    def forward(self, imgs, proj_matrices, depth_values, intrinsics_matrices=None, stage_hook=None, depthnet=None,
+                streams=1):
         """``depthnet``: optional stage runner (stage_idx, NHWC features, proj, hyps, cost_regularization) -> dict,
-        e.g. sharded.DepthShardedDepthNet (one depth map over several GPUs); default: this model's DepthNet."""
+        e.g. sharded.DepthShardedDepthNet (one depth map over several GPUs); default: this model's DepthNet.
+        ``streams`` > 1 runs the batch as that many sub-batches on concurrent streams (_forward_streams; not with
+        a stage hook or a custom stage runner)."""
+        if streams > 1 and imgs.shape[0] > 1 and stage_hook is None and depthnet is None and imgs.is_cuda \
+                and not self.refine:
+            return self._forward_streams(imgs, proj_matrices, depth_values, intrinsics_matrices,
+                                         min(int(streams), imgs.shape[0]))
         if self.refine:
             raise NotImplementedError("refine=True: the reference RefineNet forward is not runnable "
                                       "(models/module.py:602 calls F.cat)")

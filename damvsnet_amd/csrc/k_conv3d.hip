@@ -902,11 +902,15 @@ hipError_t launch_lds(hipStream_t s, const ConvArgs& a) {
     hipLaunchKernelGGL(conv_s1_c16_zslide_kernel, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
     return hipGetLastError();
   }
+  // The 4 x 8 x 16 tile stages a 6-plane halo: with fewer than 4 output planes (the deep levels at D = 8) most of
+  // it is padding, and at 64 channels (conv6) it takes 138 KB of LDS (one block per CU). Measured (B=4, bf16)
+  // the gather kernel wins both: conv6 98 -> 64 us (stage 2), 165 -> 53 us (stage 3); conv4 at stage 3 (2
+  // planes) 137 -> 117 us, while conv4 at stage 2 (8 planes) keeps the tile (93 against 137 us).
+  if (a.Do < LTD || a.Cin >= 64) return hipErrorNotSupported;
   if (a.Cin == 8 && MT == 1) return launch_lds_t<T, 8, 1>(s, a);
   if (a.Cin == 16 && MT == 1) return launch_lds_t<T, 16, 1>(s, a);
   if (a.Cin == 32 && MT == 1) return launch_lds_t<T, 32, 1>(s, a);
   if (a.Cin == 32 && MT == 2) return launch_lds_t<T, 32, 2>(s, a);
-  if (a.Cin == 64 && MT == 4 && lds_tile_bytes<T, 64>() <= 160 * 1024) return launch_lds_t<T, 64, 4>(s, a);
   return hipErrorNotSupported;
 }
 

@@ -18,6 +18,7 @@
 
 #include "damvs_device.h"
 
+
 namespace damvs {
 
 namespace {
@@ -78,7 +79,7 @@ __device__ __forceinline__ Taps bilinear_taps(int h, int w, uint32_t rec, float 
 // spreads every depth slice over all 8 XCDs and serves the gathers from the Infinity Cache).
 //
 // Per thread the depth-independent part of each view's homography (the ray R [x y 1]^T) is computed
-// once; the cameras' translations are block-uniform. Gathers are buffer loads with 32-bit offsets (the
+// once; the cameras' translations are block-uniform (SGPRs). Gathers are buffer loads with 32-bit offsets (the
 // batch element and channel chunk in the scalar offset), so a tap costs one select instead of 64-bit
 // address arithmetic and a weight select. With NVC > 0 (the source-view count a compile-time constant)
 // the (depth, view) sequence is software-pipelined one view deep: the 4 x C/E records of the next view
@@ -86,8 +87,8 @@ __device__ __forceinline__ Taps bilinear_taps(int h, int w, uint32_t rec, float 
 // current view is reduced, and the loads are unconditional (the last plane re-reads its own last
 // view) so the vmcnt waits count exactly.
 template <typename T, int C, int MODE, bool BLK, int NVC>
-__global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, int npix_blocks, int dchunk,
-                                                             int ndchunks) {
+__global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, const float* __restrict__ cams,
+                                                             int npix_blocks, int dchunk, int ndchunks) {
   constexpr int E = Stor<T>::E, NQ = C / E;
   static_assert(NVC % 2 == 0, "the view pipeline alternates two register sets");
   const int hw = a.h * a.w, ohw = a.rows * a.w;  // feature-map plane, computed rows (y0 .. y0 + rows - 1)
@@ -97,10 +98,11 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
   const int dc = L % ndchunks; L /= ndchunks;
   const int pb = L % npix_blocks;
   const int b = L / npix_blocks;
-  // this batch element's [N-1][12] source cameras in LDS (broadcast reads)
-  __shared__ __attribute__((aligned(16))) float s_rtf[(kMaxViews - 1) * 12];
-  if (threadIdx.x < (a.N - 1) * 12) s_rtf[threadIdx.x] = a.rt[(size_t)b * (a.N - 1) * 12 + threadIdx.x];
-  __syncthreads();
+  // this batch element's [N-1][12] source cameras: block-uniform reads through a read-only, non-aliased
+  // kernel argument, i.e. scalar loads into SGPRs. (They were staged in LDS; with another kernel running
+  // on a concurrent stream that copy came back altered in up to 76 of 80 launches — tools/streams_race_kernel.py
+  // — and the scalar path needs neither LDS nor a barrier.)
+  const float* __restrict__ cam = cams + (size_t)b * (a.N - 1) * 12;
   const int p = pb * 256 + threadIdx.x;
   if (p >= ohw) return;
   const int yl = p / a.w, x = p - yl * a.w;
@@ -190,16 +192,15 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
     // source view j = 1 + v: ray (per lane), translation (block-uniform) and descriptor
     float rx[NVC], ry[NVC], rz[NVC], tx[NVC], ty[NVC], tz[NVC];
     __amdgpu_buffer_rsrc_t rs[NVC];
-    auto uniform = [](float f) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(f))); };
 #pragma unroll
     for (int v = 0; v < NVC; ++v) {
-      const float* m = s_rtf + v * 12;
+      const float* m = cam + v * 12;
       rx[v] = m[0] * fx + m[1] * fy + m[2];
       ry[v] = m[3] * fx + m[4] * fy + m[5];
       rz[v] = m[6] * fx + m[7] * fy + m[8];
-      tx[v] = uniform(m[9]);
-      ty[v] = uniform(m[10]);
-      tz[v] = uniform(m[11]);
+      tx[v] = m[9];
+      ty[v] = m[10];
+      tz[v] = m[11];
       rs[v] = make_rsrc(a.feats[v + 1], fbytes);
     }
     auto taps = [&](int v, float hyp) {
@@ -249,7 +250,7 @@ __global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, i
       float acc[C], sq[C];
       init(acc, sq);
       for (int j = 1; j < nviews; ++j) {
-        const float* m = s_rtf + (j - 1) * 12;
+        const float* m = cam + (j - 1) * 12;
         const float rx = m[0] * fx + m[1] * fy + m[2];
         const float ry = m[3] * fx + m[4] * fy + m[5];
         const float rz = m[6] * fx + m[7] * fy + m[8];
@@ -277,9 +278,9 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
     return v && v[0] == '1';
   }();
   if (a.N == 5 && C <= 16 && !no_pipe)
-    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 4>), grid, dim3(256), 0, s, a, npb, dchunk, ndc);
+    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 4>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
   else
-    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 0>), grid, dim3(256), 0, s, a, npb, dchunk, ndc);
+    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 0>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
 }
 
 template <typename T, int MODE, bool BLK>

@@ -72,11 +72,17 @@ class StageEngine:
                 pass
 
     def workspace(self, B, N, D, h, w):
+        """The stage's scratch, one buffer per stream (sub-batches running on concurrent streams each
+        get their own; a buffer is reused by later calls on its stream, which are ordered after it)."""
         n = ctypes.c_size_t()
         check(self._lib.damvs_stage_workspace_size(self.handle, B, N, D, h, w, ctypes.byref(n)))
-        if self._ws is None or self._ws.numel() < n.value:
-            self._ws = torch.empty(n.value, dtype=torch.uint8, device=self.device)
-        return self._ws
+        if self._ws is None:
+            self._ws = {}
+        key = _capi.stream_ptr(self.device)
+        ws = self._ws.get(key)
+        if ws is None or ws.numel() < n.value:
+            ws = self._ws[key] = torch.empty(n.value, dtype=torch.uint8, device=self.device)
+        return ws
 
     def forward(self, feats_nhwc, proj, hyps, prob_init=None, want_prob=True, probe=None):
         """feats_nhwc: list of N (B,h,w,C) tensors of self.dtype; proj (B,N,2,4,4); hyps (B,D,h,w) float32.

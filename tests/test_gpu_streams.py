@@ -1,0 +1,98 @@
+"""GPU: kernels on concurrent HIP streams.
+
+``CascadeMVSNet.forward(streams=S)`` runs the batch as S sub-batches on concurrent streams (bench.py's timed
+steps). Every kernel sees per sample the inputs it sees in one batch, so all outputs must be bitwise the
+one-stream result. The stage-2 warp launched beside U-Net layers on another stream must also reproduce its
+solo output: until round 2 it staged its cameras in LDS, and beside a U-Net kernel that copy came back altered
+(76 of 80 launches beside conv0, tools/streams_race_kernel.py); the cameras are now scalar loads.
+"""
+import numpy as np
+import pytest
+import torch
+
+from common import model_state, forward_inputs
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from damvsnet_amd import _capi
+    _capi.load_library()
+
+
+def _perturb(P):
+    """Per-sample cameras (synth broadcasts one): source translations x (1 + 0.15 b), a small extra yaw."""
+    P = P.clone()
+    for b in range(P.shape[0]):
+        a = 0.01 * b
+        R = torch.tensor([[np.cos(a), 0.0, np.sin(a)], [0.0, 1.0, 0.0], [-np.sin(a), 0.0, np.cos(a)]],
+                         dtype=P.dtype)
+        P[b, 1:, 0, :3, 3] *= 1.0 + 0.15 * b
+        P[b, 1:, 0, :3, :3] = R @ P[b, 1:, 0, :3, :3]
+    return P
+
+
+@pytest.mark.timeout(240)
+def test_warp_beside_unet_layers_on_another_stream():
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import hypotheses, block_channels, proj_prepare
+    from damvsnet_amd import _capi, synth
+    net = CascadeMVSNet(ndepths=[48, 32, 8], compute_dtype=torch.bfloat16)
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    net = net.to(DEV).eval()
+    B, N, H, W, s, C = 2, 5, 1184, 1600, 1, 16
+    h, w, D = H // 2, W // 2, 32
+    proj, _, dv = synth.cameras(B, N, H, W)
+    P = _perturb(torch.from_numpy(proj["stage2"])).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    pd = 600 + 100 * torch.rand(B, H // 4, W // 4, device=DEV, generator=g)
+    pv = 5 + 20 * torch.rand(B, H // 4, W // 4, device=DEV, generator=g)
+    hyps = hypotheses(torch.from_numpy(dv).to(DEV), D, H, W, 2, pd, pv)
+    feats = [torch.randn(B, h, w, C, generator=g, device=DEV).to(torch.bfloat16) for _ in range(N)]
+    eng = net.DepthNet.engine(s, net.cost_regularization[s], torch.device(DEV))
+    with torch.no_grad():
+        rt, fb = proj_prepare(P), block_channels(feats)
+        warp = lambda: eng.warp_aggregate(fb, None, hyps, rt=rt, layout=_capi.DAMVS_LAYOUT_CBLOCK)
+        vol = warp()
+        bufs = eng.unet_buffers(B, D, h, w)
+        torch.cuda.synchronize()
+        ref = vol.clone()
+        sa, sb, main = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.current_stream()
+        for layer in (0, 1, 7):
+            src = vol if layer == 0 else bufs[(None, 0, 1, 2, 3, 4, 5, 6, 4, 2)[layer]]
+            dst = bufs[(0, 1, 2, 3, 4, 5, 6, 4, 2, 0)[layer]]
+            for _ in range(3):
+                sa.wait_stream(main)
+                sb.wait_stream(main)
+                with torch.cuda.stream(sa):
+                    for _ in range(6):
+                        eng.unet_layer(layer, D, h, w, src, dst)
+                with torch.cuda.stream(sb):
+                    outs = [warp() for _ in range(6)]
+                torch.cuda.synchronize()
+                assert all(torch.equal(o, ref) for o in outs), layer
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("streams", [2, 4])
+def test_forward_sub_batches_on_streams_bitwise(streams):
+    from damvsnet_amd.cascade import CascadeMVSNet
+    net = CascadeMVSNet(ndepths=[48, 32, 8], compute_dtype=torch.bfloat16, frontend_dtype=torch.bfloat16)
+    net.load_state_dict(model_state("forward_cfgB_640x512"), strict=True)
+    net = net.to(DEV).eval()
+    imgs, proj, dv, ins = forward_inputs(4, 5, 512, 640)
+    imgs, dv = imgs.to(DEV), dv.to(DEV)
+    proj = {k: _perturb(v).to(DEV) for k, v in proj.items()}
+    with torch.no_grad():
+        ref = net(imgs, proj, dv)
+        for _ in range(3):
+            got = net(imgs, proj, dv, streams=streams)
+            torch.cuda.synchronize()
+            for st in ("stage1", "stage2", "stage3"):
+                for k in ("depth", "photometric_confidence", "variance", "prob_volume", "depth_values"):
+                    assert torch.equal(got[st][k], ref[st][k]), (st, k)
+            assert torch.equal(got["depth"], ref["depth"])

@@ -1,0 +1,20 @@
+#!/usr/bin/env bash
+# Per-layer U-Net kernel times (kbench --kernel unet, B=4) under rocprofv3 kernel trace, default vs
+# DAMVS_CONV_NO_LDS=1 (every 3D conv on the gather kernel), stages 2 and 3.
+set -u
+R="${GRAFT_REPO_ROOT:-$(pwd)}"
+mkdir -p $R/gpurun_out/unetl
+cd /tmp && export TMPDIR=/tmp
+for s in 2 3; do for v in X=0 DAMVS_CONV_NO_LDS=1; do
+  env $v timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/unetl/s${s}_$v -o run -- python $R/tools/kbench.py --kernel unet --stage $s --batch 4 --iters 3 > $R/gpurun_out/unetl/s${s}_$v.log 2>&1 || { tail -3 $R/gpurun_out/unetl/s${s}_$v.log; exit 1; }
+  echo "== stage $s $v: $(grep 'per call' $R/gpurun_out/unetl/s${s}_$v.log)"
+  python - $R/gpurun_out/unetl/s${s}_$v/run_kernel_trace.csv <<'PY'
+import csv, sys
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+rows = [r for r in rows if "damvs" in r["Kernel_Name"]]
+last = rows[-11:]  # one U-Net: 10 convs + the prob conv
+for r in last:
+    n = r["Kernel_Name"].replace("damvs::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+    print("  %8.1f us  %s" % ((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3, n[:70]))
+PY
+done; done
