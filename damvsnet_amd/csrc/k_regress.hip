@@ -133,7 +133,9 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
   typedef typename std::conditional<sizeof(T) == 4, float4, uint4>::type raw;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float4* tile = reinterpret_cast<float4*>(smem);               // 2 x FQ x NVOX (double buffer)
-  float* lg = reinterpret_cast<float*>(tile + 2 * FQ * NVOX);   // [D][256] logits, column per thread
+  // [D - 1][256] logits, column per thread; the last plane's logit stays in a register: at D = 32 that 1 KB
+  // is what lets a third block onto the CU (2 x 21.3 KB tiles + 31 KB column = 52.3 KB)
+  float* lg = reinterpret_cast<float*>(tile + 2 * FQ * NVOX);
 
   const int tid = threadIdx.x;
   const int ty = tid / kTX, tx = tid % kTX;
@@ -231,7 +233,7 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
     }
     return;
   }
-  lg[(D - 1) * 256 + tid] = am1;
+  float last = am1;  // plane D - 1
 
   const int y = y0 + ty, x = x0 + tx;
   if (y >= h || x >= w) return;
@@ -239,20 +241,21 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
   const float* hy = hyps + (size_t)b * D * hw + pix;
   const float* pin = prob_init ? prob_init + (size_t)b * D * hw + pix : nullptr;
   float* lcol = lg + tid;
+  auto col = [&](int d) -> float& { return d == D - 1 ? last : lcol[d * 256]; };
   if (pin)
-    for (int d = 0; d < D; ++d) lcol[d * 256] += pin[(size_t)d * hw];
+    for (int d = 0; d < D; ++d) col(d) += pin[(size_t)d * hw];
   float mx = -INFINITY;
-  for (int d = 0; d < D; ++d) mx = fmaxf(mx, lcol[d * 256]);
+  for (int d = 0; d < D; ++d) mx = fmaxf(mx, col(d));
   float sum = 0.f;
   for (int d = 0; d < D; ++d) {
-    const float e = expf(lcol[d * 256] - mx);
-    lcol[d * 256] = e;
+    const float e = expf(col(d) - mx);
+    col(d) = e;
     sum += e;
   }
   float dep = 0.f, idx = 0.f;
   for (int d = 0; d < D; ++d) {
-    const float pr = lcol[d * 256] / sum;
-    lcol[d * 256] = pr;
+    const float pr = col(d) / sum;
+    col(d) = pr;
     dep += pr * hy[(size_t)d * hw];
     idx += pr * (float)d;
   }
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
   float c = 0.f, vs = 0.f;
   float* po = prob ? prob + (size_t)b * D * hw + pix : nullptr;
   for (int d = 0; d < D; ++d) {
-    const float pr = lcol[d * 256];
+    const float pr = col(d);
     const float df = hy[(size_t)d * hw] - dep;
     vs += df * df * pr;
     if (d >= ii - 1 && d <= ii + 2) c += pr;
@@ -388,7 +391,7 @@ __global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int
 
 template <typename T, int CB>
 size_t prob_regress_smem(int D) {
-  return 2 * (size_t)kHY * kHX * CB * 4 + (size_t)D * 256 * 4;  // fp32 plane tiles + logit column
+  return 2 * (size_t)kHY * kHX * CB * 4 + (size_t)(D > 0 ? D - 1 : 0) * 256 * 4;  // fp32 plane tiles + logit column
 }
 
 template <typename T, int CB>
