@@ -418,7 +418,9 @@ def main():
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr["bytes"] if tr else None,
                          "traffic_source": ("committed PMC profile " + tr["source"]) if tr else None,
-                         "ms_per_launch": round(pipe_ms, 4), "algorithmic_bytes": int(alg),
+                         "ms_per_launch": round(pipe_ms, 4), "launch": "whole batch (B=%d) on one stream, the "
+                         "attribution pass after the timed steps; rocprof check: tools/prof_roofline_kernel.py" % args.batch,
+                         "algorithmic_bytes": int(alg),
                          "isolated_ms_per_launch": round(iso_ms, 4),
                          "isolated_frac": round(alg / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "hot_path_roofline": hp,
