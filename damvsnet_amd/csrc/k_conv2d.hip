@@ -676,7 +676,7 @@ hipError_t launch_halo_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span)
   constexpr int KC = 4 * Stor<T>::E;
   const int tx = (a.Wq + HGC - 1) / HGC, ty = (a.Hq + HGR - 1) / HGR;
   const int nsl = (a.c0 + a.c1) / KC;
-  const size_t smem = 2 * (size_t)(HGR + span - 1) * (HGC + span - 1) * 4 * 16;
+  const size_t smem = (nsl > 1 ? 2 : 1) * (size_t)(HGR + span - 1) * (HGC + span - 1) * 4 * 16;  // one slice: one buffer
   const long long nblk = (long long)tx * ty * a.B * a.nphase;
   const dim3 grid((unsigned)nblk, (unsigned)(a.MTtot / (MT * WM)));
   if (a.c1 > 0)
@@ -696,7 +696,15 @@ hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a) {
     const char* v = getenv("DAMVS_CONV2D_HALO");
     return v ? atoi(v) : 2;
   }();
-  if (a.MTtot > max_mt || (a.MTtot > 2 && a.MTtot < 8) || a.in_stride != 1 || a.c0 % KC || a.c1 % KC || a.c0 + a.c1 < 2 * KC || a.MTtot < 2 || a.ngeo > 1)
+  // one-slice inputs (Cin = KC) and single cout tiles as well: the half-resolution GeoBlock convs with a depth
+  // plane (32+g -> 32: 173 -> 146 us, 32+g -> 16: 101 -> 79 us at B=4); DAMVS_CONV2D_HALO_THIN=0 restores the
+  // gather kernel for them
+  static const bool thin = [] {
+    const char* v = getenv("DAMVS_CONV2D_HALO_THIN");
+    return !(v && v[0] == '0');
+  }();
+  if (a.MTtot > max_mt || (a.MTtot > 2 && a.MTtot < 8) || a.in_stride != 1 || a.c0 % KC || a.c1 % KC ||
+      a.c0 + a.c1 < (thin ? KC : 2 * KC) || a.MTtot < (thin ? 1 : 2) || a.ngeo > 1)
     return hipErrorNotSupported;
   int dmin = 0, dmax = 0;
   for (int p = 0; p < a.nphase; ++p)
@@ -716,6 +724,7 @@ hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a) {
   if (T_is_bf16<T>::value && a.MTtot % 8 == 0 && tiles * (a.MTtot / 8) >= 240) return launch_halo_t<T, 8, 1>(s, a, dmin, span);
   if (a.MTtot % 4 == 0 && tiles * (a.MTtot / 4) >= 240) return launch_halo_t<T, 4, 1>(s, a, dmin, span);
   if (a.MTtot % 2 == 0) return launch_halo_t<T, 2, 1>(s, a, dmin, span);
+  if (a.MTtot == 1) return launch_halo_t<T, 1, 1>(s, a, dmin, span);
   return hipErrorNotSupported;
 }
 

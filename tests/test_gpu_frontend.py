@@ -57,6 +57,8 @@ CASES = [
     (False, 3, 1, 1, 0, 128, 128, (256,), 256, True, True, 2),      # wide: two inputs + plane, both residuals
     (True, 5, 2, 2, 1, 256, 0, (), 128, True, False, 1),            # wide: k5 s2 transposed decoder + skip
     (False, 1, 1, 0, 0, 64, 0, (64,), 128, False, False, 0),        # wide: 1x1 (GeoBlock downsample)
+    (False, 3, 1, 1, 0, 32, 0, (0,), 32, True, True, 0),            # halo, one slice (bf16): 32+g -> 32
+    (False, 3, 1, 1, 0, 32, 0, (32,), 16, True, False, 0),          # halo, one slice, one cout tile
 ]
 
 

@@ -32,6 +32,10 @@ CASES = {
     "L dec4 128->64 k3 r4": (True, 3, 1, 1, 0, 128, 0, 0, 64, True, 1, 296, 400, False, 0),
     "M dec5 64->32 k5s2 r2": (True, 5, 2, 2, 1, 64, 0, 0, 32, True, 1, 296, 400, False, 1),
     "N geo conv2 128+g->128 r4 B=4": (False, 3, 1, 1, 0, 128, 0, 1, 128, True, 4, 296, 400, True, 0),
+    "O geo conv2 32+g->32 r2 B=4": (False, 3, 1, 1, 0, 32, 0, 1, 32, True, 4, 592, 800, True, 0),
+    "P dec 32->16 k3 r2 B=4": (False, 3, 1, 1, 0, 32, 0, 0, 16, True, 4, 592, 800, False, 0),
+    "Q geo conv2 32+g->16 r2 B=4": (False, 3, 1, 1, 0, 32, 0, 1, 16, True, 4, 592, 800, True, 0),
+    "R dec 64->32 k3 r4 B=4": (False, 3, 1, 1, 0, 64, 0, 0, 32, True, 4, 296, 400, False, 0),
 }
 
 
