@@ -36,6 +36,8 @@ CASES = {
     "P dec 32->16 k3 r2 B=4": (False, 3, 1, 1, 0, 32, 0, 0, 16, True, 4, 592, 800, False, 0),
     "Q geo conv2 32+g->16 r2 B=4": (False, 3, 1, 1, 0, 32, 0, 1, 16, True, 4, 592, 800, True, 0),
     "R dec 64->32 k3 r4 B=4": (False, 3, 1, 1, 0, 64, 0, 0, 32, True, 4, 296, 400, False, 0),
+    "S fpn top k4s2 32->8 x20": (True, 4, 2, 1, 0, 32, 0, 0, 8, False, 20, 592, 800, False, 0),
+    "T geo dec k3s2 16->8 B=4": (True, 3, 2, 1, 1, 16, 0, 0, 8, True, 4, 592, 800, False, 0),
 }
 
 
