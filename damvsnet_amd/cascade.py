@@ -103,8 +103,7 @@ class CascadeMVSNet(nn.Module):
         feat, _ = self._frontend()
         B, N = imgs.shape[:2]
         if self.frontend_impl == "hip":
-            x = imgs.transpose(0, 1).reshape(N * B, *imgs.shape[2:])  # view-major: view v = rows v*B..
-            f = feat(x)
+            f = feat(imgs)  # view-major rows: view v = rows v*B.. (the images are read in place)
             return [{k: v[i * B:(i + 1) * B] for k, v in f.items()} for i in range(N)]
         x = imgs.reshape(B * N, *imgs.shape[2:]).contiguous(memory_format=torch.channels_last)
         f = feat(x)
@@ -198,8 +197,9 @@ class CascadeMVSNet(nn.Module):
             if s >= 1:
                 hook(name + ".geofusion")
                 _, geo = self._frontend()
-                ref_img = F.interpolate(imgs[:, 0], scale_factor=1.0 / 2 ** (2 - s), mode="bilinear",
-                                        align_corners=False)
+                # scale 1 (stage 3) is the identity (source index (x + 0.5) - 0.5 = x): read imgs[:, 0] in place
+                ref_img = imgs[:, 0] if s == 2 and self.frontend_impl == "hip" else \
+                    F.interpolate(imgs[:, 0], scale_factor=1.0 / 2 ** (2 - s), mode="bilinear", align_corners=False)
                 dl = F.interpolate(depth.unsqueeze(1), scale_factor=2, mode="bilinear", align_corners=False)
                 cl = F.interpolate(conf.unsqueeze(1), scale_factor=2, mode="bilinear", align_corners=False)
                 if self.frontend_impl == "hip":

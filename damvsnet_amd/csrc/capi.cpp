@@ -732,6 +732,18 @@ int damvs_hypotheses(void* stream, int B, int D, int H, int W, int scale, const 
   return hip_check(launch_hyp_refine(s, B, D, H, W, scale, prev_depth, prev_var, hp, wp, hyps), "hyp_refine launch");
 }
 
+int damvs_sparse_depth_pyramid(void* stream, int B, int h, int w, const float* depth, const float* depth_values, int Dv,
+                               const float* mask, float* d0, float* d1, float* d2, float* d3, float* scratch) {
+  if (!depth || !depth_values || !d0 || !d1 || !d2 || !d3 || !scratch) return fail(DAMVS_E_ARG, "null argument");
+  if (B < 1 || h < 8 || w < 8 || Dv < 1) return fail(DAMVS_E_SHAPE, "bad shape (h, w >= 8)");
+  if ((long long)B * h * w >= (1ll << 31)) return fail(DAMVS_E_SHAPE, "depth map too large");
+  float* m1 = scratch;
+  float* m2 = scratch + (size_t)B * (h / 2) * (w / 2);
+  return hip_check(launch_sparse_pyramid(reinterpret_cast<hipStream_t>(stream), B, h, w, depth, depth_values, Dv, mask,
+                                         d0, d1, d2, d3, m1, m2),
+                   "sparse_pool launch");
+}
+
 }  // extern "C"
 
 // ============================================================================ 2D convolutions

@@ -122,6 +122,8 @@ hipError_t launch_proj_prepare(hipStream_t s, int B, int N, const float* proj, f
 hipError_t launch_hyp_linear(hipStream_t s, int B, int D, int h, int w, const float* dv, int Dv, float* out);
 hipError_t launch_hyp_refine(hipStream_t s, int B, int D, int H, int W, int scale, const float* pd,
                              const float* pv, int hp, int wp, float* out);
+hipError_t launch_sparse_pyramid(hipStream_t s, int B, int h, int w, const float* depth, const float* dv, int Dv,
+                                 const float* mask, float* d0, float* d1, float* d2, float* d3, float* m1, float* m2);
 struct FeatPtrs {
   const void* p[kMaxViews];
 };

@@ -8,6 +8,9 @@
 //                 upsample of the previous depth / exp-variance (models/cas_mvsnet.py:250-253) and the
 //                 trilinear downsample to stage resolution (:293-296), never materialising the
 //                 full-resolution (B,D,H,W) tensor the reference builds.
+//  sparse_pool  : GeoFeatureFusion's depth pyramid, models/geometry.py:90-96 (normalised depth and
+//                 valid mask) and SparseDownSampleClose(stride 2), models/geometry.py:443-455, one
+//                 launch per level instead of ~10 elementwise/max-pool launches.
 #include "damvs_device.h"
 
 namespace damvs {
@@ -154,6 +157,74 @@ __global__ void hyp_refine_kernel(int B, int D, int H, int W, int scale, const f
   }
 }
 
+// One 2x2 stride-2 window of SparseDownSampleClose: the pooled max of encode = -(1-m)*600 - d (scanned
+// row-major with aten's max_pool "v > max || isnan(v)" update, so ties and NaNs resolve identically)
+// and of the mask; d_out = -max(encode) - (1 - max(mask)) * 600. Every product is exact (m is 0 or 1).
+__device__ __forceinline__ void close_pool(const float dv[4], const float mv[4], float& dout, float& mout) {
+  float me = -__builtin_inff(), mm = -__builtin_inff();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float e = (-(1.f - mv[k])) * 600.f - dv[k];
+    if (e > me || isnan(e)) me = e;
+    if (mv[k] > mm || isnan(mv[k])) mm = mv[k];
+  }
+  dout = -me - (1.f - mm) * 600.f;
+  mout = mm;
+}
+
+// Level 0 -> 1: thread per level-1 window over ceil(h/2) x ceil(w/2) (odd edges write level 0 only).
+// d0 = (depth - dmin) / (dmax - dmin); mask0 = mask ? mask : (d0 > 0).
+__global__ void sparse_pool0_kernel(int h, int w, const float* __restrict__ depth, const float* __restrict__ dvals,
+                                    int Dv, const float* __restrict__ mask, float* __restrict__ d0,
+                                    float* __restrict__ d1, float* __restrict__ m1) {
+  const int h1 = h >> 1, w1 = w >> 1, hc = (h + 1) >> 1, wc = (w + 1) >> 1;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x, b = blockIdx.y;
+  if (p >= hc * wc) return;
+  const int y = p / wc, x = p % wc;
+  const float dmin = dvals[b * Dv], den = dvals[b * Dv + Dv - 1] - dmin;
+  const size_t base = (size_t)b * h * w;
+  float dv[4], mv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int Y = 2 * y + (k >> 1), X = 2 * x + (k & 1);
+    dv[k] = mv[k] = 0.f;
+    if (Y < h && X < w) {
+      const size_t i = base + (size_t)Y * w + X;
+      dv[k] = (depth[i] - dmin) / den;
+      mv[k] = mask ? mask[i] : (dv[k] > 0.f ? 1.f : 0.f);
+      d0[i] = dv[k];
+    }
+  }
+  if (y < h1 && x < w1) {
+    float dd, mm;
+    close_pool(dv, mv, dd, mm);
+    const size_t o = (size_t)b * h1 * w1 + (size_t)y * w1 + x;
+    d1[o] = dd;
+    m1[o] = mm;
+  }
+}
+
+// Level l -> l+1 (h, w: level-l size). mout may be NULL (the last level's mask is unused).
+__global__ void sparse_pool_kernel(int h, int w, const float* __restrict__ din, const float* __restrict__ min_,
+                                   float* __restrict__ dout, float* __restrict__ mout) {
+  const int h1 = h >> 1, w1 = w >> 1;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x, b = blockIdx.y;
+  if (p >= h1 * w1) return;
+  const int y = p / w1, x = p % w1;
+  float dv[4], mv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const size_t i = (size_t)b * h * w + (size_t)(2 * y + (k >> 1)) * w + 2 * x + (k & 1);
+    dv[k] = din[i];
+    mv[k] = min_[i];
+  }
+  float dd, mm;
+  close_pool(dv, mv, dd, mm);
+  const size_t o = (size_t)b * h1 * w1 + p;
+  dout[o] = dd;
+  if (mout) mout[o] = mm;
+}
+
 }  // namespace
 
 hipError_t launch_proj_prepare(hipStream_t s, int B, int N, const float* proj, float* rt) {
@@ -174,6 +245,20 @@ hipError_t launch_hyp_refine(hipStream_t s, int B, int D, int H, int W, int scal
   int hw = (H / scale) * (W / scale);
   hipLaunchKernelGGL(hyp_refine_kernel, dim3((hw + 255) / 256, B), dim3(256), 0, s, B, D, H, W, scale, pd, pv, hp, wp,
                      out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sparse_pyramid(hipStream_t s, int B, int h, int w, const float* depth, const float* dv, int Dv,
+                                 const float* mask, float* d0, float* d1, float* d2, float* d3, float* m1, float* m2) {
+  const int hc = (h + 1) >> 1, wc = (w + 1) >> 1;
+  hipLaunchKernelGGL(sparse_pool0_kernel, dim3((hc * wc + 255) / 256, B), dim3(256), 0, s, h, w, depth, dv, Dv, mask,
+                     d0, d1, m1);
+  const int h1 = h >> 1, w1 = w >> 1, h2 = h1 >> 1, w2 = w1 >> 1, h3 = h2 >> 1, w3 = w2 >> 1;
+  if (h2 * w2 > 0)
+    hipLaunchKernelGGL(sparse_pool_kernel, dim3((h2 * w2 + 255) / 256, B), dim3(256), 0, s, h1, w1, d1, m1, d2, m2);
+  if (h3 * w3 > 0)
+    hipLaunchKernelGGL(sparse_pool_kernel, dim3((h3 * w3 + 255) / 256, B), dim3(256), 0, s, h2, w2, d2, m2, d3,
+                       (float*)nullptr);
   return hipGetLastError();
 }
 

@@ -20,7 +20,7 @@ import torch.nn as nn
 from . import _capi
 from ._capi import check, ptr
 from .engine import DTYPES
-from .frontend import ConvBNReLU2d, DeconvBNReLU2d, GeoBlock, sparse_pool_close
+from .frontend import ConvBNReLU2d, DeconvBNReLU2d, GeoBlock
 
 
 class HipConv2d:
@@ -57,12 +57,20 @@ class HipConv2d:
             except Exception:
                 pass
 
-    def __call__(self, B, Hi, Wi, in0=None, in1=None, geo=(), res_pre=None, res_post=None, post_up=1):
+    def out_shape(self, B, Hi, Wi):
         ho, wo, cs = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(self._lib.damvs_conv2d_out_size(self.handle, Hi, Wi, ctypes.byref(ho), ctypes.byref(wo),
                                               ctypes.byref(cs)))
+        return (B, ho.value, wo.value, cs.value)
+
+    def __call__(self, B, Hi, Wi, in0=None, in1=None, geo=(), res_pre=None, res_post=None, post_up=1, out=None):
         dev = (in0 if in0 is not None else geo[0][0]).device
-        out = torch.empty(B, ho.value, wo.value, cs.value, device=dev, dtype=self.dtype)
+        shape = self.out_shape(B, Hi, Wi)
+        if out is None:
+            out = torch.empty(shape, device=dev, dtype=self.dtype)
+        elif tuple(out.shape) != shape or out.dtype != self.dtype or not out.is_contiguous():
+            raise ValueError("conv2d out: need a contiguous %s %s tensor, got %s %s"
+                             % (self.dtype, shape, out.dtype, tuple(out.shape)))
         gp = gs = None
         if self.ngeo:
             assert len(geo) == self.ngeo, (len(geo), self.ngeo)
@@ -74,10 +82,28 @@ class HipConv2d:
 
 
 def planes(t):
-    """(B, C, H, W) fp32 tensor -> list of C (plane view, batch stride) for the geo inputs."""
-    t = t.float().contiguous()
-    B, C, H, W = t.shape
-    return [(t[:, c], C * H * W) for c in range(C)]
+    """(B, C, H, W) fp32 tensor -> list of C (plane view, batch stride) for the geo inputs. Rows must be
+    dense (a view of a larger tensor such as imgs[:, v] is taken as is, its batch stride passed along)."""
+    t = t.float()
+    if t.stride(3) != 1 or t.stride(2) != t.shape[3] or t.stride(1) != t.shape[2] * t.shape[3]:
+        t = t.contiguous()
+    return [(t[:, c], t.stride(0)) for c in range(t.shape[1])]
+
+
+def sparse_depth_pyramid(depth, depth_values, mask=None):
+    """GeoFeatureFusion's normalised depth and its three SparseDownSampleClose levels
+    (models/geometry.py:90-96, 117-119, 443-455) in three launches: depth (B,1,h,w) fp32 ->
+    [d, d_s2, d_s3, d_s4] as (B,1,h>>l,w>>l) fp32. mask: the 'mean' valid mask (None: 'basic', d > 0)."""
+    depth = depth.float().contiguous()
+    B, _, h, w = depth.shape
+    dv = depth_values.float().contiguous()
+    mk = mask.float().contiguous() if mask is not None else None
+    outs = [torch.empty(B, 1, h >> l, w >> l, device=depth.device) for l in range(4)]
+    scratch = torch.empty(B * (h // 2) * (w // 2) + B * (h // 4) * (w // 4) + 1, device=depth.device)
+    lib = _capi.load_library()
+    check(lib.damvs_sparse_depth_pyramid(_capi.stream_ptr(depth.device), B, h, w, ptr(depth), ptr(dv), dv.shape[1],
+                                         ptr(mk), *[ptr(o) for o in outs], ptr(scratch)))
+    return outs
 
 
 def fpn_top_layers(inner2, out3, dtype):
@@ -141,8 +167,18 @@ class HipFeatureNet:
                 self.out3 = L(fnet.out3, False, c0=fnet.out3.in_channels)
 
     def __call__(self, x):
-        B, _, H, W = x.shape
-        t = self.c0[0](B, H, W, geo=planes(x))
+        """x: (B, 3, H, W), or (B, N, 3, H, W) views batched view-major (row v*B + b) with no copy of the
+        images: the first layer reads each view's planes in place, one launch per view."""
+        if x.dim() == 5:
+            Bv, N, _, H, W = x.shape
+            B = N * Bv
+            L = self.c0[0]
+            t = torch.empty(L.out_shape(B, H, W), device=x.device, dtype=L.dtype)
+            for v in range(N):
+                L(Bv, H, W, geo=planes(x[:, v]), out=t[v * Bv:(v + 1) * Bv])
+        else:
+            B, _, H, W = x.shape
+            t = self.c0[0](B, H, W, geo=planes(x))
         c0 = self.c0[1](B, H, W, t)
         h, w = c0.shape[1:3]
         t = c0
@@ -224,17 +260,13 @@ class HipGeoFeatureFusion:
 
     def __call__(self, rgb, depth, confidence, depth_values, stage_idx, origin_feat):
         """rgb (B,3,h,w), depth/confidence (B,1,h,w) fp32; origin_feat NHWC (B,h,w,C). Returns NHWC."""
-        dmin = depth_values[:, 0, None, None, None]
-        dmax = depth_values[:, -1, None, None, None]
-        d = ((depth - dmin) / (dmax - dmin)).float()
-        if self.mask_type == "basic":
-            vm = (d > 0).float()
-        else:
-            vm = torch.logical_and(d > 0, confidence > confidence.mean()).float()
-        d2, m2 = sparse_pool_close(d, vm)
-        d3, m3 = sparse_pool_close(d2, m2)
-        d4, _ = sparse_pool_close(d3, m3)
-        P = {k: planes(v) for k, v in (("d", d), ("d2", d2), ("d3", d3), ("d4", d4))}
+        mask = None
+        if self.mask_type != "basic":
+            dmin = depth_values[:, 0, None, None, None]
+            d = (depth - dmin) / (depth_values[:, -1, None, None, None] - dmin)
+            mask = torch.logical_and(d > 0, confidence > confidence.mean()).float()
+        pyr = sparse_depth_pyramid(depth, depth_values, mask)
+        P = {k: planes(v) for k, v in zip(("d", "d2", "d3", "d4"), pyr)}
         B, _, h, w = rgb.shape
         r0 = self.rgb_init(B, h, w, geo=planes(rgb) + P["d"])
         e = self.rgb_enc

@@ -176,6 +176,14 @@ int damvs_regress(void* stream, int B, int D, int h, int w, const float* logits,
 int damvs_hypotheses(void* stream, int B, int D, int H, int W, int scale, const float* depth_values, int Dv,
                      const float* prev_depth, const float* prev_var, int hp, int wp, float* hyps);
 
+/* GeoFeatureFusion's sparse depth pyramid (models/geometry.py:90-96, 117-121; SparseDownSampleClose,
+ * models/geometry.py:443-455): d0 = (depth - depth_values[b][0]) / (depth_values[b][Dv-1] - depth_values[b][0]),
+ * valid mask = mask ? mask : (d0 > 0) ('basic'), then three 2x2 stride-2 closest-valid poolings.
+ * depth / mask: [B][h][w] fp32, h, w >= 8; d_l: [B][h >> l][w >> l] (floor sizes, as max_pool2d); scratch: at least
+ * B*(h/2)*(w/2) + B*(h/4)*(w/4) floats (the level-1/2 masks). Bitwise equal to the reference's torch ops. */
+int damvs_sparse_depth_pyramid(void* stream, int B, int h, int w, const float* depth, const float* depth_values, int Dv,
+                               const float* mask, float* d0, float* d1, float* d2, float* d3, float* scratch);
+
 /* ---- 2D front-end convolutions (FeatureNet models/module.py:355-462,
  * GeoFeatureFusion models/geometry.py:14-277). One layer = Conv2d or ConvTranspose2d with BN already
  * folded into weight/bias by the caller, optional ReLU, fused concat of up to two NHWC tensors and up

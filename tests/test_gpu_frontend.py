@@ -221,3 +221,50 @@ def test_geofusion_hip_vs_oracle(stage_idx, dtype, tol):
                                            nhwc(origin).to(DEV, dtype))
     err = rel_max(got.float().cpu().permute(0, 3, 1, 2).numpy(), ref.numpy())
     assert err < tol, err
+
+
+@pytest.mark.parametrize("hw", [(64, 80), (37, 51), (8, 9)])
+@pytest.mark.parametrize("mask_type", ["basic", "mean"])
+def test_sparse_depth_pyramid_bitwise_vs_torch(hw, mask_type):
+    """damvs_sparse_depth_pyramid vs the reference's own torch ops (models/geometry.py:90-96 normalisation
+    and mask, SparseDownSampleClose :443-455 three times) on the GPU: bitwise, odd sizes included."""
+    from damvsnet_amd.frontend import sparse_pool_close
+    from damvsnet_amd.frontend_hip import sparse_depth_pyramid
+    h, w = hw
+    g = torch.Generator().manual_seed(h * w)
+    depth = (425 + 500 * torch.rand(3, 1, h, w, generator=g)).to(DEV)
+    depth[:, :, : h // 3] = 300.0                                 # invalid rows (d <= 0)
+    depth[1, 0, :, 1::3] = 200.0                                  # ragged invalid columns
+    conf = torch.rand(3, 1, h, w, generator=g).to(DEV)
+    dv = torch.stack([torch.linspace(425, 935, 48), torch.linspace(400, 900, 48),
+                      torch.linspace(500, 1000, 48)]).to(DEV)
+    dmin, dmax = dv[:, 0, None, None, None], dv[:, -1, None, None, None]
+    d = (depth - dmin) / (dmax - dmin)
+    if mask_type == "basic":
+        vm, mask = torch.where(d > 0, torch.full_like(d, 1.0), torch.full_like(d, 0.0)), None
+    else:
+        vm = torch.where(torch.logical_and(d > 0, conf > conf.mean()), torch.full_like(d, 1.0), torch.full_like(d, 0.0))
+        mask = vm
+    d2, m2 = sparse_pool_close(d, vm)
+    d3, m3 = sparse_pool_close(d2, m2)
+    d4, _ = sparse_pool_close(d3, m3)
+    got = sparse_depth_pyramid(depth, dv, mask)
+    for lvl, (a, b) in enumerate(zip(got, (d, d2, d3, d4))):
+        assert a.shape == b.shape, (lvl, a.shape, b.shape)
+        assert torch.equal(a, b), (lvl, (a - b).abs().max().item())
+
+
+def test_featurenet_views_read_in_place():
+    """A (B, N, 3, H, W) batch goes through HipFeatureNet with the first layer reading each view's
+    planes in place (no view-major copy of the images): bitwise equal to the copied batch."""
+    from damvsnet_amd.frontend_hip import HipFeatureNet
+    sd = model_state("forward_160x128_48_32_8")
+    fnet, _ = _folded(sd, torch.bfloat16)
+    net = HipFeatureNet(fnet, torch.bfloat16)
+    imgs, _, _, _ = forward_inputs(2, 3, 64, 96)
+    imgs = imgs.to(DEV)
+    B, N = imgs.shape[:2]
+    a = net(imgs)
+    b = net(imgs.transpose(0, 1).reshape(N * B, *imgs.shape[2:]))
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
