@@ -155,4 +155,27 @@ template <> struct Vox8<float> {
   }
 };
 
+// Stage N 16-byte chunks into LDS with a 256-thread block: chunk c = threadIdx.x + 256 i comes from
+// load(c). Loads are issued BATCH at a time before their ds_writes, so each lane keeps BATCH HBM
+// reads in flight (a plain strided `lds[c] = load(c)` loop waits for every load before its write:
+// one read in flight per lane). Past-the-end chunks re-load chunk N - 1 and are not written.
+template <int N, int BATCH, typename Raw, typename F>
+__device__ __forceinline__ void stage_chunks(Raw* lds, F&& load) {
+  constexpr int PER = (N + 255) / 256;
+#pragma unroll
+  for (int i0 = 0; i0 < PER; i0 += BATCH) {
+    Raw r[BATCH];
+#pragma unroll
+    for (int i = 0; i < BATCH; ++i) {
+      const int c = threadIdx.x + (i0 + i) * 256;
+      if (i0 + i < PER) r[i] = load(c < N ? c : N - 1);
+    }
+#pragma unroll
+    for (int i = 0; i < BATCH; ++i) {
+      const int c = threadIdx.x + (i0 + i) * 256;
+      if (i0 + i < PER && c < N) lds[c] = r[i];
+    }
+  }
+}
+
 }  // namespace damvs

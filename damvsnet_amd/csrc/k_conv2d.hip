@@ -369,13 +369,13 @@ __global__ __launch_bounds__(256) void conv2d_lds_kernel(const Conv2dArgs a, int
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in0, (long long)a.B * a.Hi * a.Wi * CIN * ES);
   const int pin0 = b * a.Hi * a.Wi;
-  for (int c = threadIdx.x; c < TILE_CHUNKS; c += 256) {
+  stage_chunks<TILE_CHUNKS, 8>(tile, [&](int c) {
     const int row = c / ROW, col = c - row * ROW;
     const int iy = y0 - 1 + row, ix = x0 - 1 + col / CH;
     const bool ok = (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
     const uint32_t off = (uint32_t)(((pin0 + iy * a.Wi + x0 - 1) * CH + col) * 16);
-    tile[c] = IO::frag(rin, ok ? off : kOOB);
-  }
+    return IO::frag(rin, ok ? off : kOOB);
+  });
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

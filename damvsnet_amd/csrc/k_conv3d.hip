@@ -331,14 +331,14 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
   // halo fill: chunk c = (row, col) with row = (hz, hy); one row is LHW contiguous voxels in HBM
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * sizeof(T));
   const int vin0 = b * a.Di * a.Hi * a.Wi;
-  for (int c = threadIdx.x; c < TILE_CHUNKS; c += 256) {
+  stage_chunks<TILE_CHUNKS, 8>(tile, [&](int c) {
     const int row = c / ROW, col = c - row * ROW;
     const int hz = row / LHH, hy = row - hz * LHH;
     const int iz = z0 - 1 + hz, iy = y0 - 1 + hy, ix = x0 - 1 + col / CH;
     const bool ok = (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
     const uint32_t off = (uint32_t)(((vin0 + (iz * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16);
-    tile[c] = BufIO<T>::frag(rin, ok ? off : kOOB);
-  }
+    return BufIO<T>::frag(rin, ok ? off : kOOB);
+  });
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -511,14 +511,14 @@ __global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, 
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * sizeof(T));
   const int vin0 = b * a.Di * a.Hi * a.Wi;
-  for (int c = threadIdx.x; c < TILE_CHUNKS; c += 256) {
+  stage_chunks<TILE_CHUNKS, 8>(tile, [&](int c) {
     const int row = c / ROW, col = c - row * ROW;
     const int hz = row / LHH, hy = row - hz * LHH;
     const int iz = z0 - 1 + hz, iy = y0 - 1 + hy, ix = x0 - 1 + col / CH;
     const bool ok = (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
     const uint32_t off = (uint32_t)(((vin0 + (iz * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16);
-    tile[c] = BufIO<T>::frag(rin, ok ? off : kOOB);
-  }
+    return BufIO<T>::frag(rin, ok ? off : kOOB);
+  });
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

@@ -38,6 +38,8 @@ CASES = {
     "R dec 64->32 k3 r4 B=4": (False, 3, 1, 1, 0, 64, 0, 0, 32, True, 4, 296, 400, False, 0),
     "S fpn top k4s2 32->8 x20": (True, 4, 2, 1, 0, 32, 0, 0, 8, False, 20, 592, 800, False, 0),
     "T geo dec k3s2 16->8 B=4": (True, 3, 2, 1, 1, 16, 0, 0, 8, True, 4, 592, 800, False, 0),
+    "U conv0.1 8->8 k3 full x20": (False, 3, 1, 1, 0, 8, 0, 0, 8, True, 20, 1184, 1600, False, 0),
+    "V geo dec 8->8 k3 full B=4": (False, 3, 1, 1, 0, 8, 0, 0, 8, True, 4, 1184, 1600, False, 0),
 }
 
 
@@ -90,6 +92,20 @@ def main():
                     (res_post.numel() if up else 0)) + 4 * B * Hi * Wi * ngeo
         print("%-30s %8.1f us  %7.1f TFLOP/s  %6.2f TB/s" % (name, us, flop / us * 1e-6, byt / us * 1e-6), flush=True)
     print("total %.1f us" % tot)
+    # HBM ceiling for a read + write stream of these sizes: a device copy (torch) of in0's bytes
+    for nb in (606 * 2 ** 20, 121 * 2 ** 20):
+        x = torch.empty(nb // 2, device=dev, dtype=torch.bfloat16)
+        y = torch.empty_like(x)
+        for _ in range(3):
+            y.copy_(x)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iters):
+            y.copy_(x)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / args.iters
+        print("copy %4d MiB -> %4d MiB      %8.1f us  %6.2f TB/s (read + write)" % (nb >> 20, nb >> 20, us, 2 * nb / us * 1e-6))
 
 
 if __name__ == "__main__":
