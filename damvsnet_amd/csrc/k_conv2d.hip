@@ -1085,18 +1085,9 @@ hipError_t launch_lds2(hipStream_t s, const Conv2dArgs& a) {
 // loads in flight per row, each row feeding both pixels); weights sit in LDS as wave-uniform
 // broadcast reads.
 template <typename T, int COUT, int K, int NG>
-__global__ __launch_bounds__(256) void conv2d_planes_kernel(const Conv2dArgs a) {
-  constexpr int P = K / 2, RW = K * NG * COUT / 4;  // float4s per kernel row
-  // [K + 2][kx][g][COUT]: kernel rows -1 and K are zero, so the two pixels' accumulations need no
-  // row-validity branches (row r feeds pixel 0 with kernel row r and pixel 1 with kernel row r-1).
-  __shared__ float4 s_w[(K + 2) * RW];
-  for (int i = threadIdx.x; i < (K + 2) * RW; i += blockDim.x) {
-    const int row = i / RW - 1, j = i % RW;
-    const int c4 = j % (COUT / 4), tg = row * K * NG + j / (COUT / 4);
-    s_w[i] = (row < 0 || row >= K) ? make_float4(0.f, 0.f, 0.f, 0.f)
-                                   : *reinterpret_cast<const float4*>(a.wgeo + (size_t)tg * a.cout_pad + c4 * 4);
-  }
-  __syncthreads();
+__global__ __launch_bounds__(256) void conv2d_planes_kernel(const Conv2dArgs a, const float* __restrict__ wg) {
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  constexpr int P = K / 2;
   const int Hp = (a.Ho + 1) / 2;
   const int Qtot = a.B * Hp * a.Wo;  // host checks it fits in int
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1104,13 +1095,18 @@ __global__ __launch_bounds__(256) void conv2d_planes_kernel(const Conv2dArgs a) 
   const int ox = q % a.Wo;
   const int oy0 = (q / a.Wo) % Hp * 2;
   const int b = q / (a.Wo * Hp);
-  float acc0[COUT], acc1[COUT];
+  // Weights are wave-uniform: scalar loads (restrict const argument) feed packed FMAs over channel
+  // pairs, (c, c+1) per v_pk_fma_f32 with one weight pair from SGPRs (per lane the same fused
+  // multiply-adds as the scalar form). Input row r feeds pixel 0 with kernel row r (r < K) and
+  // pixel 1 with kernel row r-1 (r > 0).
+  f32x2_t acc0[COUT / 2], acc1[COUT / 2];
 #pragma unroll
-  for (int c = 0; c < COUT; ++c) acc0[c] = acc1[c] = a.bias[c];
+  for (int c = 0; c < COUT / 2; ++c) acc0[c] = acc1[c] = (f32x2_t){a.bias[2 * c], a.bias[2 * c + 1]};
   const float* gp[NG];
 #pragma unroll
   for (int g = 0; g < NG; ++g) gp[g] = a.geo[g] + (size_t)b * a.geo_bstride[g];
-#pragma unroll 1
+  const int cp = a.cout_pad;
+#pragma unroll 1  // (fully unrolled: all rows' loads hoisted, 1.2-2.4x slower)
   for (int r = 0; r <= K; ++r) {
     const int iy = oy0 - P + r;
     const bool oky = (unsigned)iy < (unsigned)a.Hi;
@@ -1127,29 +1123,33 @@ __global__ __launch_bounds__(256) void conv2d_planes_kernel(const Conv2dArgs a) 
         v[kx][g] = ok ? x : 0.f;
       }
     }
-    const float4* w0 = s_w + (r + 1) * RW;  // kernel row r for pixel 0
-    const float4* w1 = s_w + r * RW;        // kernel row r-1 for pixel 1
+    auto row = [&](const float* w, f32x2_t* acc) {
 #pragma unroll
-    for (int kx = 0; kx < K; ++kx)
+      for (int kx = 0; kx < K; ++kx)
 #pragma unroll
-      for (int g = 0; g < NG; ++g)
+        for (int g = 0; g < NG; ++g) {
+          const f32x2_t x = {v[kx][g], v[kx][g]};
+          const float* wt = w + (kx * NG + g) * cp;
 #pragma unroll
-        for (int c4 = 0; c4 < COUT / 4; ++c4) {
-          const float4 u = w0[(kx * NG + g) * (COUT / 4) + c4];
-          const float4 z = w1[(kx * NG + g) * (COUT / 4) + c4];
-          const float x = v[kx][g];
-          acc0[c4 * 4 + 0] += u.x * x; acc0[c4 * 4 + 1] += u.y * x;
-          acc0[c4 * 4 + 2] += u.z * x; acc0[c4 * 4 + 3] += u.w * x;
-          acc1[c4 * 4 + 0] += z.x * x; acc1[c4 * 4 + 1] += z.y * x;
-          acc1[c4 * 4 + 2] += z.z * x; acc1[c4 * 4 + 3] += z.w * x;
+          for (int c = 0; c < COUT / 2; ++c)
+            acc[c] = __builtin_elementwise_fma((f32x2_t){wt[2 * c], wt[2 * c + 1]}, x, acc[c]);
         }
+    };
+    if (r < K) row(wg + (size_t)r * K * NG * cp, acc0);
+    if (r > 0) row(wg + (size_t)(r - 1) * K * NG * cp, acc1);
+  }
+  float o0[COUT], o1[COUT];
+#pragma unroll
+  for (int c = 0; c < COUT / 2; ++c) {
+    o0[2 * c] = acc0[c].x; o0[2 * c + 1] = acc0[c].y;
+    o1[2 * c] = acc1[c].x; o1[2 * c + 1] = acc1[c].y;
   }
   const bool two = oy0 + 1 < a.Ho;
 #pragma unroll
   for (int c0 = 0; c0 < COUT; c0 += 4) {
     if (c0 >= a.cout) break;
-    tail4<T>(a, b, oy0, ox, c0, acc0 + c0);
-    if (two) tail4<T>(a, b, oy0 + 1, ox, c0, acc1 + c0);
+    tail4<T>(a, b, oy0, ox, c0, o0 + c0);
+    if (two) tail4<T>(a, b, oy0 + 1, ox, c0, o1 + c0);
   }
 }
 
@@ -1193,10 +1193,10 @@ hipError_t launch_planes_k(hipStream_t st, const Conv2dArgs& a) {
   const long long Qtot = (long long)a.B * ((a.Ho + 1) / 2) * a.Wo;
   dim3 grid((unsigned)((Qtot + 255) / 256));
   switch (a.ngeo) {
-    case 1: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 1>), grid, dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 2>), grid, dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 3>), grid, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 4>), grid, dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 1>), grid, dim3(256), 0, st, a, a.wgeo); break;
+    case 2: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 2>), grid, dim3(256), 0, st, a, a.wgeo); break;
+    case 3: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 3>), grid, dim3(256), 0, st, a, a.wgeo); break;
+    default: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 4>), grid, dim3(256), 0, st, a, a.wgeo); break;
   }
   return hipGetLastError();
 }

@@ -59,6 +59,8 @@ CASES = [
     (False, 1, 1, 0, 0, 64, 0, (64,), 128, False, False, 0),        # wide: 1x1 (GeoBlock downsample)
     (False, 3, 1, 1, 0, 32, 0, (0,), 32, True, True, 0),            # halo, one slice (bf16): 32+g -> 32
     (False, 3, 1, 1, 0, 32, 0, (32,), 16, True, False, 0),          # halo, one slice, one cout tile
+    (False, 3, 1, 1, 0, 0, 0, (0, 1, 2), 8, True, False, 0),         # planes: FeatureNet RGB conv 3->8
+    (False, 5, 1, 2, 0, 0, 0, (0, 1), 8, True, False, 0),            # planes: depth_conv_init 2->8
 ]
 
 

@@ -40,6 +40,9 @@ CASES = {
     "T geo dec k3s2 16->8 B=4": (True, 3, 2, 1, 1, 16, 0, 0, 8, True, 4, 592, 800, False, 0),
     "U conv0.1 8->8 k3 full x20": (False, 3, 1, 1, 0, 8, 0, 0, 8, True, 20, 1184, 1600, False, 0),
     "V geo dec 8->8 k3 full B=4": (False, 3, 1, 1, 0, 8, 0, 0, 8, True, 4, 1184, 1600, False, 0),
+    "W conv0.0 planes g3->8 k3 x20": (False, 3, 1, 1, 0, 0, 0, 3, 8, True, 20, 1184, 1600, False, 0),
+    "X rgb init g4->8 k5 B=4": (False, 5, 1, 2, 0, 0, 0, 4, 8, True, 4, 1184, 1600, False, 0),
+    "Y depth init g2->8 k5 B=4": (False, 5, 1, 2, 0, 0, 0, 2, 8, True, 4, 1184, 1600, False, 0),
 }
 
 
