@@ -88,6 +88,8 @@ SIGNATURES = (
                                  c_int, c_int, c_void_p)),
     ("damvs_sparse_depth_pyramid", c_int, (c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p)),
+    ("damvs_fpn_top_forward", c_int, (c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p)),
     ("damvs_conv2d_create", c_int, (ctypes.POINTER(DamvsConv2dDesc), c_void_p, c_void_p, c_int,
                                     ctypes.POINTER(c_void_p))),
     ("damvs_conv2d_destroy", c_int, (c_void_p,)),

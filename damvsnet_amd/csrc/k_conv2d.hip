@@ -1304,7 +1304,111 @@ __global__ __launch_bounds__(256) void border_bias_kernel(BorderArgs a, int B, i
   }
 }
 
+// FeatureNet's FPN top level in one launch (bf16): out = conv3x3_p1(c0; Wc) + ConvTranspose2d_k4s2p1(f; Wt) + bias,
+// the two layers fpn_top_layers (frontend_hip.py) re-associates out3(up2(f) + inner2(c0)) into
+// (models/module.py:455-459), fused so the transposed conv's full-resolution 8-channel output never makes an
+// HBM round trip (at cfgC 606 MB written and read back). Both terms share the x-pair MFMA layout of the
+// transposed conv: the 16 A rows are (output x parity px, channel co), the 16 B columns q-positions (output
+// x = 2q + px). The 3x3 conv joins through x-pair taps too: output pair (2q, 2q+1) reads c0 at 2q-1..2q+2,
+// one tap per lane group (8 channels), so each kernel row is one K chunk with A[(px, co)][(g, ci)] =
+// Wc[co][ci][dy][g - px] (0 outside 0..2). A block owns 8 output rows x 64 q-columns (128 output columns):
+// c0's (8+2) x 130-pixel halo sits in LDS split by x parity (16 consecutive q read 16 consecutive records)
+// and f's 6 x 66-pixel x 32-channel halo with its 16-byte chunks XOR-swizzled by (pixel >> 2) & 3; both are
+// filled by stage_chunks (8 loads in flight per lane). Per output row 3 + 6 MFMAs, the 15 A chunks in
+// registers for the whole block. Row parity py of output row y0 + j is j & 1 (y0 is a multiple of 8).
+constexpr int FT_R = 8, FT_Q = 64;
+
+__global__ __launch_bounds__(256) void fpn_top_kernel(const bf16_t* __restrict__ c0, const bf16_t* __restrict__ f,
+                                                      const uint4* __restrict__ apack, const float* __restrict__ bias,
+                                                      bf16_t* __restrict__ out, int B, int H, int W, int tiles_x,
+                                                      int tiles_y, int ntiles) {
+  typedef BufIO<bf16_t> IO;
+  constexpr int CW = FT_Q + 2;                       // c0 records per (row, parity): q0-1 .. q0+64
+  constexpr int C0_CHUNKS = (FT_R + 2) * 2 * CW;
+  constexpr int FR = FT_R / 2 + 2, FC = FT_Q + 2;    // f halo rows x columns
+  constexpr int F_CHUNKS = FR * FC * 4;
+  __shared__ uint4 sc0[C0_CHUNKS];
+  __shared__ uint4 sf[F_CHUNKS];
+
+  const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
+  int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tx = tt % tiles_x; tt /= tiles_x;
+  const int ty = tt % tiles_y;
+  const int b = tt / tiles_y;
+  const int y0 = ty * FT_R, q0 = tx * FT_Q;
+  const int Hh = H >> 1, Wh = W >> 1;
+  const __amdgpu_buffer_rsrc_t rc0 = make_rsrc(c0, (long long)B * H * W * 16);
+  const __amdgpu_buffer_rsrc_t rf = make_rsrc(f, (long long)B * Hh * Wh * 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+
+  uint4 af[15];
+#pragma unroll
+  for (int c = 0; c < 15; ++c) af[c] = apack[c * 64 + lane];
+
+  stage_chunks<C0_CHUNKS, 8>(sc0, [&](int c) {
+    const int hr = c / (2 * CW), rem = c - hr * (2 * CW), par = rem / CW, jj = rem - par * CW;
+    const int y = y0 - 1 + hr, x = 2 * (q0 - 1 + jj) + par;
+    const bool ok = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+    return IO::frag(rc0, ok ? (uint32_t)(((b * H + y) * W + x) * 16) : kOOB);
+  });
+  stage_chunks<F_CHUNKS, 8>(sf, [&](int c) {
+    const int p = c >> 2, fr = p / FC, fc = p - fr * FC;
+    const int chunk = (c & 3) ^ ((fc >> 2) & 3);
+    const int y = (y0 >> 1) - 1 + fr, x = q0 - 1 + fc;
+    const bool ok = (unsigned)y < (unsigned)Hh && (unsigned)x < (unsigned)Wh;
+    return IO::frag(rf, ok ? (uint32_t)((((b * Hh + y) * Wh + x) * 4 + chunk) * 16) : kOOB);
+  });
+  __syncthreads();
+
+  f32x4_t acc[FT_R];
+#pragma unroll
+  for (int j = 0; j < FT_R; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  const int qn = wave * 16 + n;
+  // c0 record of lane group g (x = 2q - 1 + g): parity plane (g + 1) & 1, index q - q0 + 1 + ((g - 1) >> 1)
+  const uint4* c0b = sc0 + ((g + 1) & 1) * CW + qn + 1 + ((g - 1) >> 1);
+#pragma unroll
+  for (int j = 0; j < FT_R; ++j) {
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) Frag2<bf16_t>::mma(af[dy], c0b[(j + dy) * 2 * CW], acc[j]);
+    const int py = j & 1;
+#pragma unroll
+    for (int r2 = 0; r2 < 2; ++r2)
+#pragma unroll
+      for (int xx = 0; xx < 3; ++xx) {
+        const int fr = j / 2 + r2 + py, fc = qn + xx;
+        Frag2<bf16_t>::mma(af[3 + py * 6 + r2 * 3 + xx], sf[(fr * FC + fc) * 4 + (g ^ ((fc >> 2) & 3))], acc[j]);
+      }
+  }
+
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(out, (long long)B * H * W * 16);
+  const int px = g >> 1, cb = (g & 1) * 4;
+  float bs[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bs[i] = bias[cb + i];
+  const int x = 2 * (q0 + qn) + px;
+#pragma unroll
+  for (int j = 0; j < FT_R; ++j) {
+    const int y = y0 + j;
+    float r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = acc[j][i] + bs[i];
+    const bool ok = y < H && x < W;
+    IO::stq(ro, ok ? (uint32_t)((((b * H + y) * W + x) * 8 + cb) * 2) : kOOB, r);
+  }
+}
+
 }  // namespace
+
+hipError_t launch_fpn_top(hipStream_t s, int B, int H, int W, const void* c0, const void* f, const void* apack,
+                          const float* bias, void* out) {
+  const int tx = (W / 2 + FT_Q - 1) / FT_Q, ty = (H + FT_R - 1) / FT_R;
+  const long long nt = (long long)tx * ty * B;
+  hipLaunchKernelGGL(fpn_top_kernel, dim3((unsigned)nt), dim3(256), 0, s, static_cast<const bf16_t*>(c0),
+                     static_cast<const bf16_t*>(f), static_cast<const uint4*>(apack), bias, static_cast<bf16_t*>(out),
+                     B, H, W, tx, ty, (int)nt);
+  return hipGetLastError();
+}
 
 hipError_t launch_border_bias(hipStream_t s, int store, const BorderArgs& a, int B, int H, int W, int cstored, int cout,
                               void* out) {

@@ -13,6 +13,7 @@ SparseDownSampleClose geometry.py:443-455.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -119,8 +120,8 @@ def fpn_top_layers(inner2, out3, dtype):
                             fall outside the image at border pixels (zero padding of the sum):
                             damvs_conv2d_border_bias with corr[tap] = out3[tap] . bias.
 
-    Returns (transposed layer on f, 3x3 layer on c0, corr [9 * cout] fp32) — the second layer takes
-    the first's output as its pre-activation residual."""
+    Returns (transposed layer on f, 3x3 layer on c0, corr [9 * cout] fp32, (Wt, Wc, bias) fp32 for the
+    fused launch) — the second layer takes the first's output as its pre-activation residual."""
     W3 = out3.weight.detach().to("cpu", torch.float64)                 # (co, m, 3, 3)
     W1 = inner2.weight.detach().to("cpu", torch.float64)[:, :, 0, 0]   # (m, ci)
     b1 = inner2.bias.detach().to("cpu", torch.float64)                 # (m,)
@@ -137,7 +138,33 @@ def fpn_top_layers(inner2, out3, dtype):
     c0 = nn.Conv2d(ci, co, 3, padding=1, bias=True)
     c0.weight.data = torch.einsum("omyx,mi->oiyx", W3, W1).float()
     c0.bias.data = corr.sum((0, 1)).float()
-    return HipConv2d(up, dtype, False, c0=m), HipConv2d(c0, dtype, False, c0=ci), corr.reshape(-1).float().contiguous()
+    return (HipConv2d(up, dtype, False, c0=m), HipConv2d(c0, dtype, False, c0=ci), corr.reshape(-1).float().contiguous(),
+            (up.weight.data.clone(), c0.weight.data.clone(), c0.bias.data.clone()))
+
+
+def pack_fpn_top(wt, wc):
+    """MFMA A chunks of damvs_fpn_top_forward (15 x 64 lanes x 8 bf16): lane (g = lane >> 4, row = lane & 15)
+    holds A[row][8g .. 8g+7], row = (output x parity px = row >> 3, channel co = row & 7).
+      chunks 0-2  (3x3 conv, kernel row dy): k = (x-pair tap g: c0 column 2q-1+g, channel) -> Wc[co][ci][dy][g-px];
+      chunks 3-14 (ConvTranspose k4 s2 p1, row parity py, input row m-1+rr with rr = r2+py, column q-1+xx):
+                  k = channel 8g+e -> Wt[ci][co][ky][kx], ky = py+3-2rr, kx = px+3-2xx (zero outside 0..3).
+    wt: (32, 8, 4, 4), wc: (8, 8, 3, 3) fp32."""
+    A = torch.zeros(15, 64, 8, dtype=torch.float32)
+    for lane in range(64):
+        g, row = lane >> 4, lane & 15
+        px, co = row >> 3, row & 7
+        for dy in range(3):
+            kx = g - px
+            if 0 <= kx <= 2:
+                A[dy, lane] = wc[co, :, dy, kx]
+        for py in range(2):
+            for r2 in range(2):
+                ky = py + 3 - 2 * (r2 + py)
+                for xx in range(3):
+                    kx = px + 3 - 2 * xx
+                    if 0 <= kx <= 3:
+                        A[3 + py * 6 + r2 * 3 + xx, lane] = wt[8 * g:8 * g + 8, co, ky, kx]
+    return A.to(torch.bfloat16)
 
 
 class HipFeatureNet:
@@ -155,7 +182,12 @@ class HipFeatureNet:
             self.inner1 = L(fnet.inner1, False, c0=fnet.inner1.in_channels)
             self.out2 = L(fnet.out2, False, c0=fnet.out2.in_channels)
             if self.num_stage == 3:
-                self.top_up, self.top_c0, self.top_corr = fpn_top_layers(fnet.inner2, fnet.out3, dtype)
+                self.top_up, self.top_c0, self.top_corr, (wt, wc, bc) = fpn_top_layers(fnet.inner2, fnet.out3, dtype)
+                # one fused launch (damvs_fpn_top_forward) for bf16; DAMVS_FPN_TOP_FUSED=0 keeps the two layers
+                self.top_fused = None
+                if dtype == torch.bfloat16 and wt.shape[0] == 32 and wt.shape[1] == 8 and wc.shape[1] == 8 and \
+                        os.environ.get("DAMVS_FPN_TOP_FUSED", "1") != "0":
+                    self.top_fused = (pack_fpn_top(wt, wc), bc.float())
         else:
             self.up = []
             for fu in [fnet.deconv1] + ([fnet.deconv2] if self.num_stage == 3 else []):
@@ -194,9 +226,17 @@ class HipFeatureNet:
             out["stage2"] = self.out2(B, f.shape[1], f.shape[2], f)
             if self.num_stage == 3:
                 # out3(up2(f) + inner2(c0)) without the 32-channel full-resolution sum (fpn_top_layers)
-                t = self.top_up(B, f.shape[1], f.shape[2], f)
-                o3 = self.top_c0(B, h, w, c0, res_pre=t)
                 lib = self.top_c0._lib
+                if self.top_fused is not None and h == 2 * f.shape[1] and w == 2 * f.shape[2]:
+                    ap, bc = self.top_fused
+                    if ap.device != c0.device:
+                        self.top_fused = ap, bc = ap.to(c0.device), bc.to(c0.device)
+                    o3 = torch.empty(B, h, w, 8, device=c0.device, dtype=c0.dtype)
+                    check(lib.damvs_fpn_top_forward(_capi.stream_ptr(c0.device), B, h, w, ptr(c0), ptr(f), ptr(ap),
+                                                    ptr(bc), ptr(o3)))
+                else:
+                    t = self.top_up(B, f.shape[1], f.shape[2], f)
+                    o3 = self.top_c0(B, h, w, c0, res_pre=t)
                 check(lib.damvs_conv2d_border_bias(_capi.stream_ptr(o3.device), DTYPES[o3.dtype], B, h, w, o3.shape[3],
                                                    self.top_c0.cout, _capi.float_ptr(self.top_corr), ptr(o3)))
                 out["stage3"] = o3

@@ -225,6 +225,15 @@ int damvs_conv2d_forward(const damvs_conv2d* layer, void* stream, int B, int Hi,
 int damvs_conv2d_border_bias(void* stream, int dtype, int B, int H, int W, int cout_stored, int cout, const float* corr,
                              void* out);
 
+/* FeatureNet's FPN top level (models/module.py:455-459, out3(up2(f) + inner2(c0))) in one launch, bf16:
+ * out = conv3x3_p1(c0) + ConvTranspose2d_k4s2p1(f) + bias — the two layers of the re-association in
+ * damvsnet_amd/frontend_hip.py:fpn_top_layers, fused. c0 [B][H][W][8], f [B][H/2][W/2][32], out [B][H][W][8]
+ * (bf16); apack: 15 MFMA A chunks x 64 lanes x 8 bf16 (frontend_hip.pack_fpn_top: chunks 0-2 the 3x3 conv's
+ * kernel rows as x-pair taps, 3-14 the transposed conv's (row parity, input row, x offset) taps); bias: device
+ * fp32 [8]. H, W even. The border fix-up (damvs_conv2d_border_bias) follows as a separate call. */
+int damvs_fpn_top_forward(void* stream, int B, int H, int W, const void* c0, const void* f, const void* apack,
+                          const float* bias, void* out);
+
 /* ------------------------------------------------------------------ depth fusion (f4)
  * One reference view of the reference's dynamic-consistency fusion (filter/dypcd.py:98-297,
  * filter_depth per ref view): all maps [H][W] fp32 device buffers of one resolution. Camera
