@@ -316,24 +316,21 @@ hipError_t launch_t(hipStream_t s, int mode, const WarpArgs& a) {
   return hipErrorInvalidValue;
 }
 
-// [N views][B][h][w][C] -> [B][C/E][h][w][E] per view; one thread per (view, b, pixel, chunk).
-template <typename T>
-__global__ __launch_bounds__(256) void block_channels_kernel(const FeatPtrs src, FeatPtrs dst, int B, int hw, int C,
-                                                             int N) {
-  constexpr int E = Stor<T>::E;
-  const int CH = C / E;
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long per_view = (long long)B * hw * CH;
-  if (i >= per_view * N) return;
-  const int v = (int)(i / per_view);
-  long long r = i - v * per_view;
-  const int p = (int)(r % hw);
-  r /= hw;
-  const int q = (int)(r % CH);
-  const int b = (int)(r / CH);
-  const T* sp = reinterpret_cast<const T*>(src.p[v]) + ((size_t)b * hw + p) * C + q * E;
-  T* dp = const_cast<T*>(reinterpret_cast<const T*>(dst.p[v])) + (((size_t)b * CH + q) * hw + p) * E;
-  *reinterpret_cast<uint4*>(dp) = *reinterpret_cast<const uint4*>(sp);
+// [N views][B][h][w][C] -> [B][C/E][h][w][E] per view. One thread per pixel: it reads the pixel's NQ
+// consecutive 16-byte chunks (one contiguous C-vector) and writes chunk q to plane q, so both the reads and
+// each plane's writes are contiguous across the wave; blockIdx.y = view * B + batch element (no division).
+template <int NQ>
+__global__ __launch_bounds__(256) void block_channels_kernel(const FeatPtrs src, FeatPtrs dst, int B, int hw) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= hw) return;
+  const int v = blockIdx.y / B, b = blockIdx.y - v * B;
+  const uint4* sp = reinterpret_cast<const uint4*>(src.p[v]) + ((size_t)b * hw + p) * NQ;
+  uint4* dp = const_cast<uint4*>(reinterpret_cast<const uint4*>(dst.p[v])) + (size_t)b * NQ * hw + p;
+  uint4 r[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) r[q] = sp[q];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) dp[(size_t)q * hw] = r[q];
 }
 
 }  // namespace
@@ -345,12 +342,19 @@ hipError_t launch_warp_aggregate(hipStream_t s, int store, int mode, const WarpA
 
 hipError_t launch_block_channels(hipStream_t s, int store, const FeatPtrs& src, const FeatPtrs& dst, int N, int B,
                                  int hw, int C) {
-  const long long n = (long long)N * B * hw * (C / (store == ST_BF16 ? 8 : 4));
-  dim3 grid((unsigned)((n + 255) / 256));
-  if (store == ST_BF16)
-    hipLaunchKernelGGL(block_channels_kernel<bf16_t>, grid, dim3(256), 0, s, src, dst, B, hw, C, N);
-  else
-    hipLaunchKernelGGL(block_channels_kernel<float>, grid, dim3(256), 0, s, src, dst, B, hw, C, N);
+  const int nq = C / (store == ST_BF16 ? 8 : 4);
+  dim3 grid((unsigned)((hw + 255) / 256), (unsigned)(N * B));
+  switch (nq) {
+    case 1: hipLaunchKernelGGL(block_channels_kernel<1>, grid, dim3(256), 0, s, src, dst, B, hw); break;
+    case 2: hipLaunchKernelGGL(block_channels_kernel<2>, grid, dim3(256), 0, s, src, dst, B, hw); break;
+    case 3: hipLaunchKernelGGL(block_channels_kernel<3>, grid, dim3(256), 0, s, src, dst, B, hw); break;
+    case 4: hipLaunchKernelGGL(block_channels_kernel<4>, grid, dim3(256), 0, s, src, dst, B, hw); break;
+    case 5: hipLaunchKernelGGL(block_channels_kernel<5>, grid, dim3(256), 0, s, src, dst, B, hw); break;
+    case 6: hipLaunchKernelGGL(block_channels_kernel<6>, grid, dim3(256), 0, s, src, dst, B, hw); break;
+    case 7: hipLaunchKernelGGL(block_channels_kernel<7>, grid, dim3(256), 0, s, src, dst, B, hw); break;
+    case 8: hipLaunchKernelGGL(block_channels_kernel<8>, grid, dim3(256), 0, s, src, dst, B, hw); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -139,6 +139,20 @@ def test_warp_aggregate_channel_blocked_layout(C, dtype):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("C,dtype", [(32, torch.bfloat16), (16, torch.bfloat16), (8, torch.bfloat16),
+                                     (24, torch.bfloat16), (32, torch.float32), (4, torch.float32)])
+def test_block_channels_is_the_blocked_permutation(C, dtype):
+    """damvs_block_channels = NHWC (B,h,w,C) -> [B][C/E][h][w][E] (E = 16 bytes), bitwise, for several views,
+    a pixel count that is not a multiple of the 256-pixel block and every chunk count."""
+    from damvsnet_amd.engine import block_channels
+    g = torch.Generator().manual_seed(C)
+    B, h, w = 3, 17, 29
+    E = 16 // torch.empty((), dtype=dtype).element_size()
+    nhwc = [cuda(torch.randn(B, h, w, C, generator=g).to(dtype)) for _ in range(3)]
+    for src, got in zip(nhwc, block_channels(nhwc)):
+        assert torch.equal(got, src.view(B, h, w, C // E, E).permute(0, 3, 1, 2, 4).contiguous())
+
+
 @pytest.mark.parametrize("s,D", [(0, 48), (1, 32), (0, 64)])
 def test_prob_mfma_vs_split_path(s, D, monkeypatch):
     """bf16 stage forward (banded-MFMA prob conv + regression, k_regress.hip; opt-in DAMVS_PROB_MFMA=1)
