@@ -63,6 +63,15 @@ __device__ __forceinline__ void store_vec(T* p, const float* v) {
   for (int i = 0; i < C; i += Stor<T>::E) Stor<T>::store16(p + i, v + i);
 }
 
+// Occupancy cap: amdgpu_waves_per_eu(n) bounds the register allocation (VGPRs + AGPRs) so n waves fit per SIMD.
+// Used where a kernel's natural allocation sits just above a wave boundary (e.g. 132 + 64 AGPRs -> 160 VGPRs, no
+// spill: 2 -> 3 waves). n = 1 leaves the allocation free. -DDAMVS_NO_OCC builds drop every cap (A/B).
+#ifdef DAMVS_NO_OCC
+#define DAMVS_WAVES(n)
+#else
+#define DAMVS_WAVES(n) __attribute__((amdgpu_waves_per_eu(n)))
+#endif
+
 typedef unsigned int v4u32_t __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u32_t __attribute__((ext_vector_type(2)));
 

@@ -108,7 +108,7 @@ __device__ __forceinline__ void tail4(const Conv2dArgs& a, int b, int oy, int ox
 // so lane group g holds channels (g & 1) * 4 of output x = 2 qx + (g >> 1); group g + 1 hands its 4
 // channels to group g (g even), which loads / stores the pixel's whole 8-channel record.
 template <typename T, int MT, bool TWO, bool XP = false>
-__global__ __launch_bounds__(256) void conv2d_mfma_kernel(const Conv2dArgs a, int nqblk) {
+__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO ? 3 : 1)) void conv2d_mfma_kernel(const Conv2dArgs a, int nqblk) {
   typedef BufIO<T> IO;
   typedef typename IO::raw raw;
   constexpr int E = Stor<T>::E;
@@ -346,7 +346,7 @@ __device__ constexpr int halo2_toff(int t) {
 }
 
 template <typename T, int CIN, int MT>
-__global__ __launch_bounds__(256) void conv2d_lds_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int ntiles) {
+__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && CIN == 32 && MT == 2 ? 3 : 1)) void conv2d_lds_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int ntiles) {
   typedef BufIO<T> IO;
   typedef typename IO::raw raw;
   constexpr int E = Stor<T>::E;
@@ -752,7 +752,7 @@ constexpr int WC = 64, WR = 2;  // q-tile columns x rows
 constexpr int WPER = 7;         // halo pieces per thread: up to 448 pixels
 
 template <bool TWO>
-__global__ __launch_bounds__(256) void conv2d_wide_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int nsl,
+__global__ __launch_bounds__(256) DAMVS_WAVES(3) void conv2d_wide_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int nsl,
                                                           int dmin, int span) {
   typedef uint4 raw;
   typedef BufIO<bf16_t> IO;

@@ -106,7 +106,7 @@ __device__ __forceinline__ void finish4(const ConvArgs& a, __amdgpu_buffer_rsrc_
 // XP: x-parity-pair deconv phases (build_phases_xpair): MFMA row r = (x parity r >> 3, channel r & 7),
 // so lane group g stores channels (g & 1) * 4 .. +3 of output x = 2 qx + (g >> 1).
 template <typename T, int MT, bool XP>
-__global__ __launch_bounds__(256) void conv3d_mfma_kernel(const ConvArgs a, int nqblk) {
+__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1)) void conv3d_mfma_kernel(const ConvArgs a, int nqblk) {
   typedef BufIO<T> IO;
   typedef typename IO::raw raw;
   constexpr int E = Stor<T>::E;  // input channels per lane per K-chunk
@@ -922,7 +922,7 @@ hipError_t launch_lds(hipStream_t s, const ConvArgs& a) {
 // x offset, g & 1 = channel half) with the 9 A fragments in registers, so the whole layer is the
 // skip read + output write + one pass over the input, with no per-lane tap decoding or bounds tests
 // in the K loop. Same K order and weights as the x-pair gather kernel: identical results.
-__global__ __launch_bounds__(256) void deconv_xpair_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y,
+__global__ __launch_bounds__(256) DAMVS_WAVES(3) void deconv_xpair_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y,
                                                                   int nzc, int zc, int ntiles) {
   typedef uint4 raw;
   constexpr int CH = 2, QX = 16, QY = 8, PW = QX + 1, PH = QY + 1;

@@ -87,7 +87,7 @@ __device__ __forceinline__ Taps bilinear_taps(int h, int w, uint32_t rec, float 
 // current view is reduced, and the loads are unconditional (the last plane re-reads its own last
 // view) so the vmcnt waits count exactly.
 template <typename T, int C, int MODE, bool BLK, int NVC>
-__global__ __launch_bounds__(256) void warp_aggregate_kernel(const WarpArgs a, const float* __restrict__ cams,
+__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC == 0 && MODE == AGG_ADAPTIVE ? 3 : 1)) void warp_aggregate_kernel(const WarpArgs a, const float* __restrict__ cams,
                                                              int npix_blocks, int dchunk, int ndchunks) {
   constexpr int E = Stor<T>::E, NQ = C / E;
   static_assert(NVC % 2 == 0, "the view pipeline alternates two register sets");
