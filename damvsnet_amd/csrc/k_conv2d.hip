@@ -346,7 +346,7 @@ __device__ constexpr int halo2_toff(int t) {
 }
 
 template <typename T, int CIN, int MT>
-__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && CIN == 32 && MT == 2 ? 3 : 1)) void conv2d_lds_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int ntiles) {
+__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) != 2 ? 1 : CIN == 32 ? (MT == 2 ? 3 : 1) : MT == 1 ? 6 : 1)) void conv2d_lds_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int ntiles) {
   typedef BufIO<T> IO;
   typedef typename IO::raw raw;
   constexpr int E = Stor<T>::E;
