@@ -90,7 +90,7 @@ template <typename T, int C, int MODE, bool BLK, int NVC>
 __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC == 0 && MODE == AGG_ADAPTIVE ? 3 : 1)) void warp_aggregate_kernel(const WarpArgs a, const float* __restrict__ cams,
                                                              int npix_blocks, int dchunk, int ndchunks) {
   constexpr int E = Stor<T>::E, NQ = C / E;
-  static_assert(NVC % 2 == 0, "the view pipeline alternates two register sets");
+  static_assert(NVC % 2 == 0 || NVC < 0, "the view pipeline alternates two register sets");
   const int hw = a.h * a.w, ohw = a.rows * a.w;  // feature-map plane, computed rows (y0 .. y0 + rows - 1)
   const int nblk = npix_blocks * ndchunks * a.B;
   const int bid = blockIdx.x, q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
@@ -188,34 +188,53 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
     }
   };
 
-  if constexpr (NVC > 0) {
-    // source view j = 1 + v: ray (per lane), translation (block-uniform) and descriptor
-    float rx[NVC], ry[NVC], rz[NVC], tx[NVC], ty[NVC], tz[NVC];
-    __amdgpu_buffer_rsrc_t rs[NVC];
+  if constexpr (NVC != 0) {
+    // source view j = 1 + v: ray (per lane), translation (block-uniform) and descriptor. NVC > 0: the view count
+    // is a compile-time constant and the rays are hoisted out of the depth loop; NVC < 0: any even number of
+    // source views (a.N - 1, checked by the launcher), the view loop not unrolled and each view's ray recomputed
+    // from the SGPR camera (the same expression, so the same coordinates), so registers do not grow with N.
+    constexpr int NH = NVC > 0 ? NVC : 1;
+    const int nv = NVC > 0 ? NVC : a.N - 1;
+    float rx[NH], ry[NH], rz[NH], tx[NH], ty[NH], tz[NH];
+    __amdgpu_buffer_rsrc_t rs[NH];
+    if constexpr (NVC > 0) {
 #pragma unroll
-    for (int v = 0; v < NVC; ++v) {
-      const float* m = cam + v * 12;
-      rx[v] = m[0] * fx + m[1] * fy + m[2];
-      ry[v] = m[3] * fx + m[4] * fy + m[5];
-      rz[v] = m[6] * fx + m[7] * fy + m[8];
-      tx[v] = m[9];
-      ty[v] = m[10];
-      tz[v] = m[11];
-      rs[v] = make_rsrc(a.feats[v + 1], fbytes);
+      for (int v = 0; v < NVC; ++v) {
+        const float* m = cam + v * 12;
+        rx[v] = m[0] * fx + m[1] * fy + m[2];
+        ry[v] = m[3] * fx + m[4] * fy + m[5];
+        rz[v] = m[6] * fx + m[7] * fy + m[8];
+        tx[v] = m[9];
+        ty[v] = m[10];
+        tz[v] = m[11];
+        rs[v] = make_rsrc(a.feats[v + 1], fbytes);
+      }
     }
     auto taps = [&](int v, float hyp) {
-      const float qx = rx[v] * hyp + tx[v], qy = ry[v] * hyp + ty[v], qz = rz[v] * hyp + tz[v];
+      float qx, qy, qz;
+      if constexpr (NVC > 0) {
+        qx = rx[v] * hyp + tx[v], qy = ry[v] * hyp + ty[v], qz = rz[v] * hyp + tz[v];
+      } else {
+        const float* m = cam + v * 12;
+        const float vx = m[0] * fx + m[1] * fy + m[2];
+        const float vy = m[3] * fx + m[4] * fy + m[5];
+        const float vz = m[6] * fx + m[7] * fy + m[8];
+        qx = vx * hyp + m[9], qy = vy * hyp + m[10], qz = vz * hyp + m[11];
+      }
       // g = (q/qz) / ((W-1)/2) - 1 and ix = ((g + 1) W - 1) / 2 fold to ix = (q/qz) W/(W-1) - 1/2:
       // one reciprocal instead of four IEEE divisions (coordinates agree to ~1 ulp)
       const float iz = __builtin_amdgcn_rcpf(qz);
       return bilinear_taps(a.h, a.w, rec, qx * iz * kx - 0.5f, qy * iz * ky - 0.5f);
     };
     auto issue = [&](int v, const Taps& t, uint4* rv, float* wt) {
+      __amdgpu_buffer_rsrc_t r;
+      if constexpr (NVC > 0) r = rs[v];
+      else r = make_rsrc(a.feats[v + 1], fbytes);
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          rv[q * 4 + k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs[v], t.off[k], sb + q * qstep, 0));
+          rv[q * 4 + k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, t.off[k], sb + q * qstep, 0));
 #pragma unroll
       for (int k = 0; k < 4; ++k) wt[k] = t.wt[k];
     };
@@ -230,14 +249,22 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
       init(acc, sq);
       // view v's records are in (cur, wcur); the next (view, plane)'s go to (nxt, wnxt) before v is reduced
       auto step = [&](int v, const uint4* cur, const float* wcur, uint4* nxt, float* wnxt) {
-        if (v + 1 < NVC) issue(v + 1, taps(v + 1, hyp), nxt, wnxt);
+        if (v + 1 < nv) issue(v + 1, taps(v + 1, hyp), nxt, wnxt);
         else issue(0, taps(0, hyp_n), nxt, wnxt);  // next plane's first view (the last plane: a re-read)
         reduce(cur, wcur, acc, sq);
       };
+      if constexpr (NVC > 0) {
 #pragma unroll
-      for (int v = 0; v < NVC; v += 2) {
-        step(v, ra, wa, rb, wb);
-        step(v + 1, rb, wb, ra, wa);
+        for (int v = 0; v < NVC; v += 2) {
+          step(v, ra, wa, rb, wb);
+          step(v + 1, rb, wb, ra, wa);
+        }
+      } else {
+#pragma unroll 1
+        for (int v = 0; v < nv; v += 2) {
+          step(v, ra, wa, rb, wb);
+          step(v + 1, rb, wb, ra, wa);
+        }
       }
       hyp = hyp_n;
       hyp_n = hyp_nn;
@@ -277,8 +304,17 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
     const char* v = getenv("DAMVS_WARP_NO_PIPE");
     return v && v[0] == '1';
   }();
-  if (a.N == 5 && C <= 16 && !no_pipe)
+  // view pipeline: unrolled for N = 5 (the DTU default), a runtime view loop for any other odd N (7, 11: the
+  // cfgD / cfgE benchmark configs; 3)
+  static const bool runtime_views = [] {  // DAMVS_WARP_RUNTIME_VIEWS=1: the runtime view loop for N = 5 too
+    const char* v = getenv("DAMVS_WARP_RUNTIME_VIEWS");
+    return v && v[0] == '1';
+  }();
+  const bool pipe = C <= 16 && !no_pipe && a.N >= 3 && (a.N - 1) % 2 == 0;
+  if (pipe && a.N == 5 && !runtime_views)
     hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 4>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
+  else if (pipe)
+    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, -1>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
   else
     hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 0>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
 }
