@@ -304,16 +304,25 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
     const char* v = getenv("DAMVS_WARP_NO_PIPE");
     return v && v[0] == '1';
   }();
-  // view pipeline: unrolled for N = 5 (the DTU default), a runtime view loop for any other odd N (7, 11: the
-  // cfgD / cfgE benchmark configs; 3)
+  // view pipeline: unrolled for N = 5 (the DTU default) at 16 channels (stage 2; A/B: 2.29 against 2.37 ms, while
+  // stage 3 runs 1.47 against 1.50 ms on the runtime loop), a runtime view loop for any other odd
+  // N (7, 11: the cfgD / cfgE benchmark configs; 3) and for 32 channels (the unrolled form needs 360 registers)
   static const bool runtime_views = [] {  // DAMVS_WARP_RUNTIME_VIEWS=1: the runtime view loop for N = 5 too
     const char* v = getenv("DAMVS_WARP_RUNTIME_VIEWS");
     return v && v[0] == '1';
   }();
-  const bool pipe = C <= 16 && !no_pipe && a.N >= 3 && (a.N - 1) % 2 == 0;
-  if (pipe && a.N == 5 && !runtime_views)
-    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 4>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
-  else if (pipe)
+  static const bool pipe32 = [] {  // DAMVS_WARP_PIPE32=0: 32-channel maps (stage 1) on the generic view loop
+    const char* v = getenv("DAMVS_WARP_PIPE32");
+    return !(v && v[0] == '0');
+  }();
+  const bool pipe = (C <= 16 || pipe32) && !no_pipe && a.N >= 3 && (a.N - 1) % 2 == 0;
+  if constexpr (C == 16) {
+    if (pipe && a.N == 5 && !runtime_views) {
+      hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 4>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
+      return;
+    }
+  }
+  if (pipe)
     hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, -1>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
   else
     hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 0>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
