@@ -560,3 +560,43 @@ def test_stage_odd_batch_matches_per_sample(s, D, H, W):
         assert torch.equal(l1, logits[b:b + 1]), b
         d1 = eng.forward(one, cuda(P[b:b + 1]), cuda(hyps[b:b + 1]))[0]
         assert torch.equal(d1[0], depth[b]), b
+
+
+_WARP_VIEWS_SCRIPT = r"""
+import sys, torch
+sys.path[:0] = [sys.argv[2], sys.argv[2] + "/tests"]
+from common import model_state, depthnet_inputs
+from damvsnet_amd.cascade import CascadeMVSNet
+from damvsnet_amd.engine import StageEngine
+net = CascadeMVSNet(ndepths=[48, 32, 8])
+net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+feats, P, hyps = depthnet_inputs(B=2, N=5, H=40, W=72, D=8, stage_idx=1, C=16)
+eng = StageEngine(net.cost_regularization[1], net.DepthNet.weight_net[1], "adaptive", torch.bfloat16, torch.device("cuda"))
+nhwc = [f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).cuda() for f in feats]
+torch.save(eng.warp_aggregate(nhwc, P.cuda(), hyps.cuda()).cpu(), sys.argv[1])
+"""
+
+
+def test_warp_runtime_view_loop_matches_unrolled(tmp_path):
+    """The warp's runtime view loop (rays recomputed per view from the cameras; N = 3, 7, 11 and every 8 / 32-channel
+    map) against the unrolled N = 5 form with hoisted rays (16 channels), bitwise: the same expressions give the same
+    sampling coordinates. The runtime loop is forced for N = 5 in a child process (DAMVS_WARP_RUNTIME_VIEWS=1 is read
+    once per process)."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = str(tmp_path / "vol_runtime.pt")
+    env = dict(os.environ, DAMVS_WARP_RUNTIME_VIEWS="1")
+    subprocess.run([sys.executable, "-c", _WARP_VIEWS_SCRIPT, out, repo], env=env, check=True, timeout=200)
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    feats, P, hyps = depthnet_inputs(B=2, N=5, H=40, W=72, D=8, stage_idx=1, C=16)
+    eng = StageEngine(net.cost_regularization[1], net.DepthNet.weight_net[1], "adaptive", torch.bfloat16,
+                      torch.device(DEV))
+    nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats]
+    unrolled = eng.warp_aggregate(nhwc, cuda(P), cuda(hyps)).cpu()
+    runtime = torch.load(out, weights_only=True)
+    assert torch.equal(unrolled, runtime)
