@@ -220,7 +220,7 @@ def warp_roofline(net, imgs, proj, dv, stage, dtype, iters=20):
     """
     from damvsnet_amd import _capi
     from damvsnet_amd.depthnet import to_nhwc
-    from damvsnet_amd.engine import hypotheses, proj_prepare, block_channels
+    from damvsnet_amd.engine import hypotheses, proj_prepare, block_channels, warp_blocked
     name = "stage%d" % (stage + 1)
     B, N, _, H, W = imgs.shape
     scale = (4, 2, 1)[stage]
@@ -228,7 +228,7 @@ def warp_roofline(net, imgs, proj, dv, stage, dtype, iters=20):
         feats = net.extract_features(imgs)
         fs = [f[name].to(dtype).contiguous() if net.frontend_impl == "hip" else to_nhwc(f[name], dtype)
               for f in feats]
-        blocked = fs[0].shape[-1] * fs[0].element_size() > 16
+        blocked = warp_blocked(fs[0].shape[-1], fs[0].element_size())
         fb = block_channels(fs) if blocked else fs
         layout = _capi.DAMVS_LAYOUT_CBLOCK if blocked else _capi.DAMVS_LAYOUT_NHWC
         hyps = hypotheses(dv, net.ndepths[stage], H, W, scale)
@@ -255,6 +255,15 @@ def pmc_traffic(config, batch, kernel_substr="warp_aggregate"):
     (profiles/<round>/pmc_*.json, produced by tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE,
     the gfx950 correction of MI355X_MICROARCH.md), or None."""
     import glob
+    # preferred: the kernel as the pipeline runs it (tools/pmc_warp_inpipe.py: FETCH_SIZE x2 + WRITE_SIZE of the
+    # in-pipeline launches, whose per-pixel hypotheses scatter the gathers far more than kbench's)
+    inpipe = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_warp_inpipe_%s_b%d.json" % (config, batch))))
+    if inpipe and kernel_substr == "warp_aggregate":
+        with open(inpipe[-1]) as f:
+            p = json.load(f)["summary"]["pipeline"]
+        if "fetch_bytes_x2_gfx950" in p and "write_bytes" in p:
+            return {"bytes": int(p["fetch_bytes_x2_gfx950"] + p["write_bytes"]),
+                    "source": os.path.relpath(inpipe[-1], REPO) + " (in-pipeline launches)"}
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_%s_%s_b%d.json" % (kernel_substr, config, batch))))
     if not files:
         return None

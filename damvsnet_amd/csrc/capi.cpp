@@ -260,7 +260,18 @@ struct Workspace {
 };
 
 // c[i] holds conv_i's output for i = 0..6 (conv7/9/11 accumulate in place into c4/c2/c0).
-bool feat_needs_blocking(const damvs_stage* st) { return st->C * (st->dtype == DAMVS_BF16 ? 2 : 4) > 16; }
+// Channel-blocked copies of the feature maps for the warp's gathers when a pixel is wider than 32 bytes (stage 1:
+// 32 bf16 channels). 32-byte pixels (stage 2: 16 bf16 channels) are gathered NHWC in place: with the pipeline's
+// per-pixel hypotheses a bilinear corner then costs one cache line instead of one per 16-byte chunk (in-pipeline
+// stage-2 warp 2.25 -> 2.08 ms, and no repack launch), while at 64 bytes the blocked form stays ahead (1.21 against
+// 1.65 ms). DAMVS_WARP_BLOCK32=1 (A/B) blocks 32-byte pixels too. engine.warp_blocked is the Python mirror.
+bool feat_needs_blocking(const damvs_stage* st) {
+  static const int limit = [] {
+    const char* v = getenv("DAMVS_WARP_BLOCK32");
+    return v && v[0] == '1' ? 16 : 32;
+  }();
+  return st->C * (st->dtype == DAMVS_BF16 ? 2 : 4) > limit;
+}
 
 Workspace plan_ws(const damvs_stage* st, int B, int N, int D, int h, int w) {
   const size_t es = st->dtype == DAMVS_BF16 ? 2 : 4;

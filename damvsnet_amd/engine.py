@@ -7,6 +7,7 @@ its current stream; all compute of the hot path happens in libdamvs.so.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -187,6 +188,13 @@ def proj_prepare(proj):
     rt = torch.empty(B, N - 1, 12, device=proj.device, dtype=torch.float32)
     check(lib.damvs_proj_prepare(_capi.stream_ptr(proj.device), B, N, ptr(proj), ptr(rt)))
     return rt
+
+
+def warp_blocked(C, element_size):
+    """Whether the warp gathers channel-blocked copies of C-channel feature maps (pixels wider than 32 bytes;
+    DAMVS_WARP_BLOCK32=1: wider than 16) -- the C library's feat_needs_blocking (capi.cpp)."""
+    limit = 16 if os.environ.get("DAMVS_WARP_BLOCK32", "") == "1" else 32
+    return C * element_size > limit
 
 
 def block_channels(feats_nhwc):

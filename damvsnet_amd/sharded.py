@@ -281,7 +281,7 @@ class DepthShardedDepthNet:
         self.net, self.comm, self.warp, self.want_prob, self.hook = net, comm, warp, want_prob, hook
 
     def __call__(self, stage_idx, feats_nhwc, proj_matrices, depth_values, cost_regularization):
-        from .engine import block_channels, proj_prepare
+        from .engine import block_channels, proj_prepare, warp_blocked
         dn = self.net.DepthNet
         dev = depth_values.device
         eng = dn.engine(stage_idx, cost_regularization, dev)
@@ -289,7 +289,7 @@ class DepthShardedDepthNet:
                  for f in feats_nhwc]
         B, h, w, C = feats[0].shape
         layout = _capi.DAMVS_LAYOUT_NHWC
-        if C * feats[0].element_size() > 16:
+        if warp_blocked(C, feats[0].element_size()):
             feats, layout = block_channels(feats), _capi.DAMVS_LAYOUT_CBLOCK
         hyps = depth_values.float().contiguous()
         rt = proj_prepare(proj_matrices.float().contiguous())

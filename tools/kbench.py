@@ -45,11 +45,11 @@ def main():
         pv = 5 + 20 * torch.rand(B, H // ps, W // ps, device=dev, generator=g)
         hyps = hypotheses(dv, D, H, W, scale, pd, pv)
     from damvsnet_amd import _capi
-    from damvsnet_amd.engine import block_channels, proj_prepare
+    from damvsnet_amd.engine import block_channels, proj_prepare, warp_blocked
     eng = net.DepthNet.engine(s, net.cost_regularization[s], dev)
     P = proj["stage%d" % (s + 1)]
     rt = proj_prepare(P)
-    blocked = C * feats[0].element_size() > 16
+    blocked = warp_blocked(C, feats[0].element_size())
     fb = block_channels(feats) if blocked else feats
     layout = _capi.DAMVS_LAYOUT_CBLOCK if blocked else _capi.DAMVS_LAYOUT_NHWC
     vol = eng.warp_aggregate(fb, None, hyps, rt=rt, layout=layout)
