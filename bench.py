@@ -213,7 +213,8 @@ def latency_b1(net, imgs, proj, dv, ins, steps=10):
 
 def warp_roofline(net, imgs, proj, dv, stage, dtype, iters=20):
     """Time the product-path fused warp+aggregation kernel of one stage alone (HIP events on the
-    stream it is launched on): channel-blocked features and cameras prepared outside the loop.
+    stream it is launched on): features in the stage's gather layout, cameras and the pipeline's hypotheses
+    (stage >= 1: refined from the previous stage's depth and variance) prepared outside the loop.
 
     Algorithmic bytes per launch: e * (N*C*h*w [features, read
     once] + C*D*h*w [volume write]) + 4*D*h*w [fp32 hypotheses] + 4*B*(N-1)*12 [cameras].
@@ -231,7 +232,11 @@ def warp_roofline(net, imgs, proj, dv, stage, dtype, iters=20):
         blocked = warp_blocked(fs[0].shape[-1], fs[0].element_size())
         fb = block_channels(fs) if blocked else fs
         layout = _capi.DAMVS_LAYOUT_CBLOCK if blocked else _capi.DAMVS_LAYOUT_NHWC
-        hyps = hypotheses(dv, net.ndepths[stage], H, W, scale)
+        if stage == 0:
+            hyps = hypotheses(dv, net.ndepths[stage], H, W, scale)
+        else:  # the pipeline's hypotheses: refined around the previous stage's depth by its uncertainty
+            prev = net(imgs, proj, dv)["stage%d" % stage]
+            hyps = hypotheses(dv, net.ndepths[stage], H, W, scale, prev["depth"], prev["variance"])
         rt = proj_prepare(proj[name])
         eng = net.DepthNet.engine(stage, net.cost_regularization[stage], imgs.device)
         eng.warp_aggregate(fb, None, hyps, rt=rt, layout=layout)
