@@ -182,12 +182,25 @@ def sharded_latency(net, H, W, N, device, comm=None, emulate=1, warp="depth", st
             torch.distributed.barrier()
         el = time.perf_counter() - t0
         timer = StageTimer()
-        run_all(timer)
+        res = {}
+
+        def checked(c, hook=None):  # one sharded forward, every stage bitwise against the unsharded one
+            out = step(c, hook)
+            if c.rank == 0:
+                ref = net(imgs, proj, dv, ins)
+                res["bitwise_vs_unsharded"] = all(
+                    torch.equal(out[st][k], ref[st][k]) for st in ("stage1", "stage2", "stage3")
+                    for k in ("depth", "photometric_confidence", "variance", "prob_volume"))
+        if comm is not None:
+            checked(comm, timer)
+        else:
+            ThreadGroup(emulate).run(lambda c: checked(c, timer if c.rank == 0 else None))
         torch.cuda.synchronize()
     from damvsnet_amd.dist import max_over_ranks
     el = max_over_ranks(el, device=device) if comm is not None else el
     return {"ms_per_map": round(el / steps * 1e3, 3), "ranks": world, "warp": warp,
             "transport": "rccl" if comm is not None else "threads on one GPU (rehearsal)",
+            "bitwise_vs_unsharded": res.get("bitwise_vs_unsharded"),
             "phases_rank0_ms": {k: round(sum(v), 3) for k, v in timer.per_phase_ms().items()}}
 
 
@@ -331,8 +344,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        import datetime
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # a finite collective timeout: a rank that fails inside the depth-sharded block cannot leave its peers
+        # waiting in a P2P exchange forever (the NCCL watchdog aborts the group instead)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                             timeout=datetime.timedelta(seconds=300))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
@@ -393,10 +410,18 @@ def main():
     shard_block = None
     if world > 1 and not args.no_shard_latency:  # every rank takes part
         from damvsnet_amd.sharded import TorchComm
+        err = None
         try:
             shard_block = sharded_latency(net, H, W, N, device, comm=TorchComm())
         except Exception as ex:  # reported, never fatal for the throughput line
-            shard_block = {"error": repr(ex)[:300]}
+            err = repr(ex)[:300]
+        # every rank leaves the block knowing whether any rank failed (a failure after the last exchange would
+        # otherwise go unnoticed by the peers); a failure before an exchange ends at the collective timeout
+        flag = torch.tensor([1 if err else 0], device=device)
+        torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.SUM)
+        if int(flag.item()):
+            shard_block = {"error": err or "failed on %d other rank(s)" % int(flag.item()),
+                           "failed_ranks": int(flag.item())}
 
     result = None
     if rank == 0:

@@ -58,6 +58,7 @@ class DamvsFusionCams(ctypes.Structure):
 SIGNATURES = (
     ("damvs_abi_version", c_int, ()),
     ("damvs_last_error_string", ctypes.c_char_p, ()),
+    ("damvs_build_id", ctypes.c_char_p, ()),
     ("damvs_stage_create", c_int, (ctypes.POINTER(DamvsCostregParams), ctypes.POINTER(DamvsAggweightParams), c_int,
                                    c_int, ctypes.POINTER(c_void_p))),
     ("damvs_stage_destroy", c_int, (c_void_p,)),
@@ -73,6 +74,7 @@ SIGNATURES = (
                                 c_void_p)),
     ("damvs_warp_aggregate", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_void_p),
                                      c_int, c_void_p, c_void_p, c_void_p)),
+    ("damvs_warp_feat_blocked", c_int, (c_int, c_int)),
     ("damvs_block_channels", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_void_p),
                                      ctypes.POINTER(c_void_p))),
     ("damvs_costreg_logits", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t,
@@ -129,6 +131,13 @@ def load_library(path: str = LIB_PATH):
         fn.argtypes = list(args)
     if lib.damvs_abi_version() != 1:
         raise RuntimeError("libdamvs ABI mismatch")
+    if os.path.abspath(path) == os.path.abspath(os.path.join(_HERE, "libdamvs.so")):
+        # the in-tree library must be the build of the sources beside it (A/B builds through DAMVS_LIB are exempt)
+        from .build import source_hash
+        got, want = lib.damvs_build_id().decode(), source_hash()
+        if got != want:
+            raise RuntimeError("libdamvs.so is stale: built from sources %s, the tree holds %s — rebuild with "
+                               "`python -m damvsnet_amd.build`" % (got, want))
     _lib = lib
     return lib
 

@@ -1,13 +1,18 @@
 """Build libdamvs.so in-tree with hipcc for gfx950 (no CMake, no JIT cache).
 
 ``python -m damvsnet_amd.build`` or ``damvsnet_amd.build.build()``. Objects are compiled in
-parallel and linked into ``damvsnet_amd/libdamvs.so``; a rebuild is skipped when the library
-is newer than every source and header.
+parallel and linked into ``damvsnet_amd/libdamvs.so``. The library carries the sha256 of the sources,
+headers and compiler flags it was built from (``damvs_build_id()``, passed as -DDAMVS_BUILD_ID); a rebuild
+is skipped only when that stamp (kept beside the library in ``libdamvs.so.build_id``) equals the hash of the
+tree, and ``_capi.load_library`` refuses an in-tree library whose embedded stamp differs from the sources
+beside it. So the library that runs is provably the build of the sources that travel with it (file times
+play no part: a snapshot copied to another machine keeps the check meaningful).
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -17,6 +22,7 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIB = os.path.join(PKG, "libdamvs.so")
+STAMP = LIB + ".build_id"
 OBJ = os.path.join(PKG, "build_obj")
 ARCH = os.environ.get("DAMVS_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -29,18 +35,38 @@ def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
-def _stale():
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    deps = sources() + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
-    return any(os.path.getmtime(p) > t for p in deps)
+def _inputs():
+    return sources() + sorted(glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h")))
 
 
-def _compile(src):
+def source_hash() -> str:
+    """First 16 hex digits of sha256 over (path relative to the repo, contents) of every source and header, plus
+    the compiler flags that do not depend on where the repo lives."""
+    h = hashlib.sha256()
+    for p in _inputs():
+        h.update(os.path.relpath(p, REPO).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    h.update(" ".join(f for f in CFLAGS if not f.startswith("-I")).encode())
+    return h.hexdigest()[:16]
+
+
+def stamp() -> str | None:
+    try:
+        with open(STAMP) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _stale(want: str) -> bool:
+    return not os.path.exists(LIB) or stamp() != want
+
+
+def _compile(src, build_id):
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
-    lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "hip"]
-    cmd = [HIPCC] + CFLAGS + lang + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + CFLAGS + ['-DDAMVS_BUILD_ID="%s"' % build_id, "-x", "hip", "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (src, " ".join(cmd), r.stderr))
@@ -48,12 +74,15 @@ def _compile(src):
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+    want = source_hash()
+    if not force and not _stale(want):
+        if verbose:
+            print("libdamvs.so up to date: build id %s == sources %s" % (stamp(), want), file=sys.stderr)
         return LIB
     os.makedirs(OBJ, exist_ok=True)
     srcs = sources()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        results = list(ex.map(_compile, srcs))
+        results = list(ex.map(lambda s: _compile(s, want), srcs))
     objs = [o for o, _ in results]
     if verbose:
         for (_, err), s in zip(results, srcs):
@@ -65,6 +94,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if r.returncode != 0:
         raise RuntimeError("link failed:\n%s\n%s" % (" ".join(cmd), r.stderr))
     os.replace(tmp, LIB)
+    with open(STAMP, "w") as f:
+        f.write(want + "\n")
+    if verbose:
+        print("libdamvs.so built from sources %s" % want, file=sys.stderr)
     return LIB
 
 

@@ -264,14 +264,16 @@ struct Workspace {
 // 32 bf16 channels). 32-byte pixels (stage 2: 16 bf16 channels) are gathered NHWC in place: with the pipeline's
 // per-pixel hypotheses a bilinear corner then costs one cache line instead of one per 16-byte chunk (in-pipeline
 // stage-2 warp 2.25 -> 2.08 ms, and no repack launch), while at 64 bytes the blocked form stays ahead (1.21 against
-// 1.65 ms). DAMVS_WARP_BLOCK32=1 (A/B) blocks 32-byte pixels too. engine.warp_blocked is the Python mirror.
-bool feat_needs_blocking(const damvs_stage* st) {
+// 1.65 ms). DAMVS_WARP_BLOCK32=1 (A/B) blocks 32-byte pixels too; read once per process. damvs_warp_feat_blocked
+// exports the decision (engine.warp_blocked asks it, so Python and the stage forward always agree).
+bool feat_blocked(int dtype, int C) {
   static const int limit = [] {
     const char* v = getenv("DAMVS_WARP_BLOCK32");
     return v && v[0] == '1' ? 16 : 32;
   }();
-  return st->C * (st->dtype == DAMVS_BF16 ? 2 : 4) > limit;
+  return C * (dtype == DAMVS_BF16 ? 2 : 4) > limit;
 }
+bool feat_needs_blocking(const damvs_stage* st) { return feat_blocked(st->dtype, st->C); }
 
 Workspace plan_ws(const damvs_stage* st, int B, int N, int D, int h, int w) {
   const size_t es = st->dtype == DAMVS_BF16 ? 2 : 4;
@@ -411,6 +413,11 @@ constexpr int kLayerLevels[10][2] = {{0, 0}, {0, 1}, {1, 1}, {1, 2}, {2, 2}, {2,
 extern "C" {
 
 int damvs_abi_version(void) { return DAMVS_ABI_VERSION; }
+
+#ifndef DAMVS_BUILD_ID
+#define DAMVS_BUILD_ID "unstamped"
+#endif
+const char* damvs_build_id(void) { return DAMVS_BUILD_ID; }
 
 const char* damvs_last_error_string(void) { return g_err.c_str(); }
 
@@ -647,6 +654,12 @@ int damvs_warp_aggregate(const damvs_stage* st, void* stream, int B, int N, int 
   return hip_check(launch_warp_aggregate(reinterpret_cast<hipStream_t>(stream), st->dtype, st->mode, a,
                                          layout == DAMVS_LAYOUT_CBLOCK),
                    "warp_aggregate launch");
+}
+
+int damvs_warp_feat_blocked(int dtype, int C) {
+  if (dtype != DAMVS_F32 && dtype != DAMVS_BF16) return fail(DAMVS_E_DTYPE, "dtype %d unsupported", dtype);
+  if (C < 1) return fail(DAMVS_E_SHAPE, "C %d", C);
+  return feat_blocked(dtype, C) ? 1 : 0;
 }
 
 int damvs_block_channels(void* stream, int dtype, int N, int B, int h, int w, int C, const void* const* src,

@@ -187,4 +187,37 @@ __device__ __forceinline__ void stage_chunks(Raw* lds, F&& load) {
   }
 }
 
+
+// Diagnostic builds only (-DDAMVS_DIAG, tools/build_variant.sh; never the product library): a per-translation-unit
+// record buffer that kernels append to (vector atomics on global memory) and damvs_diag_take_<unit>() reads and
+// clears from the host. A record is 8 words: kind, block, index, observed bits, expected bits, HW_ID, LDS_ALLOC,
+// XCC_ID (the last three from s_getreg: the CU / SIMD / wave slot, the LDS allocation the hardware gave the workgroup
+// and the XCD it runs on).
+#ifdef DAMVS_DIAG
+constexpr int kDiagRecords = 64;
+static __device__ unsigned g_diag[8 + 8 * kDiagRecords];
+__device__ __forceinline__ void diag_record(unsigned kind, unsigned idx, unsigned seen, unsigned want) {
+  const unsigned slot = atomicAdd(&g_diag[0], 1u);
+  if (slot >= (unsigned)kDiagRecords) return;
+  unsigned* r = g_diag + 8 + 8 * slot;
+  r[0] = kind;
+  r[1] = blockIdx.x;
+  r[2] = idx;
+  r[3] = seen;
+  r[4] = want;
+  r[5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+  r[6] = __builtin_amdgcn_s_getreg((31 << 11) | 6);   // LDS_ALLOC
+  r[7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+}
+#define DAMVS_DIAG_EXPORT(unit)                                                              \
+  extern "C" int damvs_diag_take_##unit(unsigned* host, int nwords) {                        \
+    const size_t n = (size_t)(nwords < (int)(sizeof(damvs::g_diag) / 4) ? nwords : sizeof(damvs::g_diag) / 4); \
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(damvs::g_diag), n * 4, 0, hipMemcpyDeviceToHost) != hipSuccess) \
+      return -4;                                                                             \
+    static const unsigned zero[8 + 8 * damvs::kDiagRecords] = {0};                                   \
+    return hipMemcpyToSymbol(HIP_SYMBOL(damvs::g_diag), zero, sizeof(zero), 0, hipMemcpyHostToDevice) == hipSuccess \
+               ? 0 : -4;                                                                     \
+  }
+#endif
+
 }  // namespace damvs

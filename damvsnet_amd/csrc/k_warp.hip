@@ -19,9 +19,50 @@
 #include "damvs_device.h"
 
 
+// Diagnostic variants (DIAGNOSTIC builds only, tools/diag_streams.py; the product is always 0 / 0):
+// DAMVS_DIAG_WARP_LDS_CAMS = 1 stages the cameras in LDS as round 2 first did and, with -DDAMVS_DIAG, records every
+// camera word whose LDS copy differs from the global cameras right after the barrier and again after the depth walk;
+// DAMVS_DIAG_WARP_NT = 1 writes the volume with nontemporal stores.
+#ifndef DAMVS_DIAG_WARP_LDS_CAMS
+#define DAMVS_DIAG_WARP_LDS_CAMS 0
+#endif
+#ifndef DAMVS_DIAG_WARP_NT
+#define DAMVS_DIAG_WARP_NT 0
+#endif
+
 namespace damvs {
 
 namespace {
+
+#if DAMVS_DIAG_WARP_LDS_CAMS && defined(DAMVS_DIAG)
+__device__ __forceinline__ void diag_check_cams(const float* s_cam, const float* gcam, int n, unsigned kind) {
+  if ((int)threadIdx.x < n) {
+    const unsigned seen = __float_as_uint(reinterpret_cast<const volatile float*>(s_cam)[threadIdx.x]);
+    const unsigned want = __float_as_uint(gcam[threadIdx.x]);
+    if (seen != want) diag_record(kind, threadIdx.x, seen, want);
+  }
+}
+#endif
+
+template <typename T, int C>
+__device__ __forceinline__ void store_vol(T* p, const float* v) {
+#if DAMVS_DIAG_WARP_NT
+#pragma unroll
+  for (int i = 0; i < C; i += Stor<T>::E) {
+    uint32_t w[4];
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] = (uint32_t)f2bf(v[i + 2 * k]) | ((uint32_t)f2bf(v[i + 2 * k + 1]) << 16);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] = __float_as_uint(v[i + k]);
+    }
+    __builtin_nontemporal_store((v4u32_t){w[0], w[1], w[2], w[3]}, reinterpret_cast<v4u32_t*>(p + i));
+  }
+#else
+  store_vec<T, C>(p, v);
+#endif
+}
 
 // One 16-byte storage record -> E floats.
 template <typename T> struct Rec16;
@@ -102,7 +143,18 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
   // kernel argument, i.e. scalar loads into SGPRs. (They were staged in LDS; with another kernel running
   // on a concurrent stream that copy came back altered in up to 76 of 80 launches — tools/streams_race_kernel.py
   // — and the scalar path needs neither LDS nor a barrier.)
+#if DAMVS_DIAG_WARP_LDS_CAMS
+  __shared__ __attribute__((aligned(16))) float s_cam[(kMaxViews - 1) * 12];
+  const float* gcam = cams + (size_t)b * (a.N - 1) * 12;
+  if ((int)threadIdx.x < (a.N - 1) * 12) s_cam[threadIdx.x] = gcam[threadIdx.x];
+  __syncthreads();
+#ifdef DAMVS_DIAG
+  diag_check_cams(s_cam, gcam, (a.N - 1) * 12, 1);
+#endif
+  const float* cam = s_cam;
+#else
   const float* __restrict__ cam = cams + (size_t)b * (a.N - 1) * 12;
+#endif
   const int p = pb * 256 + threadIdx.x;
   if (p >= ohw) return;
   const int yl = p / a.w, x = p - yl * a.w;
@@ -178,7 +230,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
 #pragma unroll
       for (int c = 0; c < C; ++c) o[c] = acc[c];
     }
-    store_vec<T, C>(reinterpret_cast<T*>(a.out) + vox_of(d) * C, o);
+    store_vol<T, C>(reinterpret_cast<T*>(a.out) + vox_of(d) * C, o);
   };
   auto init = [&](float* acc, float* sq) {
 #pragma unroll
@@ -296,6 +348,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
       finish(d, acc, sq);
     }
   }
+#if DAMVS_DIAG_WARP_LDS_CAMS && defined(DAMVS_DIAG)
+  diag_check_cams(s_cam, gcam, (a.N - 1) * 12, 2);
+#endif
 }
 
 template <typename T, int C, int MODE, bool BLK>
@@ -404,3 +459,7 @@ hipError_t launch_block_channels(hipStream_t s, int store, const FeatPtrs& src, 
 }
 
 }  // namespace damvs
+
+#ifdef DAMVS_DIAG
+DAMVS_DIAG_EXPORT(warp)
+#endif

@@ -7,11 +7,10 @@ train.py:492-496) — with NO collective on the data path. Collectives are used 
 a MAX of the per-rank elapsed time for benchmarking, and an optional gather of the finished
 (small) depth/confidence maps to one rank.
 
-Why not shard one depth map's cost volume over GPUs along D? The 3D U-Net
-couples neighbouring depth planes through three stride-2 levels, so a D-sharded volume must be
-all-gathered before regularisation; at cfgC stage 2 that is 485 MB (bf16) per map, ~0.5 ms over
-xGMI at ~1 TB/s per GPU — longer than the whole fused warp+aggregation it would parallelise
-(~0.6 ms on one GPU). See DESIGN.md "Multi-GPU".
+Latency (one depth map over several GPUs) is a separate mode: damvsnet_amd/sharded.py shards each stage's cost
+volume along the depth-hypothesis axis (north_star), re-shards it to row slabs for the U-Net (whose 3x3x3 kernels
+and stride-2 levels couple all planes) with one all-to-all, exchanges slab halos per layer and all-gathers the
+regressed rows. See DESIGN.md section 7 "Multi-GPU".
 """
 from __future__ import annotations
 

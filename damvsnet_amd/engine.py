@@ -7,7 +7,6 @@ its current stream; all compute of the hot path happens in libdamvs.so.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -191,10 +190,12 @@ def proj_prepare(proj):
 
 
 def warp_blocked(C, element_size):
-    """Whether the warp gathers channel-blocked copies of C-channel feature maps (pixels wider than 32 bytes;
-    DAMVS_WARP_BLOCK32=1: wider than 16) -- the C library's feat_needs_blocking (capi.cpp)."""
-    limit = 16 if os.environ.get("DAMVS_WARP_BLOCK32", "") == "1" else 32
-    return C * element_size > limit
+    """Whether damvs_stage_forward gathers channel-blocked copies of C-channel feature maps: the library's own
+    decision (damvs_warp_feat_blocked), so split-entry callers lay the maps out exactly as the stage forward does."""
+    lib = _capi.load_library()
+    r = lib.damvs_warp_feat_blocked(_capi.DAMVS_BF16 if element_size == 2 else _capi.DAMVS_F32, int(C))
+    check(r if r < 0 else 0)
+    return r == 1
 
 
 def block_channels(feats_nhwc):

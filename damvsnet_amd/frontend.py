@@ -1,9 +1,10 @@
 """2D front-end of the cascade: feature pyramid and geometry-aware reference-feature fusion.
 
-These produce the hot path's inputs; SURVEY.md section 8(f) row f1 ranks them as the next
-component to move onto hand-written kernels. In this round they run as PyTorch-ROCm
-(MIOpen) modules on the GPU, in channels-last memory so their output already has the
-NHWC layout the warp/aggregation kernel reads (no transpose at the boundary).
+These produce the hot path's inputs. The modules here own the parameters
+and the reference's state_dict keys; the computation runs on libdamvs's fused NHWC conv2d kernels
+(frontend_hip.py, BN folded by frontend_fold.py), whose outputs already have the NHWC layout the
+warp/aggregation kernel reads. ``frontend_impl="torch"`` keeps a PyTorch-ROCm (MIOpen) channels-last path
+for A/B comparisons only.
 
 The module trees reproduce the reference's ``state_dict`` keys exactly so that
 ``load_state_dict(torch.load(ckpt)['model'], strict=True)`` (test_uni.py:223-224) works:

@@ -15,8 +15,9 @@ Per stage (DepthNet.forward, models/cas_mvsnet.py:18-134), on rank r of P:
    whole-tensor kernel unchanged (damvs_costreg_layer); after every layer the halo rows are refreshed from the
    neighbouring slabs (P2P) and zeroed outside the image (the whole-image convolution's zero padding).
 4. Prob conv + softmax regression (models/cas_mvsnet.py:105-124) locally: the softmax is over D, per pixel.
-5. All-gather of the slabs' depth / confidence / variance rows (and prob volume): every rank then holds the
-   stage output, which the next stage's hypotheses and GeoFeatureFusion read whole.
+5. All-gather of the slabs' depth / confidence / variance rows (and prob volume), one collective
+   (all_gather_into_tensor over RCCL) of slabs padded to the tallest: every rank then holds the stage output, which
+   the next stage's hypotheses and GeoFeatureFusion read whole.
 
 ``warp="rows"`` builds each rank's haloed slab of the volume directly (damvs_warp_aggregate_rows) and skips the
 all-to-all: the same voxels, with redundant warp work on the halo rows instead of communication.
@@ -76,6 +77,12 @@ class Comm:
     def exchange(self, ops):
         raise NotImplementedError
 
+    def all_gather(self, t):
+        """Every rank's ``t`` (one shape on all ranks) as a list indexed by rank."""
+        outs = [torch.empty_like(t) for _ in range(self.world)]
+        self.exchange([(q, t, outs[q]) for q in range(self.world)])
+        return outs
+
 
 class TorchComm(Comm):
     """torch.distributed over the default group: batched isend/irecv (RCCL groups them into one launch; the
@@ -108,6 +115,16 @@ class TorchComm(Comm):
                 work.wait()
         for dst, src in back:
             dst.copy_(src)
+
+    def all_gather(self, t):
+        """One collective: all_gather_into_tensor (RCCL ring over xGMI) into a [world, ...] buffer; gloo gathers
+        host copies."""
+        dist = self._dist
+        t = t.contiguous()
+        src = t.cpu() if self._host and t.is_cuda else t
+        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=src.device)
+        dist.all_gather_into_tensor(out, src)  # ranks concatenated along dim 0
+        return [p.to(t.device) for p in out.chunk(self.world, 0)]
 
 
 class ThreadGroup:
@@ -261,11 +278,13 @@ def sharded_stage(comm: Comm, eng, feats, layout, rt, hyps, h: int, w: int, warp
     parts = [depth[:, None, core], conf[:, None, core], var[:, None, core]]
     if want_prob:
         parts.append(prob[:, :, core])
-    mine = torch.cat(parts, 1)  # [B][3 (+D)][rows][w]
-    K = mine.shape[1]
-    bufs = [torch.empty(B, K, ys[q + 1] - ys[q], w, device=dev, dtype=mine.dtype) for q in range(P)]
-    comm.exchange([(q, mine, bufs[q]) for q in range(P)])
-    full = torch.cat(bufs, 2)
+    # one all-gather of equal-size buffers (slabs differ by at most 8 rows: padded to the tallest)
+    rmax = max(ys[q + 1] - ys[q] for q in range(P))
+    K = 3 + (prob.shape[1] if want_prob else 0)
+    mine = torch.zeros(B, K, rmax, w, device=dev, dtype=depth.dtype)  # [B][3 (+D)][rows][w]
+    mine[:, :, :y1 - y0].copy_(torch.cat(parts, 1))
+    got = comm.all_gather(mine)
+    full = torch.cat([got[q][:, :, :ys[q + 1] - ys[q]] for q in range(P)], 2)
     depth, conf, var = full[:, 0].contiguous(), full[:, 1].contiguous(), full[:, 2].contiguous()
     prob = full[:, 3:].contiguous() if want_prob else None
     hook("end")

@@ -78,6 +78,10 @@ typedef struct damvs_stage damvs_stage;
 
 int damvs_abi_version(void);
 const char* damvs_last_error_string(void);
+/* Provenance: sha256 (hex, first 16 digits) of the sources, headers and compiler flags this library was built
+ * from (damvsnet_amd/build.py), "unstamped" for builds outside build.py. The Python binding compares it with the
+ * sources next to it and refuses a stale library. */
+const char* damvs_build_id(void);
 
 /* One cascade stage's weights (replaces DepthNet.weight_net[s] + cost_regularization[s],
  * models/cas_mvsnet.py:16,180-182). `aggw` may be NULL for DAMVS_AGG_VARIANCE. Uses the
@@ -130,6 +134,10 @@ int damvs_warp_aggregate(const damvs_stage* st, void* stream, int B, int N, int 
                          const void* const* feats, int layout, const float* rt, const float* hyps, void* volume);
 
 /* NHWC [B][h][w][C] -> DAMVS_LAYOUT_CBLOCK for N maps (src[v] -> dst[v], device buffers). */
+/* 1 if the stage forward gathers C-channel maps of this dtype from channel-blocked copies (damvs_block_channels:
+ * pixels wider than 32 bytes), 0 if it gathers the NHWC maps in place, negative on a bad argument. The split entry
+ * point damvs_warp_aggregate takes either layout; callers that mirror damvs_stage_forward ask here. */
+int damvs_warp_feat_blocked(int dtype, int C);
 int damvs_block_channels(void* stream, int dtype, int N, int B, int h, int w, int C, const void* const* src,
                          void* const* dst);
 

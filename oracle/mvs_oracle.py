@@ -317,10 +317,12 @@ STAGE_SCALE = (4, 2, 1)  # models/cas_mvsnet.py:154-164
 
 
 def cascade_forward(sd, imgs, proj_matrices, depth_values, ndepths=(48, 32, 8), agg_mode="adaptive",
-                    share_cr=False, arch_mode="fpn", warp_impl="grid_sample", stage_hook=None):
+                    share_cr=False, arch_mode="fpn", warp_impl="grid_sample", stage_hook=None, depthnet=None):
     """CascadeMVSNet.forward — models/cas_mvsnet.py:190-319 (inference, grad_method 'detach').
 
-    ``stage_hook(name)`` (optional) is called around the major phases for timing.
+    ``stage_hook(name)`` (optional) is called around the major phases for timing. ``depthnet`` (optional, tests
+    only) replaces depthnet_stage: called as depthnet(stage_idx, features, proj, hyps) -> the stage's output dict
+    (e.g. a depth-sharded stage, tests/test_sharded.py).
     Returns the reference's output dict: per-stage dicts plus stage-3 keys at top level.
     """
     hook = stage_hook or (lambda name: None)
@@ -341,7 +343,10 @@ def cascade_forward(sd, imgs, proj_matrices, depth_values, ndepths=(48, 32, 8), 
         hook(name + ".hypotheses")
         hyps = stage_hypotheses(s, depth_values, depth, var, nd, H, W, STAGE_SCALE[s])
         hook(name + ".depthnet")
-        out = depthnet_stage(s, fs, proj_matrices[name], hyps, sd, agg_mode, share_cr, warp_impl)
+        if depthnet is not None:
+            out = depthnet(s, fs, proj_matrices[name], hyps)
+        else:
+            out = depthnet_stage(s, fs, proj_matrices[name], hyps, sd, agg_mode, share_cr, warp_impl)
         depth, conf, var = out["depth"], out["photometric_confidence"], out["variance"]
         outputs[name] = out
         outputs.update(out)

@@ -30,6 +30,14 @@ def test_library_builds_and_exports_every_symbol():
     assert lib.damvs_abi_version() == 1
 
 
+def test_library_is_the_build_of_this_tree():
+    """The in-tree library embeds the hash of the sources it was compiled from; it must be this tree's."""
+    from damvsnet_amd import build, _capi
+    build.build()
+    lib = _capi.load_library()  # raises on a stale library
+    assert lib.damvs_build_id().decode() == build.source_hash() == build.stamp()
+
+
 def test_binding_covers_header():
     from damvsnet_amd import _capi
     bound = {name for name, _, _ in _capi.SIGNATURES}

@@ -156,6 +156,67 @@ def _gloo_worker(rank, world, port, warp, q):
         dist.destroy_process_group()
 
 
+def _cascade_case():
+    """A whole cascade (FeatureNet, GeoFeatureFusion, three stages 48/32/8) at 96 x 64, 3 views, float64."""
+    from common import forward_inputs
+    sd = model_state("forward_cfgB_640x512")
+    sd = {k: (v.to(F64) if torch.is_floating_point(v) else v) for k, v in sd.items()}
+    imgs, proj, dv, _ = forward_inputs(1, 3, 64, 96)
+    return sd, imgs.to(F64), {k: v.to(F64) for k, v in proj.items()}, dv.to(F64)
+
+
+def _cascade(sd, imgs, proj, dv, comm=None, warp="depth"):
+    """oracle.cascade_forward with every stage's DepthNet depth-sharded over ``comm`` (None: unsharded)."""
+    def stage(s, fs, P, hyps):
+        eng = CpuStageEngine(sd, s, "adaptive", fs, P)
+        d, c, v, p = S.sharded_stage(comm, eng, None, None, None, hyps.to(F64), hyps.shape[2], hyps.shape[3], warp=warp)
+        return {"depth": d, "photometric_confidence": c, "variance": v, "prob_volume": p, "depth_values": hyps}
+    with torch.no_grad():
+        return O.cascade_forward(sd, imgs, proj, dv, (48, 32, 8), "adaptive", warp_impl="gather",
+                                 depthnet=None if comm is None else stage)
+
+
+def _gloo_cascade_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        case = _cascade_case()
+        got = _cascade(*case, comm=S.TorchComm())
+        if rank == world - 1:
+            ref = _cascade(*case)
+            try:
+                for st in ("stage1", "stage2", "stage3"):
+                    # float64: the sharded U-Net's CPU GEMM blocking differs with the slab height, and the cascade
+                    # re-centres each stage on the previous depth, so summation-order noise grows stage by stage
+                    np.testing.assert_allclose(got[st]["depth"].numpy(), ref[st]["depth"].numpy(), rtol=1e-9)
+                    np.testing.assert_allclose(got[st]["prob_volume"].numpy(), ref[st]["prob_volume"].numpy(),
+                                               rtol=1e-7, atol=1e-10)
+                q.put(("ok", None))
+            except AssertionError as e:
+                q.put(("fail", str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_whole_cascade_every_stage_sharded():
+    """The whole cascade (front-end replicated, every stage's DepthNet depth-sharded over 2 gloo ranks) against the
+    unsharded float64 cascade: the all-to-all, halo exchanges and all-gather of all three stages, and the next
+    stage's hypotheses and GeoFeatureFusion reading the gathered maps."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_cascade_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(280)
+        assert p.exitcode == 0
+    status, msg = q.get(timeout=10)
+    assert status == "ok", msg
+
+
 @pytest.mark.timeout(180)
 @pytest.mark.parametrize("world,warp", [(2, "depth"), (3, "depth"), (3, "rows")])
 def test_gloo_world_matches_unsharded(world, warp):
