@@ -330,6 +330,8 @@ def main():
     ap.add_argument("--streams", type=int, default=2,
                     help="sub-batches of the per-GPU batch on concurrent HIP streams in the timed steps "
                          "(bitwise the one-stream result; ms_per_stage / rooflines come from a one-stream pass)")
+    ap.add_argument("--dtype", choices=["bf16", "f32"], default=None,
+                    help="override the config's compute dtype (cfgC is bf16 in BASELINE.json; f32 = the parity path)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--frontend", default="hip", choices=["hip", "torch"], help="2D front-end implementation")
     ap.add_argument("--cpu-budget", type=float, default=60.0)
@@ -354,6 +356,9 @@ def main():
     torch.cuda.set_device(device)
 
     H, W, N, nd, dtype, desc = CONFIGS[args.config]
+    if args.dtype:
+        dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+        desc = desc.rsplit(",", 1)[0] + ", " + args.dtype
     dname = "bf16" if dtype == torch.bfloat16 else "f32"
     net, _ = build_model(nd, dtype, device, args.frontend)
     if args.shard:
@@ -431,7 +436,8 @@ def main():
         iso_ms, alg = warp_roofline(net, imgs, proj, dv, 1, dtype)
         pipe_ms = per_stage[1]["warp"]
         achieved = alg / (pipe_ms * 1e-3) / 1e9
-        tr = pmc_traffic(args.config, args.batch)
+        native = dtype == CONFIGS[args.config][4]  # committed PMC profiles are of the config's own dtype
+        tr = pmc_traffic(args.config, args.batch) if native else None
         result = {
             "metric": "depth maps/sec (full CascadeMVSNet forward)",
             "value": round(maps / elapsed, 4),
@@ -463,7 +469,7 @@ def main():
                          "isolated_ms_per_launch": round(iso_ms, 4),
                          "isolated_frac": round(alg / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "hot_path_roofline": hp,
-            "mfma_utilisation": pmc_mfma(args.config, args.batch),
+            "mfma_utilisation": pmc_mfma(args.config, args.batch) if native else None,
         }
         if shard_block is not None:
             result["depth_sharded"] = shard_block

@@ -271,7 +271,15 @@ bool feat_blocked(int dtype, int C) {
     const char* v = getenv("DAMVS_WARP_BLOCK32");
     return v && v[0] == '1' ? 16 : 32;
   }();
-  return C * (dtype == DAMVS_BF16 ? 2 : 4) > limit;
+  static const bool split_off = [] {  // the launcher's switch (k_warp.hip split_lanes): read the same variable
+    const char* v = getenv("DAMVS_WARP_SPLIT");
+    return v && v[0] == '0';
+  }();
+  const int bytes = C * (dtype == DAMVS_BF16 ? 2 : 4);
+  // 32- and 64-byte pixels go to the channel-split warp, which gathers the NHWC maps in place (a lane quad reads a
+  // 64-byte pixel in one instruction, where the blocked layout needs one line per 16-byte chunk)
+  if (!split_off && limit == 32 && (bytes == 32 || bytes == 64)) return false;
+  return bytes > limit;
 }
 bool feat_needs_blocking(const damvs_stage* st) { return feat_blocked(st->dtype, st->C); }
 

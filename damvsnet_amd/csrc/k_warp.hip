@@ -29,18 +29,26 @@
 #ifndef DAMVS_DIAG_WARP_NT
 #define DAMVS_DIAG_WARP_NT 0
 #endif
+// DAMVS_DIAG_WARP_FULLWAIT = 1: s_waitcnt vmcnt(0) before every view reduction of the pipelined loop (every load in
+// flight has landed before any sample register is read)
+#ifndef DAMVS_DIAG_WARP_FULLWAIT
+#define DAMVS_DIAG_WARP_FULLWAIT 0
+#endif
 
 namespace damvs {
 
 namespace {
 
 #if DAMVS_DIAG_WARP_LDS_CAMS && defined(DAMVS_DIAG)
+// every thread compares all n camera words of the LDS copy with global memory; one record per mismatching thread
 __device__ __forceinline__ void diag_check_cams(const float* s_cam, const float* gcam, int n, unsigned kind) {
-  if ((int)threadIdx.x < n) {
-    const unsigned seen = __float_as_uint(reinterpret_cast<const volatile float*>(s_cam)[threadIdx.x]);
-    const unsigned want = __float_as_uint(gcam[threadIdx.x]);
-    if (seen != want) diag_record(kind, threadIdx.x, seen, want);
+  unsigned bad = 0, first = 0, seen0 = 0, want0 = 0;
+  for (int i = 0; i < n; ++i) {
+    const unsigned seen = __float_as_uint(reinterpret_cast<const volatile float*>(s_cam)[i]);
+    const unsigned want = __float_as_uint(gcam[i]);
+    if (seen != want && !bad++) { first = i; seen0 = seen; want0 = want; }
   }
+  if (bad) diag_record(kind, (threadIdx.x << 8) | first, seen0, want0);
 }
 #endif
 
@@ -133,9 +141,25 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
   constexpr int E = Stor<T>::E, NQ = C / E;
   static_assert(NVC % 2 == 0 || NVC < 0, "the view pipeline alternates two register sets");
   const int hw = a.h * a.w, ohw = a.rows * a.w;  // feature-map plane, computed rows (y0 .. y0 + rows - 1)
-  const int nblk = npix_blocks * ndchunks * a.B;
-  const int bid = blockIdx.x, q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
-  int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;  // bijective XCD remap
+  // Block order (dispatch position bid runs on XCD bid % 8). order 0: XCD-contiguous over the whole grid (XCD k
+  // takes the k-th eighth of (batch, pixel block, depth chunk)). order 1: batch-synchronous bands -- the grid is
+  // dispatched one batch element at a time and within it XCD k takes the k-th eighth, so every XCD works in its
+  // own band of the SAME batch element (one element's source maps hot in the Infinity Cache instead of B / 2
+  // elements'). order 2: plain dispatch order (consecutive blocks on different XCDs).
+  const int bid = blockIdx.x;
+  auto xcd_remap = [](int i, int n) {  // bijective on [0, n): XCD i % 8 gets the (i % 8)-th contiguous eighth
+    const int q8 = n / 8, r8 = n % 8, x = i % 8;
+    return (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + i / 8;
+  };
+  int L;
+  if (a.order == 1) {
+    const int nb = npix_blocks * ndchunks;
+    L = (bid / nb) * nb + xcd_remap(bid % nb, nb);
+  } else if (a.order == 2) {
+    L = bid;
+  } else {
+    L = xcd_remap(bid, npix_blocks * ndchunks * a.B);
+  }
   const int dc = L % ndchunks; L /= ndchunks;
   const int pb = L % npix_blocks;
   const int b = L / npix_blocks;
@@ -151,7 +175,20 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
 #ifdef DAMVS_DIAG
   diag_check_cams(s_cam, gcam, (a.N - 1) * 12, 1);
 #endif
+#if DAMVS_DIAG_WARP_LDS_CAMS == 2
+  // the cameras read back one word at a time (ds_read_b32: an opaque per-read index keeps the load-store optimiser
+  // from merging them into ds_read_b64 / b128) into a private copy
+  float cam_w[(kMaxViews - 1) * 12];
+#pragma unroll
+  for (int i = 0; i < 4 * 12; ++i) {
+    int j = i;
+    asm volatile("" : "+v"(j));
+    cam_w[i] = s_cam[j];
+  }
+  const float* cam = cam_w;
+#else
   const float* cam = s_cam;
+#endif
 #else
   const float* __restrict__ cam = cams + (size_t)b * (a.N - 1) * 12;
 #endif
@@ -261,6 +298,21 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
         tz[v] = m[11];
         rs[v] = make_rsrc(a.feats[v + 1], fbytes);
       }
+#if DAMVS_DIAG_WARP_LDS_CAMS && defined(DAMVS_DIAG)
+      // the hoisted rays / translations against the same expressions on the global cameras (kind 4: record word =
+      // lane << 8 | view * 8 + component)
+#pragma unroll
+      for (int v = 0; v < NVC; ++v) {
+        const float* g = gcam + v * 12;
+        const float e[6] = {g[0] * fx + g[1] * fy + g[2], g[3] * fx + g[4] * fy + g[5], g[6] * fx + g[7] * fy + g[8],
+                            g[9], g[10], g[11]};
+        const float h[6] = {rx[v], ry[v], rz[v], tx[v], ty[v], tz[v]};
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+          if (__float_as_uint(e[k]) != __float_as_uint(h[k]))
+            diag_record(4, ((threadIdx.x & 63) << 8) | (v * 8 + k), __float_as_uint(h[k]), __float_as_uint(e[k]));
+      }
+#endif
     }
     auto taps = [&](int v, float hyp) {
       float qx, qy, qz;
@@ -303,6 +355,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
       auto step = [&](int v, const uint4* cur, const float* wcur, uint4* nxt, float* wnxt) {
         if (v + 1 < nv) issue(v + 1, taps(v + 1, hyp), nxt, wnxt);
         else issue(0, taps(0, hyp_n), nxt, wnxt);  // next plane's first view (the last plane: a re-read)
+#if DAMVS_DIAG_WARP_FULLWAIT
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
         reduce(cur, wcur, acc, sq);
       };
       if constexpr (NVC > 0) {
@@ -353,19 +408,239 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
 #endif
 }
 
+// Channel-split form (NHWC maps whose pixel is S = C * sizeof(T) / 16 chunks of 16 bytes, S = 2 or 4): S
+// consecutive lanes share one voxel, lane q owning channel chunk q. Per (voxel, view) sample each lane issues 4
+// loads (its chunk of the 4 bilinear corners) instead of 4 S, and the S lanes of a voxel read one contiguous
+// 16 S-byte pixel record per corner in the SAME instruction: one L1 tag lookup per corner per voxel where the
+// one-lane-per-voxel form needs S (the TA, not HBM, bounds the gather: DESIGN.md section 6). The sample
+// coordinates are computed redundantly by the S lanes; the adaptive weight net's channel dot product is summed
+// across them with DPP quad permutes (VALU only). The per-(plane, view) sequence is pipelined one view deep as in
+// warp_aggregate_kernel (NVC > 0: view count a compile-time constant, rays hoisted; NVC < 0: runtime view loop).
+__device__ __forceinline__ float dpp_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+}
+__device__ __forceinline__ float dpp_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+}
+
+template <typename T, int C, int MODE, int NVC>
+__global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const float* __restrict__ cams,
+                                                         int npix_blocks, int dchunk, int ndchunks) {
+  constexpr int E = Stor<T>::E;  // channels per 16-byte chunk
+  constexpr int S = C / E;       // lanes per voxel
+  constexpr int PPB = 256 / S;   // pixels per block
+  static_assert(S == 2 || S == 4, "channel-split form: 2 or 4 chunks per pixel");
+  static_assert(NVC % 2 == 0 || NVC < 0, "the view pipeline alternates two register sets");
+  const int hw = a.h * a.w, ohw = a.rows * a.w;
+  const int bid = blockIdx.x;
+  auto xcd_remap = [](int i, int n) {
+    const int q8 = n / 8, r8 = n % 8, x = i % 8;
+    return (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + i / 8;
+  };
+  int L = xcd_remap(bid, npix_blocks * ndchunks * a.B);
+  const int dc = L % ndchunks; L /= ndchunks;
+  const int pb = L % npix_blocks;
+  const int b = L / npix_blocks;
+  const float* __restrict__ cam = cams + (size_t)b * (a.N - 1) * 12;
+  const int q = threadIdx.x & (S - 1);                // this lane's channel chunk
+  const int p = pb * PPB + (int)(threadIdx.x / S);    // the S lanes of a pixel are consecutive: they exit together
+  if (p >= ohw) return;
+  const int yl = p / a.w, x = p - yl * a.w;
+  const int y = a.y0 + yl, pg = y * a.w + x;
+  const float fx = (float)x, fy = (float)y;
+  const float kx = (float)a.w / (float)(a.w - 1), ky = (float)a.h / (float)(a.h - 1);
+  constexpr uint32_t rec = C * sizeof(T);
+  const uint32_t bbytes = (uint32_t)hw * rec;
+  const uint32_t sb = (uint32_t)b * bbytes;
+  const uint32_t qoff = (uint32_t)q * 16u;
+  const long long fbytes = (long long)a.B * bbytes;
+
+  float ref[E];
+  if (MODE != AGG_WARP_ONLY) {
+    const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.feats[0], fbytes);
+    Rec16<T>::unpack(__builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r0, (uint32_t)pg * rec + qoff, sb, 0)),
+                     ref);
+  }
+  float kq[E];  // this lane's chunk of the weight net's first 1x1 conv (selects, no dynamic kernarg indexing)
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    float k = a.k1[e];
+#pragma unroll
+    for (int j = 1; j < S; ++j) k = q == j ? a.k1[j * E + e] : k;
+    kq[e] = k;
+  }
+  const float inv_n = 1.f / (float)a.N, inv_n1 = 1.f / (float)(a.N - 1);
+  const int d0 = dc * dchunk, d1 = min(a.D, d0 + dchunk);
+  auto vox_of = [&](int d) { return (((size_t)b * a.D + d) * a.out_rows + a.out_y) * a.w + p; };
+
+  auto reduce = [&](const uint4* rv, const float* wt, float* acc, float* sq) {
+    float v[4][E];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Rec16<T>::unpack(rv[k], v[k]);
+    float s[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) s[e] = ((v[0][e] * wt[0] + v[1][e] * wt[1]) + v[2][e] * wt[2]) + v[3][e] * wt[3];
+    if (MODE == AGG_WARP_ONLY) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[e] = s[e];
+    } else if (MODE == AGG_VARIANCE) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) { acc[e] += s[e]; sq[e] += s[e] * s[e]; }
+    } else {
+      float dot = 0.f;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const float df = ref[e] - s[e];
+        sq[e] = df * df;
+        dot += kq[e] * sq[e];
+      }
+      dot += dpp_xor1(dot);
+      if (S == 4) dot += dpp_xor2(dot);
+      const float a1 = fmaxf(dot * a.s1 + a.t1, 0.f);
+      const float wv = fmaxf(a1 * a.s2 + a.t2, 0.f) + 1.f;
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[e] += wv * sq[e];
+    }
+  };
+  auto finish = [&](int d, float* acc, float* sq) {
+    float o[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (MODE == AGG_VARIANCE) {
+        const float mean = acc[e] * inv_n;
+        o[e] = sq[e] * inv_n - mean * mean;
+      } else if (MODE == AGG_ADAPTIVE) {
+        o[e] = acc[e] * inv_n1;
+      } else {
+        o[e] = acc[e];
+      }
+    }
+    Stor<T>::store16(reinterpret_cast<T*>(a.out) + vox_of(d) * C + q * E, o);
+  };
+  auto init = [&](float* acc, float* sq) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      acc[e] = (MODE == AGG_VARIANCE) ? ref[e] : 0.f;
+      sq[e] = (MODE == AGG_VARIANCE) ? ref[e] * ref[e] : 0.f;
+    }
+  };
+
+  constexpr int NH = NVC > 0 ? NVC : 1;
+  const int nv = NVC > 0 ? NVC : a.N - 1;
+  float rx[NH], ry[NH], rz[NH], tx[NH], ty[NH], tz[NH];
+  __amdgpu_buffer_rsrc_t rs[NH];
+  if constexpr (NVC > 0) {
+#pragma unroll
+    for (int v = 0; v < NVC; ++v) {
+      const float* m = cam + v * 12;
+      rx[v] = m[0] * fx + m[1] * fy + m[2];
+      ry[v] = m[3] * fx + m[4] * fy + m[5];
+      rz[v] = m[6] * fx + m[7] * fy + m[8];
+      tx[v] = m[9];
+      ty[v] = m[10];
+      tz[v] = m[11];
+      rs[v] = make_rsrc(a.feats[v + 1], fbytes);
+    }
+  }
+  auto taps = [&](int v, float hyp) {
+    float qx, qy, qz;
+    if constexpr (NVC > 0) {
+      qx = rx[v] * hyp + tx[v], qy = ry[v] * hyp + ty[v], qz = rz[v] * hyp + tz[v];
+    } else {
+      const float* m = cam + v * 12;
+      const float vx = m[0] * fx + m[1] * fy + m[2];
+      const float vy = m[3] * fx + m[4] * fy + m[5];
+      const float vz = m[6] * fx + m[7] * fy + m[8];
+      qx = vx * hyp + m[9], qy = vy * hyp + m[10], qz = vz * hyp + m[11];
+    }
+    const float iz = __builtin_amdgcn_rcpf(qz);
+    return bilinear_taps(a.h, a.w, rec, qx * iz * kx - 0.5f, qy * iz * ky - 0.5f);
+  };
+  auto issue = [&](int v, const Taps& t, uint4* rv, float* wt) {
+    __amdgpu_buffer_rsrc_t r;
+    if constexpr (NVC > 0) r = rs[v];
+    else r = make_rsrc(a.feats[v + 1], fbytes);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      rv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, t.off[k] + qoff, sb, 0));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wt[k] = t.wt[k];
+  };
+  uint4 ra[4], rb[4];
+  float wa[4], wb[4];
+  float hyp = a.hyps[vox_of(d0)];
+  float hyp_n = a.hyps[vox_of(min(d0 + 1, d1 - 1))];
+  issue(0, taps(0, hyp), ra, wa);
+  for (int d = d0; d < d1; ++d) {
+    const float hyp_nn = a.hyps[vox_of(min(d + 2, d1 - 1))];
+    float acc[E], sq[E];
+    init(acc, sq);
+    auto step = [&](int v, const uint4* cur, const float* wcur, uint4* nxt, float* wnxt) {
+      if (v + 1 < nv) issue(v + 1, taps(v + 1, hyp), nxt, wnxt);
+      else issue(0, taps(0, hyp_n), nxt, wnxt);
+      reduce(cur, wcur, acc, sq);
+    };
+    if constexpr (NVC > 0) {
+#pragma unroll
+      for (int v = 0; v < NVC; v += 2) {
+        step(v, ra, wa, rb, wb);
+        step(v + 1, rb, wb, ra, wa);
+      }
+    } else {
+#pragma unroll 1
+      for (int v = 0; v < nv; v += 2) {
+        step(v, ra, wa, rb, wb);
+        step(v + 1, rb, wb, ra, wa);
+      }
+    }
+    hyp = hyp_n;
+    hyp_n = hyp_nn;
+    finish(d, acc, sq);
+  }
+}
+
+// Lanes per voxel the launcher uses for C-channel maps: the channel-split kernel for NHWC maps of 2 or 4 16-byte
+// chunks per pixel (DAMVS_WARP_SPLIT=0: always one lane per voxel), 1 otherwise.
+template <typename T, int C, bool BLK>
+int split_lanes(const WarpArgs& a) {
+  static const bool off = [] {
+    const char* v = getenv("DAMVS_WARP_SPLIT");
+    return v && v[0] == '0';
+  }();
+  constexpr int S = C * (int)sizeof(T) / 16;
+  if (BLK || off || (S != 2 && S != 4)) return 1;
+  const bool pipe_ok = a.N >= 3 && (a.N - 1) % 2 == 0;
+  return pipe_ok ? S : 1;
+}
+
 template <typename T, int C, int MODE, bool BLK>
 void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, int ndc) {
   static const bool no_pipe = [] {
     const char* v = getenv("DAMVS_WARP_NO_PIPE");
     return v && v[0] == '1';
   }();
-  // view pipeline: unrolled for N = 5 (the DTU default) at 16 channels (stage 2; A/B: 2.29 against 2.37 ms, while
-  // stage 3 runs 1.47 against 1.50 ms on the runtime loop), a runtime view loop for any other odd
-  // N (7, 11: the cfgD / cfgE benchmark configs; 3) and for 32 channels (the unrolled form needs 360 registers)
   static const bool runtime_views = [] {  // DAMVS_WARP_RUNTIME_VIEWS=1: the runtime view loop for N = 5 too
     const char* v = getenv("DAMVS_WARP_RUNTIME_VIEWS");
     return v && v[0] == '1';
   }();
+  if constexpr (!BLK && (C * sizeof(T) == 32 || C * sizeof(T) == 64)) {
+    if (split_lanes<T, C, BLK>(a) > 1 && !no_pipe) {
+      // DAMVS_WARP_LDS_PAD (A/B): unused dynamic LDS per block, capping the blocks per CU (fewer pixels in flight
+      // per XCD, a smaller L2 working set)
+      static const size_t pad = [] {
+        const char* e = getenv("DAMVS_WARP_LDS_PAD");
+        return e ? (size_t)atoll(e) : (size_t)0;
+      }();
+      if (a.N == 5 && !runtime_views)
+        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, 4>), grid, dim3(256), pad, s, a, a.rt, npb, dchunk, ndc);
+      else
+        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, -1>), grid, dim3(256), pad, s, a, a.rt, npb, dchunk, ndc);
+      return;
+    }
+  }
+  // view pipeline: unrolled for N = 5 (the DTU default) at 16 channels (stage 2; A/B: 2.29 against 2.37 ms, while
+  // stage 3 runs 1.47 against 1.50 ms on the runtime loop), a runtime view loop for any other odd
+  // N (7, 11: the cfgD / cfgE benchmark configs; 3) and for 32 channels (the unrolled form needs 360 registers)
   static const bool pipe32 = [] {  // DAMVS_WARP_PIPE32=0: 32-channel maps (stage 1) on the generic view loop
     const char* v = getenv("DAMVS_WARP_PIPE32");
     return !(v && v[0] == '0');
@@ -384,10 +659,18 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
 }
 
 template <typename T, int MODE, bool BLK>
-hipError_t launch_c(hipStream_t s, const WarpArgs& a) {
+hipError_t launch_c(hipStream_t s, const WarpArgs& a0) {
+  WarpArgs a = a0;
   // 32-bit buffer offsets: each view's feature tensor must stay below 2 GiB
   if ((long long)a.B * a.h * a.w * a.C * (long long)sizeof(T) >= (1LL << 31)) return hipErrorInvalidValue;
-  const int npb = (a.rows * a.w + 255) / 256;
+  int lanes = 1;  // lanes per voxel of the kernel launch_k will pick (pixels per block = 256 / lanes)
+  switch (a.C) {
+    case 8: lanes = split_lanes<T, 8, BLK>(a); break;
+    case 16: lanes = split_lanes<T, 16, BLK>(a); break;
+    case 32: lanes = split_lanes<T, 32, BLK>(a); break;
+  }
+  const int ppb = 256 / lanes;
+  const int npb = (a.rows * a.w + ppb - 1) / ppb;
   // depth chunk: as long as possible (locality) while keeping >= ~4 blocks per CU in flight
   int dchunk = a.D;
   static const long long minblk = [] {
@@ -397,6 +680,11 @@ hipError_t launch_c(hipStream_t s, const WarpArgs& a) {
   while (dchunk > 2 && (long long)npb * a.B * ((a.D + dchunk - 1) / dchunk) < minblk) dchunk = (dchunk + 1) / 2;
   const int ndc = (a.D + dchunk - 1) / dchunk;
   dim3 grid((unsigned)(npb * ndc * a.B));
+  static const int order = [] {
+    const char* e = getenv("DAMVS_WARP_ORDER");
+    return e ? atoi(e) : 0;
+  }();
+  a.order = order;
   switch (a.C) {
     case 8: launch_k<T, 8, MODE, BLK>(s, a, grid, npb, dchunk, ndc); break;
     case 16: launch_k<T, 16, MODE, BLK>(s, a, grid, npb, dchunk, ndc); break;

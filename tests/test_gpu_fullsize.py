@@ -7,7 +7,7 @@ reference's inference default, test_uni.py:77); cfgE Tanks&Temples 1920x1056, 11
   bf16-representable fp32 features (one oracle run serves both paths): the fp32 HIP path against the
   oracle (oracle/mvs_oracle.py, a restatement of models/cas_mvsnet.py:18-134) at the north-star gate,
   per-pixel |depth - ref| / ref <= 1e-3; the bf16 HIP path (the benchmark's kernels) at the stated bf16
-  gate, mean <= 5e-3 and p99 <= 2e-2 per-pixel relative depth. (10-40 s of oracle time per case.)
+  gate, mean <= 5e-4, p99 <= 1e-3 and max <= 5e-3 per-pixel relative depth. (10-40 s of oracle time per case.)
 * The bf16 cascade at each config: size-independent properties of the regression
   (models/cas_mvsnet.py:105-124) at every stage -- the depth of each pixel inside its hypothesis
   range, probabilities summing to 1 over D, confidence in [0, 1] -- plus batch independence (two
@@ -68,7 +68,11 @@ def test_depthnet_fullres_vs_oracle(cfg, s):
     # probabilities: absolute 5e-3 (a fp32 logit difference of a few 1e-3 moves a sharp D = 48 softmax
     # peak by ~1.5e-3; measured max 1.45e-3 at stage 1), the gate stays on depth as north_star states
     assert np.abs(out["prob_volume"].cpu().numpy() - ref["prob_volume"].numpy()).max() < 5e-3
-    assert pr.mean() < 5e-3 and np.quantile(pr, 0.99) < 2e-2
+    # bf16 benchmark path (bf16 volume, bf16 BN-folded weights, bf16 U-Net activations, fp32 accumulation and
+    # regression): measured max 2.6e-3 / 3.7e-4 / 9.1e-4 (cfgC stages 1-3), p99 <= 5.3e-4, mean <= 7.5e-5 over
+    # cfgC/D/E. The three bf16 roundings contribute comparably at stage 1 (tools/diag_bf16_error.py,
+    # profiles/r03/diag_bf16_error.jsonl: volume alone max 1.2e-3, weights alone 1.1e-3, both 1.3e-3).
+    assert pr.mean() < 5e-4 and np.quantile(pr, 0.99) < 1e-3 and pr.max() < 5e-3, (pr.mean(), pr.max())
 
 
 @pytest.mark.parametrize("cfg", list(CFGS))

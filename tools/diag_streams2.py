@@ -67,7 +67,7 @@ def main():
             sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
             main_s = torch.cuda.current_stream()
             summary = {"layer": which, "trials": 0, "outputs": 0, "differ_kernel_compare": 0, "details": []}
-            for trial in range(4):
+            for trial in range(int(os.environ.get("DIAG_TRIALS", "4"))):
                 sa.wait_stream(main_s)
                 sb.wait_stream(main_s)
                 with torch.cuda.stream(sa):
@@ -100,12 +100,32 @@ def main():
                         d["first_voxel"] = f
                         d["first_got"] = o[tuple(f)].float().tolist()[:4]
                         d["first_ref"] = ref[tuple(f)].float().tolist()[:4]
+                    # shape of the differing set: whole pixel columns (all D planes)? whole 64-pixel waves?
+                    pix = vox.any(1)  # (B, h, w)
+                    d["pixels_differ"] = int(pix.sum())
+                    d["pixels_all_planes_differ"] = int(vox.all(1).sum())
+                    flat = pix.reshape(B, -1)
+                    waves = flat.reshape(B, -1, 64).sum(-1)  # affected pixels per 64-pixel wave (256 | h*w)
+                    nz = waves[waves > 0]
+                    d["waves_touched"] = int(nz.numel())
+                    d["pixels_per_touched_wave"] = [int(nz.min()), float(nz.float().mean()), int(nz.max())] if nz.numel() else []
+                    lanes = flat.nonzero()[:, 1] % 64  # lane of each differing pixel in its wave
+                    d["lane_group_hist"] = torch.bincount(lanes // 16, minlength=4).tolist()
+                    d["lane_in_group_hist"] = torch.bincount(lanes % 16, minlength=16).tolist()
+                    d["wave_in_block_hist"] = torch.bincount((flat.nonzero()[:, 1] % 256) // 64, minlength=4).tolist()
+                    blocks = flat.reshape(B, -1, 256).sum(-1)
+                    d["blocks_touched"] = int((blocks > 0).sum())
                     # host copy (DMA engine), then again after a 2 GiB copy on the main stream
                     d["differ_host_copy"] = int((oi.cpu() != ref_host).sum())
                     scrub_b.copy_(scrub_a)
                     torch.cuda.synchronize()
                     d["differ_after_scrub_kernel"] = int((o.view(torch.int16) != ref.view(torch.int16)).sum())
                     summary["details"].append(d)
+            if hasattr(lib, "damvs_diag_take_warp"):
+                buf = (ctypes.c_uint * (8 + 8 * 64))()
+                lib.damvs_diag_take_warp(buf, len(buf))
+                summary["diag_records"] = int(buf[0])
+                summary["diag_first"] = [list(buf[8 + 8 * i: 16 + 8 * i]) for i in range(min(int(buf[0]), 6))]
             print(json.dumps(summary), flush=True)
 
 

@@ -20,12 +20,16 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PASSES = [["GRBM_GUI_ACTIVE", "SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD"],
-          ["TA_BUSY_avr", "TD_BUSY_avr"],
+          ["GRBM_GUI_ACTIVE", "TA_TA_BUSY_sum", "TA_BUFFER_READ_WAVEFRONTS_sum"],
           ["TCC_HIT_sum", "TCC_MISS_sum"],
           ["TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum"],
           ["FETCH_SIZE"],
+          ["TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum"],
           ["WRITE_SIZE"]]
-KERNEL = os.environ.get("PMC_WARP_KERNEL", "warp_aggregate_kernel<unsigned short, 16")
+# the stage-2 warp: the channel-split kernel (default) or the one-lane-per-voxel kernel (DAMVS_WARP_SPLIT=0)
+KERNEL = os.environ.get("PMC_WARP_KERNEL", "warp_split_kernel<unsigned short, 16"
+                        if os.environ.get("DAMVS_WARP_SPLIT", "1") != "0" else "warp_aggregate_kernel<unsigned short, 16")
+GRID = int(os.environ.get("PMC_WARP_GRID", "3788800" if "split" in KERNEL else "1894400"))  # threads per launch
 N_PIPE = 5
 
 
@@ -40,7 +44,7 @@ def run_pass(i, counters, out):
     disp = collections.OrderedDict()
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if KERNEL not in row["Kernel_Name"] or int(row.get("Grid_Size", 0) or 0) != 1894400:
+            if KERNEL not in row["Kernel_Name"] or int(row.get("Grid_Size", 0) or 0) != GRID:
                 continue
             k = int(row["Dispatch_Id"])
             e = disp.setdefault(k, {"start": int(row["Start_Timestamp"]),
@@ -75,23 +79,36 @@ def main():
         if "ns" not in m:
             continue
         s = {"launches_per_pass": len(d.get("ns", [])) // len(sel), "ms": m["ns"] / 1e6}
-        if "GRBM_GUI_ACTIVE" in m:
-            s["effective_clock_GHz"] = m["GRBM_GUI_ACTIVE"] / m["ns"]
-        for k in ("TA_BUSY_avr", "TD_BUSY_avr"):
-            if k in m and "GRBM_GUI_ACTIVE" in m:
-                s[k.replace("_avr", "") + "_frac"] = m[k] / m["GRBM_GUI_ACTIVE"]
+        if "GRBM_GUI_ACTIVE" in m:  # summed over the 8 XCDs (MI355X_MICROARCH.md): cycles = GRBM / 8
+            cyc = m["GRBM_GUI_ACTIVE"] / 8.0
+            s["effective_clock_GHz"] = cyc / m["ns"]
+            if "TA_TA_BUSY_sum" in m:  # one TA per CU: busy fraction = sum / 256 CUs / cycles
+                s["TA_busy_frac"] = m["TA_TA_BUSY_sum"] / 256.0 / cyc
+        if "TA_TA_BUSY_sum" in m and "TA_BUFFER_READ_WAVEFRONTS_sum" in m:
+            s["TA_cycles_per_buffer_read_instr"] = m["TA_TA_BUSY_sum"] / max(1.0, m["TA_BUFFER_READ_WAVEFRONTS_sum"])
+        if "TCP_TOTAL_CACHE_ACCESSES_sum" in m and "TA_BUFFER_READ_WAVEFRONTS_sum" in m:
+            s["l1_tag_lookups_per_read_instr"] = m["TCP_TOTAL_CACHE_ACCESSES_sum"] / max(1.0, m["TA_BUFFER_READ_WAVEFRONTS_sum"])
         if "TCC_HIT_sum" in m:
             s["l2_hit_rate"] = m["TCC_HIT_sum"] / max(1.0, m["TCC_HIT_sum"] + m["TCC_MISS_sum"])
-        for k in ("TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VALU", "SQ_WAVES"):
+        for k in ("TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VALU", "SQ_WAVES",
+                  "TA_BUFFER_READ_WAVEFRONTS_sum"):
             if k in m:
                 s[k] = m[k]
-        if "FETCH_SIZE" in m:  # KB units; MI355X_MICROARCH.md: x2 for 128-B requests (calibrated on streaming reads)
+        if "FETCH_SIZE" in m:
+            # KB units. profiles/r03/pmc_fetch_calibration.json (tools/pmc_calib): on gfx950 every L2 -> fabric read
+            # request is a 128-byte line fill (TCC_EA0_RDREQ_32B / _64B ~ 0) and FETCH_SIZE counts 64 bytes per
+            # request, for streaming reads AND for 16 / 32 / 64-byte record gathers in random order: x2 is the
+            # calibrated byte count for the warp's gathers too
             s["fetch_bytes_raw"] = m["FETCH_SIZE"] * 1024
             s["fetch_bytes_x2_gfx950"] = m["FETCH_SIZE"] * 1024 * 2
+        if "TCC_EA0_RDREQ_sum" in m:
+            n32, n64 = m.get("TCC_EA0_RDREQ_32B_sum", 0.0), m.get("TCC_EA0_RDREQ_64B_sum", 0.0)
+            s["read_requests"] = m["TCC_EA0_RDREQ_sum"]
+            s["read_bytes_by_request_size"] = 128 * (m["TCC_EA0_RDREQ_sum"] - n32 - n64) + 64 * n64 + 32 * n32
         if "WRITE_SIZE" in m:
             s["write_bytes"] = m["WRITE_SIZE"] * 1024
         summary[name] = s
-    json.dump({"kernel": KERNEL, "grid": 1894400, "counters": PASSES, "summary": summary},
+    json.dump({"kernel": KERNEL, "grid": GRID, "counters": PASSES, "summary": summary},
               open(os.path.join(out, "pmc_warp_inpipe.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
 
