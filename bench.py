@@ -281,6 +281,9 @@ def pmc_traffic(config, batch, kernel_substr="warp_aggregate"):
             p = json.load(f)["summary"]["pipeline"]
         if "fetch_bytes_x2_gfx950" in p and "write_bytes" in p:
             return {"bytes": int(p["fetch_bytes_x2_gfx950"] + p["write_bytes"]),
+                    "raw_bytes": int(p["fetch_bytes_raw"] + p["write_bytes"]),
+                    "read_bytes_by_request_size": int(p["read_bytes_by_request_size"]) if "read_bytes_by_request_size" in p
+                    else None,
                     "source": os.path.relpath(inpipe[-1], REPO) + " (in-pipeline launches)"}
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_%s_%s_b%d.json" % (kernel_substr, config, batch))))
     if not files:
@@ -458,10 +461,15 @@ def main():
                        "parallelism": "replicas x%d (reference views sharded over ranks)" % world},
             "ms_per_stage": phases,
             "latency_b1": lat,
-            "roofline": {"kernel": "warp_aggregate stage2 (fused homography warp + adaptive aggregation), "
-                                   "in-pipeline launch time (HIP events inside damvs_stage_forward_probed)",
+            "roofline": {"kernel": "warp_split_kernel stage2 (fused homography warp + adaptive aggregation, 2 lanes "
+                                   "per voxel), in-pipeline launch time (HIP events inside damvs_stage_forward_probed)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr["bytes"] if tr else None,
+                         "traffic_raw": tr.get("raw_bytes") if tr else None,
+                         "traffic_note": "traffic = FETCH_SIZE x 2 + WRITE_SIZE per launch: on gfx950 every L2 read "
+                                         "request is a 128-B line fill counted as 64 B, for streaming reads and for "
+                                         "16/32/64-B record gathers alike (profiles/r03/pmc_fetch_calibration.json); "
+                                         "traffic_raw = FETCH_SIZE + WRITE_SIZE as rocprofv3 reports them",
                          "traffic_source": ("committed PMC profile " + tr["source"]) if tr else None,
                          "ms_per_launch": round(pipe_ms, 4), "launch": "whole batch (B=%d) on one stream, the "
                          "attribution pass after the timed steps; rocprof check: tools/prof_roofline_kernel.py" % args.batch,

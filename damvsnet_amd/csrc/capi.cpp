@@ -805,8 +805,11 @@ int build_phases_2d(damvs_conv2d* L) {
   } else {
     if (s != 1 && s != 2) return fail(DAMVS_E_SHAPE, "transposed stride %d unsupported", s);
     L->nphase = s * s;
+    // taps in ascending input offset: a stride-1 transposed conv then has exactly the tap list of a plain conv
+    // (offsets -p .. K-1-p, row-major), so the LDS-tiled 3x3 kernel (lds3_ok) takes the full-resolution decoder
+    // layers instead of the gather kernel
     for (int r = 0; r < s; ++r)
-      for (int k = 0; k < K; ++k)
+      for (int k = K - 1; k >= 0; --k)
         if (((r + p - k) % s + s) % s == 0) { offs[r].push_back((r + p - k) / s); ks[r].push_back(k); }
   }
   int w_off = 0, g_off = 0;

@@ -30,7 +30,6 @@ struct WarpArgs {
   int B, N, C, D, h, w;          // h x w: the feature maps (and the full reference image grid)
   int y0, rows;                  // computed: reference rows [y0, y0 + rows) (0, h: the whole image) ...
   int out_rows, out_y;           // ... at rows [out_y, out_y + rows) of the hyps / out planes
-  int order;                     // block order (set by the launcher, DAMVS_WARP_ORDER): see warp_aggregate_kernel
   // adaptive weight net, BN folded: a = relu(sum_c k1[c] x_c * s1 + t1); wt = relu(a * s2 + t2)
   float k1[32];
   float s1, t1, s2, t2;

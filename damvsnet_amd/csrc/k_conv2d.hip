@@ -908,9 +908,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void conv2d_wide_kernel(const C
     }
   }
 
-  // tail: the plane chunk's A fragments and the epilogue's residual records are requested together, so
-  // their latencies overlap the plane chunk's LDS reads and MFMAs instead of following one another
-  typedef typename IO::quad quad;
+  // tail: the plane chunk (A fragments straight from global memory), then the epilogue
   const int qyw = qy0 + wn;  // the wave's q-row
   raw ag[4];
   if (ph.gchunks > 0) {
@@ -923,32 +921,6 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void conv2d_wide_kernel(const C
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout * ES);
   const __amdgpu_buffer_rsrc_t rpre = make_rsrc(a.res_pre ? a.res_pre : a.out, a.res_pre ? nout * ES : 0);
   const __amdgpu_buffer_rsrc_t rpost = make_rsrc(a.res_post ? a.res_post : a.out, a.res_post ? nout / (up * up) * ES : 0);
-  bool cok[4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) cok[m] = (mt0 + wm * 4 + m) * 16 + g * 4 < a.cout;
-  auto out_px = [&](int j, int& pout, int& ppost) {
-    const int qx = qx0 + j * 16 + n;
-    const int oy = qyw * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
-    pout = (b * a.Ho + oy) * a.Wo + ox;
-    ppost = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
-    return qyw < a.Hq && qx < a.Wq;
-  };
-  quad qres[4][4];  // res_pre, else res_post (a layer with both reads res_post in the epilogue)
-  const bool pre_first = a.res_pre != nullptr, any_res = a.res_pre || a.res_post;
-  if (any_res) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int pout, ppost;
-      const bool vok = out_px(j, pout, ppost);
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int co = (mt0 + wm * 4 + m) * 16 + g * 4;
-        const bool ok = vok && cok[m];
-        qres[j][m] = pre_first ? IO::ldq(rpre, ok ? (uint32_t)(pout * a.cout + co) * ES : kOOB)
-                               : IO::ldq(rpost, ok ? (uint32_t)(ppost * a.cout + co) * ES : kOOB);
-      }
-    }
-  }
   // the fp32 plane as a trailing K chunk (tap x plane), B from the staged plane halo
   if (ph.gchunks > 0) {
     float v[4][8];
@@ -969,38 +941,74 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void conv2d_wide_kernel(const C
   }
 
   // epilogue (as conv2d_mfma_kernel): residual before ReLU, ReLU, (upsampled) residual after, store
-  float bias[4][4];
+  {
+    // through LDS: the wave's 64 channels x 64 pixels go to a wave-private fp32 staging tile in two halves of 32
+    // pixels (the K loop's A and halo buffers are free after its last barrier; 4 x 8.5 KB stay below the plane
+    // halo, which other waves may still read), and each lane then finishes one pixel's
+    // 32-channel half: 64 contiguous bytes of residual loads and stores (16-byte accesses; the accumulator layout
+    // stores 8 bytes per lane, 16 pixels apart). Row pitch 68 floats: the b128 writes of 16 lanes (16 pixels,
+    // one column) and reads (16 pixels) hit distinct banks.
+    constexpr int PITCH = 68;
+    float* st = reinterpret_cast<float*>(abuf) + wave * (32 * PITCH);
+    const int cb = (mt0 + wm * 4) * 16;       // the wave's first output channel
+    const int lp = lane & 31, hc = lane >> 5;  // this lane's pixel within the half, its 32-channel half
+    const int co0 = cb + hc * 32;
+    const bool cvalid = co0 < a.cout;
+    const float* bias = a.bias + (cvalid ? co0 : 0);  // a padded channel tile past cout reads channel 0's bias
+    auto add8 = [](const raw& q, float* v) {
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int co = (mt0 + wm * 4 + m) * 16 + g * 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bias[m][i] = a.bias[co + i];  // padded to cout_pad
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    int pout, ppost;
-    const bool vok = out_px(j, pout, ppost);
-    quad qpost[4];
-    if (a.res_pre && a.res_post) {
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int co = (mt0 + wm * 4 + m) * 16 + g * 4;
-        qpost[m] = IO::ldq(rpost, vok && cok[m] ? (uint32_t)(ppost * a.cout + co) * ES : kOOB);
+      for (int i = 0; i < 4; ++i) {
+        v[2 * i] += __uint_as_float(w[i] << 16);
+        v[2 * i + 1] += __uint_as_float(w[i] & 0xffff0000u);
       }
-    }
+    };
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      float r[4];
+    for (int h = 0; h < 2; ++h) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) r[i] = acc[m][j][i] + bias[m][i];
-      if (a.res_pre) IO::addq(qres[j][m], r);
-      if (a.relu) {
+      for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] = fmaxf(r[i], 0.f);
+        for (int m = 0; m < 4; ++m) {
+          const f32x4_t v = acc[m][2 * h + jj];
+          *reinterpret_cast<float4*>(st + (jj * 16 + n) * PITCH + m * 16 + g * 4) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      asm volatile("" ::: "memory");  // one wave's LDS accesses complete in order: only the compiler must keep it
+      const int j = 2 * h + (lp >> 4);
+      const int qx = qx0 + j * 16 + (lp & 15);
+      const int oy = qyw * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
+      const int pout = (b * a.Ho + oy) * a.Wo + ox;
+      const int ppost = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
+      const bool ok = qyw < a.Hq && qx < a.Wq && cvalid;
+      const uint32_t ooff = ok ? (uint32_t)(pout * a.cout + co0) * ES : kOOB;
+      const uint32_t poff = ok ? (uint32_t)(ppost * a.cout + co0) * ES : kOOB;
+      raw pre[4], post[4];  // all residual records requested before the first store
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (a.res_pre) pre[k] = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rpre, ooff + 16u * k, 0, 0));
+        if (a.res_post) post[k] = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rpost, poff + 16u * k, 0, 0));
       }
-      if (a.res_post) IO::addq(a.res_pre ? qpost[m] : qres[j][m], r);
-      const int co = (mt0 + wm * 4 + m) * 16 + g * 4;
-      IO::stq(ro, vok && cok[m] ? (uint32_t)(pout * a.cout + co) * ES : kOOB, r);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // 8 channels at a time
+        float r[8];
+        const float4 v0 = *reinterpret_cast<const float4*>(st + lp * PITCH + hc * 32 + 8 * k);
+        const float4 v1 = *reinterpret_cast<const float4*>(st + lp * PITCH + hc * 32 + 8 * k + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(bias + 8 * k);
+        const float4 b1 = *reinterpret_cast<const float4*>(bias + 8 * k + 4);
+        r[0] = v0.x + b0.x; r[1] = v0.y + b0.y; r[2] = v0.z + b0.z; r[3] = v0.w + b0.w;
+        r[4] = v1.x + b1.x; r[5] = v1.y + b1.y; r[6] = v1.z + b1.z; r[7] = v1.w + b1.w;
+        if (a.res_pre) add8(pre[k], r);
+        if (a.relu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) r[e] = fmaxf(r[e], 0.f);
+        }
+        if (a.res_post) add8(post[k], r);
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(r[2 * i]) | ((uint32_t)f2bf(r[2 * i + 1]) << 16);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, make_uint4(w[0], w[1], w[2], w[3])), ro,
+                                               ooff + 16u * k, 0, 0);
+      }
+      asm volatile("" ::: "memory");  // the next half overwrites the staging tile
     }
   }
 }
@@ -1011,7 +1019,8 @@ hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
     const char* v = getenv("DAMVS_CONV2D_WIDE");
     return v && v[0] == '0';
   }();
-  if (off || a.in_stride != 1 || a.xpair || a.ngeo > 1 || a.MTtot % 8 || a.c0 % 32 || a.c1 % 32 || a.c0 + a.c1 < 64)
+  if (off || a.in_stride != 1 || a.xpair || a.ngeo > 1 || a.MTtot % 8 || a.c0 % 32 || a.c1 % 32 || a.c0 + a.c1 < 64 ||
+      a.cout % 32)  // the epilogue finishes whole 32-channel halves per lane
     return hipErrorNotSupported;
   int dmin = 0, dmax = 0;
   for (int p = 0; p < a.nphase; ++p)

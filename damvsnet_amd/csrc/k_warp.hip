@@ -141,32 +141,16 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
   constexpr int E = Stor<T>::E, NQ = C / E;
   static_assert(NVC % 2 == 0 || NVC < 0, "the view pipeline alternates two register sets");
   const int hw = a.h * a.w, ohw = a.rows * a.w;  // feature-map plane, computed rows (y0 .. y0 + rows - 1)
-  // Block order (dispatch position bid runs on XCD bid % 8). order 0: XCD-contiguous over the whole grid (XCD k
-  // takes the k-th eighth of (batch, pixel block, depth chunk)). order 1: batch-synchronous bands -- the grid is
-  // dispatched one batch element at a time and within it XCD k takes the k-th eighth, so every XCD works in its
-  // own band of the SAME batch element (one element's source maps hot in the Infinity Cache instead of B / 2
-  // elements'). order 2: plain dispatch order (consecutive blocks on different XCDs).
-  const int bid = blockIdx.x;
-  auto xcd_remap = [](int i, int n) {  // bijective on [0, n): XCD i % 8 gets the (i % 8)-th contiguous eighth
-    const int q8 = n / 8, r8 = n % 8, x = i % 8;
-    return (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + i / 8;
-  };
-  int L;
-  if (a.order == 1) {
-    const int nb = npix_blocks * ndchunks;
-    L = (bid / nb) * nb + xcd_remap(bid % nb, nb);
-  } else if (a.order == 2) {
-    L = bid;
-  } else {
-    L = xcd_remap(bid, npix_blocks * ndchunks * a.B);
-  }
+  const int nblk = npix_blocks * ndchunks * a.B;
+  const int bid = blockIdx.x, q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;  // bijective XCD remap
   const int dc = L % ndchunks; L /= ndchunks;
   const int pb = L % npix_blocks;
   const int b = L / npix_blocks;
   // this batch element's [N-1][12] source cameras: block-uniform reads through a read-only, non-aliased
-  // kernel argument, i.e. scalar loads into SGPRs. (They were staged in LDS; with another kernel running
-  // on a concurrent stream that copy came back altered in up to 76 of 80 launches — tools/streams_race_kernel.py
-  // — and the scalar path needs neither LDS nor a barrier.)
+  // kernel argument, i.e. scalar loads into SGPRs. (Staged in LDS and read back by the compiler's wide broadcast
+  // ds_read_b128 / ds_read2_b64, lanes 48-63 of some waves got wrong cameras beside U-Net kernels on another
+  // stream, while ds_read_b32 reads of the same copy were always right: DESIGN.md section 4, "Concurrent streams".)
 #if DAMVS_DIAG_WARP_LDS_CAMS
   __shared__ __attribute__((aligned(16))) float s_cam[(kMaxViews - 1) * 12];
   const float* gcam = cams + (size_t)b * (a.N - 1) * 12;
@@ -680,11 +664,6 @@ hipError_t launch_c(hipStream_t s, const WarpArgs& a0) {
   while (dchunk > 2 && (long long)npb * a.B * ((a.D + dchunk - 1) / dchunk) < minblk) dchunk = (dchunk + 1) / 2;
   const int ndc = (a.D + dchunk - 1) / dchunk;
   dim3 grid((unsigned)(npb * ndc * a.B));
-  static const int order = [] {
-    const char* e = getenv("DAMVS_WARP_ORDER");
-    return e ? atoi(e) : 0;
-  }();
-  a.order = order;
   switch (a.C) {
     case 8: launch_k<T, 8, MODE, BLK>(s, a, grid, npb, dchunk, ndc); break;
     case 16: launch_k<T, 16, MODE, BLK>(s, a, grid, npb, dchunk, ndc); break;

@@ -62,8 +62,8 @@ def main():
         ms = e0.elapsed_time(e1)
         c0 = in0.shape[-1] if in0 is not None else 0
         c1 = in1.shape[-1] if in1 is not None else 0
-        rows.append((ms, lab, "%dx%d->%dx%d B%d cin %d+%d+g%d cout %d" % (Hi, Wi, oshape[1], oshape[2], B, c0, c1, ng,
-                                                                         L.cout)))
+        rows.append((ms, lab, "%s %dx%d->%dx%d B%d cin %d+%d+g%d cout %d" % (L.desc, Hi, Wi, oshape[1], oshape[2], B, c0,
+                                                                            c1, ng, L.cout)))
         agg[lab] += ms
     print("per group (ms):", {k: round(v, 3) for k, v in agg.items()}, "total %.3f" % sum(agg.values()))
     for ms, lab, desc in sorted(rows, reverse=True)[:args.top]:

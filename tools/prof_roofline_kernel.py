@@ -12,7 +12,7 @@ import csv
 import sys
 
 
-def main(path, prefix="warp_aggregate_kernel<unsigned short, 16,"):
+def main(path, prefix="warp_split_kernel<unsigned short, 16,"):
     rows = sorted((r for r in csv.DictReader(open(path)) if prefix in r["Kernel_Name"]),
                   key=lambda r: int(r["Start_Timestamp"]))
     segs = []

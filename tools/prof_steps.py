@@ -8,7 +8,7 @@ import csv
 import sys
 
 
-ROOFLINE_KERNEL = "warp_aggregate_kernel<unsigned short, 16,"  # stage 2 (C = 16), bf16
+ROOFLINE_KERNEL = "warp_split_kernel<unsigned short, 16,"  # stage 2 (C = 16), bf16, channel-split form
 
 
 def main(path, warmup=2, steps=5, top=40, roofline_iters=20):
