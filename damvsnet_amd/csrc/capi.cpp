@@ -398,9 +398,8 @@ WarpArgs warp_args(const damvs_stage* st, int B, int N, int C, int D, int h, int
 // (models/cas_mvsnet.py:105-124) on the U-Net output c0 [B][D][h][w][base].
 int regress_tail(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, const void* feat, const float* hyps,
                  const float* prob_init, float* logits, float* depth, float* conf, float* var, float* prob) {
-  // banded MFMA prob conv + regression: TA-bound on its per-tap B loads, it beats the LDS-tiled VALU
-  // kernel only with >= 2 plane groups (measured at cfgC: stage 2 -26 us, stage 3 +50 us)
-  if (st->prob_pack && D >= 32 && D <= 64 && !prob_mfma_disabled())
+  // bf16, base 8: the prob conv on MFMA (logits in an LDS column, as the VALU kernel below)
+  if (st->prob_pack && prob_mfma_smem(D) <= 160 * 1024 && !prob_mfma_disabled())
     return hip_check(launch_prob_mfma(s, B, D, h, w, feat, st->prob_pack, prob_init, hyps, depth, conf, var, prob),
                      "prob_mfma launch");
   if (prob_regress_smem_bytes(st->dtype, st->base, D) <= 160 * 1024)  // fused: logits stay in LDS
@@ -517,27 +516,26 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
     rc = upload(pw.data(), pw.size() * 4, reinterpret_cast<void**>(&st->prob_w));
   }
   if (rc == DAMVS_OK && dtype == DAMVS_BF16 && b == 8) {
-    // Prob conv (Conv3d(8, 1, k3), models/module.py:530) as one 16 x K MFMA operand per 32-wide K
-    // chunk: rows m = 16 consecutive output planes d0 + m, K = (input plane d0 - 1 + r, r = 0..17;
-    // ky; kx; channel), entry W[kd = r - m][ky][kx][c] when 0 <= kd <= 2 (banded), else 0. The fp32
-    // weights are split into bf16 hi + lo parts (two MFMAs) so the logits keep ~16 mantissa bits.
-    const int nch = kProbChunks;
-    std::vector<uint16_t> pk((size_t)nch * 2 * 64 * 8, 0);
-    for (int s = 0; s < nch; ++s)
+    // pack_prob_rows: the prob conv (Conv3d(8, 1, k3), models/module.py:530) as prob_mfma_kernel's A operand
+    // (k_regress.hip): rows m = 4 j + dz (output pixel row j of four, kernel depth dz), K = (voxel slot
+    // sl = 3 r + kx of input row r = 0..5, channel), entry W[c][dz][ky = r - j][kx] when dz < 3, sl < 18 and
+    // 0 <= ky <= 2, else 0; [chunk][term][lane][8], the fp32 weight as three bf16 terms hi + mid + lo.
+    std::vector<uint16_t> pk((size_t)kProbRowChunks * kProbRowTerms * 64 * 8, 0);
+    for (int k = 0; k < kProbRowChunks; ++k)
       for (int lane = 0; lane < 64; ++lane)
         for (int e = 0; e < 8; ++e) {
-          const int m = lane & 15, k = s * 32 + (lane >> 4) * 8 + e, tp = k / 8, c = k % 8;
+          const int m = lane & 15, j = m >> 2, dz = m & 3, sl = 4 * k + (lane >> 4), r = sl / 3, kx = sl % 3;
+          const int ky = r - j;
           float v = 0.f;
-          if (tp < 18 * 9) {
-            const int kd = tp / 9 - m;
-            if (kd >= 0 && kd <= 2) v = cr->prob_weight[(size_t)c * 27 + kd * 9 + tp % 9];
+          if (dz < 3 && sl < 18 && ky >= 0 && ky <= 2) v = cr->prob_weight[(size_t)e * 27 + dz * 9 + ky * 3 + kx];
+          for (int t = 0; t < kProbRowTerms; ++t) {
+            const uint16_t q = to_bf16(v);
+            pk[(((size_t)k * kProbRowTerms + t) * 64 + lane) * 8 + e] = q;
+            float qf;
+            const uint32_t qb = (uint32_t)q << 16;
+            std::memcpy(&qf, &qb, 4);
+            v -= qf;  // exact: the remainder of a round-to-nearest bf16 term
           }
-          const uint16_t hi = to_bf16(v);
-          float hf;
-          const uint32_t hb = (uint32_t)hi << 16;
-          std::memcpy(&hf, &hb, 4);
-          pk[(((size_t)s * 2 + 0) * 64 + lane) * 8 + e] = hi;
-          pk[(((size_t)s * 2 + 1) * 64 + lane) * 8 + e] = to_bf16(v - hf);
         }
     rc = upload(pk.data(), pk.size() * 2, &st->prob_pack);
   }

@@ -169,11 +169,12 @@ hipError_t launch_prob_regress(hipStream_t s, int store, int B, int Cb, int D, i
                                const float* wprob, const float* prob_init, const float* hyps, float* depth,
                                float* conf, float* var, float* prob);
 size_t prob_regress_smem_bytes(int store, int Cb, int D);
-// banded-MFMA prob conv + regression (bf16 storage, base 8, D <= 64): apack from pack_prob_banded
-constexpr int kProbChunks = (18 * 9 * 8 + 31) / 32;  // 18 input planes x 9 taps x 8 channels, 32-wide chunks
+// MFMA prob conv + regression (bf16 storage, base 8; LDS bounds D): apack from pack_prob_rows (capi.cpp)
+constexpr int kProbRowChunks = 5, kProbRowTerms = 3;  // prob_mfma_kernel: 18 voxel slots x 8 channels, 3 bf16 terms
 hipError_t launch_prob_mfma(hipStream_t s, int B, int D, int h, int w, const void* feat, const void* apack,
                             const float* prob_init, const float* hyps, float* depth, float* conf, float* var,
                             float* prob);
+size_t prob_mfma_smem(int D);
 bool prob_mfma_disabled();  // DAMVS_PROB_MFMA=0 (A/B testing)
 hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float* logits, const float* hyps,
                           float* depth, float* conf, float* var, float* prob);

@@ -275,118 +275,174 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
   var[(size_t)b * hw + pix] = 3.f * sqrtf(vs);
 }
 
-// Prob conv on MFMA (bf16 storage, 8 channels). Cout = 1 would leave 15 of 16 MFMA rows empty, so
-// the rows are 16 consecutive OUTPUT PLANES instead: with K = (input plane r = 0..17 relative to
-// d0 - 1, ky, kx, channel), the 16 x K operand is the banded weight matrix W[r - m] (capi.cpp,
-// pack_prob_banded; fp32 weights as bf16 hi + lo, two MFMAs per chunk). Lane group g of a B
-// fragment is one tap = one 16-byte voxel (8 channels), so every B load is a coalesced 16-pixel row
-// segment. Wave w owns planes [16w, 16w+16) of a 64-pixel row segment (4 N-tiles reuse each A
-// fragment); the D logits of the block's 64 pixels meet in LDS and 64 threads run the regression.
-constexpr int kPR = 4;  // 16-pixel N-tiles per wave
+// Prob conv on MFMA + regression (bf16 storage, 8 channels). A block owns an 8 x 32 pixel tile for all D planes,
+// as prob_regress_kernel, but each input plane's (8+2) x (32+2) halo is staged in LDS as the raw 16-byte bf16
+// voxels (no widening) and the conv runs on the matrix cores. Wave w computes rows 4(w>>1) .. +3 x columns
+// 16(w&1) .. +15 of the tile as one 16 x 16 output tile per plane:
+//   columns n   = 16 pixels of a row,
+//   rows m      = 4 j + dz: pixel row j (0..3) of the wave, kernel depth dz (0..2; m & 3 == 3 stays zero),
+//   K           = 18 voxel slots (input row r = 0..5 relative to the wave's first row - 1, kx) x 8 channels,
+//                 5 chunks of 32 (slots 18, 19 are zero weights),
+//   A[m][r,kx,c] = W[c][dz][ky = r - j][kx] when 0 <= ky <= 2 (pack_prob_rows, capi.cpp).
+// Lane group g of a B fragment is one slot = one 16-byte voxel read from LDS (16 lanes: 256 contiguous bytes).
+// The fp32 weights enter as three bf16 terms (hi, mid, lo: 24 mantissa bits) and bf16 x bf16 products are exact,
+// so the logits are the fp32 conv up to summation order. Lane (n, g) then holds rows 4g .. 4g+3 = pixel row g,
+// column n, partial logits of kernel depth 0, 1, 2: exactly the three sums prob_regress_kernel slides over the
+// planes; the same lane keeps its pixel's two open logits and later runs that pixel's regression from the LDS
+// logit column. Per plane and wave: 2 staging loads, 5 ds_read_b128 and 15 MFMAs (the VALU kernel: 118
+// packed FMAs per voxel).
+constexpr int kPRChunks = kProbRowChunks, kPRTerms = kProbRowTerms;
+constexpr int kPRVox = kHY * kHX;  // 340 staged voxels per plane
+constexpr int kPRAhead = 4;        // input planes in flight per block
 
-__global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int w, int tiles_x,
-                                                        const bf16_t* __restrict__ feat, const uint4* __restrict__ apack,
+__global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int w, const bf16_t* __restrict__ feat,
+                                                        const uint4* __restrict__ apack,
                                                         const float* __restrict__ prob_init,
                                                         const float* __restrict__ hyps, float* __restrict__ depth,
                                                         float* __restrict__ conf, float* __restrict__ var,
                                                         float* __restrict__ prob) {
-  __shared__ float lg[64 * 64];  // [plane][pixel of the block]
-  const int tx = blockIdx.x % tiles_x, yb = blockIdx.x / tiles_x;
-  const int y = yb % h, b = yb / h;
-  const int x0 = tx * 64;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint4* tile = reinterpret_cast<uint4*>(smem);                 // 2 x 340 voxels (double buffer)
+  float* lg = reinterpret_cast<float*>(tile + 2 * kPRVox);      // [D - 1][256] logits, column per pixel
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, g = lane >> 4;
-  const int d0 = wave * 16;
-  const __amdgpu_buffer_rsrc_t rf = make_rsrc(feat, (long long)B * D * h * w * 8 * 2);
-  const uint4* ap = apack + lane;
-  f32x4_t acc[kPR];
+  const int y0 = blockIdx.y * kTY, x0 = blockIdx.x * kTX;
+  const int b = blockIdx.z;
+  const int R0 = 4 * (wave >> 1), C0 = 16 * (wave & 1);
+  const int pix = (R0 + g) * kTX + C0 + n;  // this lane's pixel in the tile: its logit column
+  const __amdgpu_buffer_rsrc_t rf = make_rsrc(feat, (long long)B * D * h * w * 16);
+
+  uint4 af[kPRChunks][kPRTerms];
 #pragma unroll
-  for (int r = 0; r < kPR; ++r) acc[r] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  auto fetch = [&](int s, uint4& ah, uint4& al, uint4* xb) {
-    ah = ap[(size_t)(2 * s) * 64];
-    al = ap[(size_t)(2 * s + 1) * 64];
-    const int tp = s * 4 + g;  // this lane group's tap
-    const int rr = tp / 9, t9 = tp - rr * 9;
-    const int iz = d0 - 1 + rr, yy = y + t9 / 3 - 1, dx = t9 % 3 - 1;
-    const bool okz = tp < 18 * 9 && (unsigned)iz < (unsigned)D && (unsigned)yy < (unsigned)h;
-    const int rowbase = ((b * D + iz) * h + yy) * w;
+  for (int k = 0; k < kPRChunks; ++k)
 #pragma unroll
-    for (int r = 0; r < kPR; ++r) {
-      const int xx = x0 + r * 16 + n + dx;
-      const bool ok = okz && (unsigned)xx < (unsigned)w;
-      xb[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rf, ok ? (uint32_t)(rowbase + xx) * 16u : kOOB, 0, 0));
-    }
+    for (int t = 0; t < kPRTerms; ++t) af[k][t] = apack[(k * kPRTerms + t) * 64 + lane];
+  int boff[kPRChunks];  // LDS voxel of this lane's slot in every chunk
+#pragma unroll
+  for (int k = 0; k < kPRChunks; ++k) {
+    const int sl = 4 * k + g, slc = sl < 18 ? sl : 17;
+    boff[k] = (R0 + slc / 3) * kHX + C0 + n + slc % 3;
+  }
+  const bool bpad = g >= 2;  // chunk 4: slots 18, 19
+
+  // staging: voxel v = tid, tid + 256 (< 340) of the halo tile
+  uint32_t goff[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int v = tid + 256 * k, row = v / kHX, col = v - row * kHX;
+    const int yy = y0 - 1 + row, xx = x0 - 1 + col;
+    const bool ok = v < kPRVox && (unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w;
+    goff[k] = ok ? (uint32_t)(((size_t)b * D * h + yy) * w + xx) * 16u : kOOB;
+  }
+  // Input planes are fetched kPRAhead planes ahead into a register ring (the per-plane work is ~20 instructions:
+  // one fetch in flight per block left every plane waiting out a full memory latency); fetches past the last plane
+  // are out-of-range buffer loads (no traffic, but counted like the others, so the wait counts stay static).
+  const uint32_t pstride = (uint32_t)h * w * 16u;
+  uint4 ring[kPRAhead][2];
+  auto gload = [&](int pl, uint4 (&st)[2]) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      st[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rf, goff[k] == kOOB || pl >= D ? kOOB : goff[k] + (uint32_t)pl * pstride, 0, 0));
   };
-  // only input planes d0 - 1 .. min(d0 + 16, D - 1) exist: skip the chunks past them (D = 8: 21 of 41)
-  const int nplanes = min(18, D - d0 + 1);
-  const int nch = min(kProbChunks, (nplanes * 9 + 3) / 4);
-  uint4 ah, al, xb[kPR];
-  fetch(0, ah, al, xb);
-  for (int s = 0; s < nch; ++s) {
-    uint4 nh, nl, nb[kPR];
-    if (s + 1 < nch) fetch(s + 1, nh, nl, nb);
+  auto lstore = [&](int bi, const uint4 (&st)[2]) {
+    tile[bi * kPRVox + tid] = st[0];
+    if (tid + 256 < kPRVox) tile[bi * kPRVox + tid + 256] = st[1];
+  };
+
 #pragma unroll
-    for (int r = 0; r < kPR; ++r) {
-      acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ah), __builtin_bit_cast(bf16x8_t, xb[r]),
-                                                       acc[r], 0, 0, 0);
-      acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, al), __builtin_bit_cast(bf16x8_t, xb[r]),
-                                                       acc[r], 0, 0, 0);
-    }
-    if (s + 1 < nch) {
-      ah = nh;
-      al = nl;
+  for (int u = 0; u < kPRAhead; ++u) gload(u, ring[u]);
+  lstore(0, ring[0]);
+  gload(kPRAhead, ring[0]);
+  __syncthreads();
+  float am1 = 0.f, a0 = 0.f;
+  for (int pl0 = 0; pl0 < D; pl0 += kPRAhead) {
 #pragma unroll
-      for (int r = 0; r < kPR; ++r) xb[r] = nb[r];
+    for (int u = 0; u < kPRAhead; ++u) {
+      const int pl = pl0 + u;
+      if (pl >= D) break;
+      const uint4* tb = tile + (pl & 1) * kPRVox;
+      f32x4_t acc[kPRTerms];
+#pragma unroll
+      for (int t = 0; t < kPRTerms; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < kPRChunks; ++k) {
+        uint4 bv = tb[boff[k]];
+        if (k == kPRChunks - 1 && bpad) bv = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int t = 0; t < kPRTerms; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[k][t]),
+                                                           __builtin_bit_cast(bf16x8_t, bv), acc[t], 0, 0, 0);
+      }
+      const f32x4_t sum = acc[0] + (acc[1] + acc[2]);  // hi + (mid + lo)
+      if (pl >= 1) lg[(pl - 1) * 256 + pix] = am1 + sum[2];
+      am1 = a0 + sum[1];
+      a0 = sum[0];
+      const int un = (u + 1) % kPRAhead;  // ring slot of plane pl + 1 (pl0 is a multiple of kPRAhead)
+      lstore((pl + 1) & 1, ring[un]);  // past the last plane: zeros into the idle buffer
+      gload(pl + 1 + kPRAhead, ring[un]);
+      __syncthreads();
     }
   }
-  // lane (n, g) holds planes d0 + 4g .. +3 of pixel r * 16 + n
-  const size_t hw = (size_t)h * w;
+  float last = am1;  // plane D - 1
+
+  const int y = y0 + R0 + g, x = x0 + C0 + n;
+  if (y >= h || x >= w) return;
+  const size_t hw = (size_t)h * w, p = (size_t)y * w + x;
+  const float* hy = hyps + (size_t)b * D * hw + p;
+  const float* pin = prob_init ? prob_init + (size_t)b * D * hw + p : nullptr;
+  float* lcol = lg + pix;
+  auto col = [&](int d) -> float& { return d == D - 1 ? last : lcol[d * 256]; };
+  if (pin)
+    for (int d = 0; d < D; ++d) col(d) += pin[(size_t)d * hw];
+  float mx = -INFINITY;
+  for (int d = 0; d < D; ++d) mx = fmaxf(mx, col(d));
+  float sm = 0.f;
+  for (int d = 0; d < D; ++d) {
+    const float e = expf(col(d) - mx);
+    col(d) = e;
+    sm += e;
+  }
+  // hypothesis loads in groups of 8 ahead of their use (one memory latency per group, not per plane)
+  float dep = 0.f, idx = 0.f;
+  for (int d0 = 0; d0 < D; d0 += 8) {
+    float hv[8];
 #pragma unroll
-  for (int r = 0; r < kPR; ++r)
+    for (int i = 0; i < 8; ++i) hv[i] = d0 + i < D ? hy[(size_t)(d0 + i) * hw] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int d = d0 + 4 * g + i, px = r * 16 + n, x = x0 + px;
+    for (int i = 0; i < 8; ++i) {
+      const int d = d0 + i;
       if (d < D) {
-        float l = acc[r][i];
-        if (prob_init && x < w) l += prob_init[((size_t)b * D + d) * hw + (size_t)y * w + x];
-        lg[d * 64 + px] = l;
+        const float pr = col(d) / sm;
+        col(d) = pr;
+        dep += pr * hv[i];
+        idx += pr * (float)d;
       }
     }
-  __syncthreads();
-  const int t = threadIdx.x, x = x0 + t;
-  if (t >= 64 || x >= w) return;
-  const size_t pix = (size_t)y * w + x;
-  const float* hy = hyps + (size_t)b * D * hw + pix;
-  float* lcol = lg + t;
-  float mx = -INFINITY;
-  for (int d = 0; d < D; ++d) mx = fmaxf(mx, lcol[d * 64]);
-  float sum = 0.f;
-  for (int d = 0; d < D; ++d) {
-    const float e = expf(lcol[d * 64] - mx);
-    lcol[d * 64] = e;
-    sum += e;
-  }
-  float dep = 0.f, idx = 0.f;
-  for (int d = 0; d < D; ++d) {
-    const float pr = lcol[d * 64] / sum;
-    lcol[d * 64] = pr;
-    dep += pr * hy[(size_t)d * hw];
-    idx += pr * (float)d;
   }
   int ii = (int)idx;
   ii = ii < 0 ? 0 : (ii > D - 1 ? D - 1 : ii);
   float c = 0.f, vs = 0.f;
-  float* po = prob ? prob + (size_t)b * D * hw + pix : nullptr;
-  for (int d = 0; d < D; ++d) {
-    const float pr = lcol[d * 64];
-    const float df = hy[(size_t)d * hw] - dep;
-    vs += df * df * pr;
-    if (d >= ii - 1 && d <= ii + 2) c += pr;
-    if (po) po[(size_t)d * hw] = pr;
+  float* po = prob ? prob + (size_t)b * D * hw + p : nullptr;
+  for (int d0 = 0; d0 < D; d0 += 8) {
+    float hv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) hv[i] = d0 + i < D ? hy[(size_t)(d0 + i) * hw] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int d = d0 + i;
+      if (d < D) {
+        const float pr = col(d);
+        const float df = hv[i] - dep;
+        vs += df * df * pr;
+        if (d >= ii - 1 && d <= ii + 2) c += pr;
+        if (po) po[(size_t)d * hw] = pr;
+      }
+    }
   }
-  depth[(size_t)b * hw + pix] = dep;
-  conf[(size_t)b * hw + pix] = c;
-  var[(size_t)b * hw + pix] = 3.f * sqrtf(vs);
+  depth[(size_t)b * hw + p] = dep;
+  conf[(size_t)b * hw + p] = c;
+  var[(size_t)b * hw + p] = 3.f * sqrtf(vs);
 }
 
 template <typename T, int CB>
@@ -478,25 +534,29 @@ hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float
 
 namespace damvs {
 
+size_t prob_mfma_smem(int D) { return 2 * (size_t)kPRVox * 16 + (size_t)(D > 0 ? D - 1 : 0) * 256 * 4; }
+
 hipError_t launch_prob_mfma(hipStream_t s, int B, int D, int h, int w, const void* feat, const void* apack,
                             const float* prob_init, const float* hyps, float* depth, float* conf, float* var,
                             float* prob) {
-  if (D < 1 || D > 64) return hipErrorInvalidValue;
-  if ((long long)B * D * h * w * 16 >= (1LL << 32)) return hipErrorInvalidValue;  // 32-bit buffer offsets
-  const int tiles_x = (w + 63) / 64, ngroups = (D + 15) / 16;
-  const long long nblk = (long long)tiles_x * h * B;
-  hipLaunchKernelGGL(prob_mfma_kernel, dim3((unsigned)nblk), dim3(64 * ngroups), 0, s, B, D, h, w, tiles_x,
-                     reinterpret_cast<const bf16_t*>(feat), reinterpret_cast<const uint4*>(apack), prob_init, hyps,
-                     depth, conf, var, prob);
+  const size_t smem = prob_mfma_smem(D);
+  if (D < 1 || smem > 160 * 1024) return hipErrorInvalidValue;
+  if ((long long)B * D * h * w * 16 >= (1LL << 32) - 16) return hipErrorInvalidValue;  // 32-bit buffer offsets
+  if (smem > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(prob_mfma_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+  }
+  const dim3 grid((w + kTX - 1) / kTX, (h + kTY - 1) / kTY, B);
+  hipLaunchKernelGGL(prob_mfma_kernel, grid, dim3(256), smem, s, B, D, h, w, reinterpret_cast<const bf16_t*>(feat),
+                     reinterpret_cast<const uint4*>(apack), prob_init, hyps, depth, conf, var, prob);
   return hipGetLastError();
 }
 
-// The banded-MFMA prob conv runs only with DAMVS_PROB_MFMA=1 (read per call: tests flip it): since the
-// VALU prob_regress widens its tiles once per voxel and runs packed FMAs it is as fast at D = 32-48
-// (stage-1/2 forwards 2.93 / 4.92 ms against 2.99 / 5.01 at B=4) and keeps the exact fp32 weights.
+// DAMVS_PROB_MFMA=0 (read per call: tests flip it) sends bf16 stages to the VALU prob_regress_kernel.
 bool prob_mfma_disabled() {
   const char* v = getenv("DAMVS_PROB_MFMA");
-  return !(v && v[0] == '1');
+  return v && v[0] == '0';
 }
 
 }  // namespace damvs

@@ -162,39 +162,47 @@ def test_block_channels_is_the_blocked_permutation(C, dtype):
         assert torch.equal(got, src.view(B, h, w, C // E, E).permute(0, 3, 1, 2, 4).contiguous())
 
 
-@pytest.mark.parametrize("s,D", [(0, 48), (1, 32), (0, 64)])
-def test_prob_mfma_vs_split_path(s, D, monkeypatch):
-    """bf16 stage forward (banded-MFMA prob conv + regression, k_regress.hip; opt-in DAMVS_PROB_MFMA=1)
-    against the split path on the same U-Net output (damvs_costreg_logits: fp32-weight VALU prob conv,
-    then damvs_regress): they differ only in the prob conv's weight split (bf16 hi + lo) and summation
-    order."""
-    monkeypatch.setenv("DAMVS_PROB_MFMA", "1")
+@pytest.mark.parametrize("s,D,W", [(0, 48, 80), (1, 32, 80), (0, 64, 80), (2, 8, 72), (1, 16, 104)])
+@pytest.mark.parametrize("with_init", [False, True])
+def test_prob_mfma_vs_split_path(s, D, W, with_init):
+    """bf16 stage regression (prob conv on MFMA + regression, prob_mfma_kernel in k_regress.hip: the default for
+    bf16 storage) against the split path on the same U-Net output (damvs_costreg_logits: fp32-weight VALU prob
+    conv, then damvs_regress). The MFMA form carries the fp32 weights as three bf16 terms and the bf16 voxels
+    exactly, so the two differ only in summation order. W = 72 / 104 leave ragged 32-pixel tiles; with_init adds
+    a prob_volume_init (models/cas_mvsnet.py:107-108) to the logits."""
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import StageEngine, regress
     C = (32, 16, 8)[s]
     net = CascadeMVSNet(ndepths=[48, 32, 8])
     net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
-    feats, P, hyps = depthnet_inputs(B=2, N=3, H=32, W=80, D=D, stage_idx=s, C=C)
+    feats, P, hyps = depthnet_inputs(B=2, N=3, H=32, W=W, D=D, stage_idx=s, C=C)
     eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.bfloat16,
                       torch.device(DEV))
     nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats]
-    depth, conf, var, prob = eng.forward(nhwc, cuda(P), cuda(hyps))
-    logits = eng.costreg_logits(eng.warp_aggregate(nhwc, cuda(P), cuda(hyps)))
-    d2, c2, v2, p2 = regress(logits, cuda(hyps))
-    assert rel_max(np_(depth), np_(d2)) < 1e-4
+    hyps = cuda(hyps)
+    logits = eng.costreg_logits(eng.warp_aggregate(nhwc, cuda(P), hyps))
+    init = None
+    if with_init:
+        g = torch.Generator().manual_seed(D)
+        init = cuda(torch.randn(logits.shape, generator=g))
+    depth, conf, var, prob = eng.forward(nhwc, cuda(P), hyps, prob_init=init)
+    d2, c2, v2, p2 = regress(logits + init if with_init else logits, hyps)
+    assert rel_max(np_(depth), np_(d2)) < 2e-6
     m = conf_mask_pair(np_(prob), np_(p2))  # the window index floor(sum p*i) may flip elsewhere
-    assert m.mean() > 0.9
-    assert np.abs(np_(conf) - np_(c2))[m].max() < 2e-3
-    assert np.abs(np_(prob) - np_(p2)).max() < 2e-3
-    assert rel_max(np_(var), np_(v2)) < 2e-2
+    assert m.mean() > 0.99
+    assert np.abs(np_(conf) - np_(c2))[m].max() < 2e-5
+    assert np.abs(np_(prob) - np_(p2)).max() < 2e-5
+    assert rel_max(np_(var), np_(v2)) < 1e-3
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("D,W", [(8, 40), (8, 72), (16, 40)])
-def test_prob_regress_fused_vs_split_path(D, W, dtype):
+def test_prob_regress_fused_vs_split_path(D, W, dtype, monkeypatch):
     """The fused prob conv + regression (prob_regress_kernel: logits in an LDS column) against the split
     path on the same U-Net output (the same LDS-tiled prob conv writing logits to HBM, then regress_kernel):
-    identical arithmetic, so equal to fp32 rounding noise. W = 72 leaves a ragged 32-pixel tile."""
+    identical arithmetic, so equal to fp32 rounding noise. W = 72 leaves a ragged 32-pixel tile. bf16 storage
+    defaults to the MFMA form (test_prob_mfma_vs_split_path); DAMVS_PROB_MFMA=0 keeps it on this kernel."""
+    monkeypatch.setenv("DAMVS_PROB_MFMA", "0")
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import StageEngine, regress
     net = CascadeMVSNet(ndepths=[48, 32, 8])
