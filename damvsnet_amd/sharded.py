@@ -13,7 +13,8 @@ Per stage (DepthNet.forward, models/cas_mvsnet.py:18-134), on rank r of P:
 3. CostRegNet (models/module.py:510-541) on the haloed slab, layer by layer. Halos of 8 / 4 / 2 / 1 rows at levels
    0-3 keep the stride-2 row parity of every level aligned with the whole-image U-Net, so each layer is the
    whole-tensor kernel unchanged (damvs_costreg_layer); after every layer the halo rows are refreshed from the
-   neighbouring slabs (P2P) and zeroed outside the image (the whole-image convolution's zero padding).
+   neighbouring slabs (P2P) and zeroed outside the image (the whole-image convolution's zero padding). The batch
+   runs as two halves so one half's halo transfer overlaps the other half's layer (_costreg_sharded).
 4. Prob conv + softmax regression (models/cas_mvsnet.py:105-124) locally: the softmax is over D, per pixel.
 5. All-gather of the slabs' depth / confidence / variance rows (and prob volume), one collective
    (all_gather_into_tensor over RCCL) of slabs padded to the tallest: every rank then holds the stage output, which
@@ -77,11 +78,33 @@ class Comm:
     def exchange(self, ops):
         raise NotImplementedError
 
+    def exchange_start(self, ops):
+        """Start ``exchange(ops)``; the returned handle's ``wait()`` completes it (stream-ordered for device tensors).
+        Communicators without asynchronous transfers complete it here."""
+        self.exchange(ops)
+        return _Done()
+
     def all_gather(self, t):
         """Every rank's ``t`` (one shape on all ranks) as a list indexed by rank."""
         outs = [torch.empty_like(t) for _ in range(self.world)]
         self.exchange([(q, t, outs[q]) for q in range(self.world)])
         return outs
+
+
+class _Done:
+    def wait(self):
+        pass
+
+
+class _TorchPending:
+    def __init__(self, works, back):
+        self.works, self.back = works, back
+
+    def wait(self):
+        for work in self.works:
+            work.wait()  # NCCL / RCCL: the current stream waits for the transfer (the host does not block)
+        for dst, src in self.back:
+            dst.copy_(src)
 
 
 class TorchComm(Comm):
@@ -95,6 +118,9 @@ class TorchComm(Comm):
         self._host = dist.get_backend() == "gloo"
 
     def exchange(self, ops):
+        self.exchange_start(ops).wait()
+
+    def exchange_start(self, ops):
         dist = self._dist
         p2p, back = [], []
         for peer, send, recv in ops:
@@ -110,11 +136,7 @@ class TorchComm(Comm):
                     r = torch.empty(recv.shape, dtype=recv.dtype)
                     back.append((recv, r))
                 p2p.append(dist.P2POp(dist.irecv, r, peer))
-        if p2p:
-            for work in dist.batch_isend_irecv(p2p):
-                work.wait()
-        for dst, src in back:
-            dst.copy_(src)
+        return _TorchPending(dist.batch_isend_irecv(p2p) if p2p else [], back)
 
     def all_gather(self, t):
         """One collective: all_gather_into_tensor (RCCL ring over xGMI) into a [world, ...] buffer; gloo gathers
@@ -185,9 +207,9 @@ class ThreadComm(Comm):
 
 # ----------------------------------------------------------------------------- one sharded stage
 
-def _halo_exchange(comm: Comm, t: torch.Tensor, hl: int):
-    """Refresh the hl-row halos of a slab tensor [B][D][rows][w][C] from the neighbouring slabs; zero the halo
-    rows that lie outside the image (first / last rank)."""
+def _halo_start(comm: Comm, t: torch.Tensor, hl: int):
+    """Start refreshing the hl-row halos of a slab tensor [B][D][rows][w][C] from the neighbouring slabs; the
+    returned callable completes it (and zeroes the halo rows that lie outside the image: first / last rank)."""
     r, P = comm.rank, comm.world
     R = t.shape[2]
     ops, top, bot = [], None, None
@@ -197,16 +219,38 @@ def _halo_exchange(comm: Comm, t: torch.Tensor, hl: int):
     if r < P - 1:
         bot = torch.empty_like(t[:, :, :hl])
         ops.append((r + 1, t[:, :, R - 2 * hl:R - hl].contiguous(), bot))
-    if ops:
-        comm.exchange(ops)
-    if top is None:
-        t[:, :, :hl].zero_()
-    else:
-        t[:, :, :hl].copy_(top)
-    if bot is None:
-        t[:, :, R - hl:].zero_()
-    else:
-        t[:, :, R - hl:].copy_(bot)
+    pending = comm.exchange_start(ops) if ops else _Done()
+
+    def finish():
+        pending.wait()
+        del ops[:]  # the staged send buffers live until the transfer has completed
+        if top is None:
+            t[:, :, :hl].zero_()
+        else:
+            t[:, :, :hl].copy_(top)
+        if bot is None:
+            t[:, :, R - hl:].zero_()
+        else:
+            t[:, :, R - hl:].copy_(bot)
+    return finish
+
+
+def _costreg_sharded(comm: Comm, eng, vol, c, D: int, R: int, w: int):
+    """The U-Net on the haloed slab with each layer's halo exchange overlapped: the batch runs as two halves, and
+    a half's halo transfer is in flight while the other half's layer computes (the next layer of a half waits
+    only for that half's halos). Same kernels per voxel as one whole-batch launch: identical results."""
+    B = vol.shape[0]
+    halves = [(0, B // 2), (B // 2, B)] if B >= 2 else [(0, B)]
+    pending = [None] * len(halves)
+    for layer, src, dst, level in _STEPS:
+        for i, (b0, b1) in enumerate(halves):
+            if pending[i] is not None:
+                pending[i]()  # this half's halos of the previous layer's output
+            x = vol if src == "v" else c[src]
+            eng.unet_layer(layer, D, R, w, x[b0:b1], c[dst][b0:b1])
+            pending[i] = _halo_start(comm, c[dst][b0:b1], HALO >> level)
+    for fin in pending:
+        fin()
 
 
 def sharded_stage(comm: Comm, eng, feats, layout, rt, hyps, h: int, w: int, warp: str = "depth",
@@ -265,10 +309,7 @@ def sharded_stage(comm: Comm, eng, feats, layout, rt, hyps, h: int, w: int, warp
 
     hook("costreg")
     c = eng.unet_buffers(B, D, R, w)
-    for layer, src, dst, level in _STEPS:
-        x = vol if src == "v" else c[src]
-        eng.unet_layer(layer, D, R, w, x, c[dst])
-        _halo_exchange(comm, c[dst], HALO >> level)
+    _costreg_sharded(comm, eng, vol, c, D, R, w)
 
     hook("regress")
     depth, conf, var, prob = eng.regress_c0(c[0], hyps_s, want_prob=want_prob)

@@ -138,12 +138,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _gloo_worker(rank, world, port, warp, q):
+def _gloo_worker(rank, world, port, warp, q, B=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        case = _case()
+        case = _case(B=B)
+        if B > 1:
+            case[3][1] *= 1.03  # distinct samples
         got = _run_sharded(S.TorchComm(), case, warp)
         if rank == world - 1:
             ref = _unsharded(*case)
@@ -218,13 +220,14 @@ def test_gloo_world2_whole_cascade_every_stage_sharded():
 
 
 @pytest.mark.timeout(180)
-@pytest.mark.parametrize("world,warp", [(2, "depth"), (3, "depth"), (3, "rows")])
-def test_gloo_world_matches_unsharded(world, warp):
-    """Real torch.distributed P2P (gloo, one process per rank): all-to-all, halo exchange, all-gather."""
+@pytest.mark.parametrize("world,warp,B", [(2, "depth", 1), (3, "depth", 1), (3, "rows", 1), (2, "depth", 2)])
+def test_gloo_world_matches_unsharded(world, warp, B):
+    """Real torch.distributed P2P (gloo, one process per rank): all-to-all, halo exchange, all-gather. B = 2 runs the
+    U-Net as two batch halves with each half's halo transfer outstanding while the other half computes."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, warp, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, warp, q, B)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
