@@ -49,6 +49,7 @@ class HipConv2d:
         check(lib.damvs_conv2d_create(ctypes.byref(d), ptr(w), ptr(b), DTYPES[dtype], ctypes.byref(h)))
         self.handle, self.dtype, self.ngeo = h, dtype, len(geo_at)
         self.desc = "%s k%d s%d" % ("convT" if tr else "conv", d.kernel, d.stride)
+        self.kernel, self.stride, self.transposed = d.kernel, d.stride, tr
         self.cout = cout
         self.cout_store = (cout + 3) // 4 * 4
 

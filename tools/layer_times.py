@@ -2,7 +2,9 @@
 
 Each damvs_conv2d layer call is bracketed by HIP events on the current stream after a warm forward; the
 table lists ms per call with the layer's shape (kernel, stride, transposed, cin c0+c1(+geo), cout,
-input H x W, B). Synchronous per layer (no overlap): a profile aid, not the bench number.
+input H x W, B), its algorithmic TFLOP/s and GB/s (tensor inputs + fp32 planes + output; residuals not counted)
+and its roofline fraction max(FLOPs / 2.5 PFLOP/s, bytes / 8 TB/s) / time. Synchronous per layer (no overlap): a
+profile aid, not the bench number.
   python tools/layer_times.py [--config cfgC] [--batch 4] [--top 40]
 """
 import argparse
@@ -58,16 +60,28 @@ def main():
         torch.cuda.synchronize()
     rows = []
     agg = collections.defaultdict(float)
+    ideal = collections.defaultdict(float)
+    flops_g = collections.defaultdict(float)
     for lab, L, B, Hi, Wi, in0, in1, ng, oshape, e0, e1 in rec:
         ms = e0.elapsed_time(e1)
         c0 = in0.shape[-1] if in0 is not None else 0
         c1 = in1.shape[-1] if in1 is not None else 0
+        cin = c0 + c1 + ng
+        px = B * Hi * Wi if L.transposed else B * oshape[1] * oshape[2]  # a transposed conv scatters k^2 taps per input
+        flops = 2.0 * px * cin * L.cout * L.kernel * L.kernel
+        byts = 2.0 * B * Hi * Wi * (c0 + c1) + 4.0 * B * Hi * Wi * ng + 2.0 * B * oshape[1] * oshape[2] * oshape[3]
+        t_roof = max(flops / 2.5e15, byts / 8e12) * 1e3  # ms
         rows.append((ms, lab, "%s %dx%d->%dx%d B%d cin %d+%d+g%d cout %d" % (L.desc, Hi, Wi, oshape[1], oshape[2], B, c0,
-                                                                            c1, ng, L.cout)))
+                                                                            c1, ng, L.cout),
+                     flops / ms / 1e9, byts / ms / 1e6, t_roof / ms))
         agg[lab] += ms
+        ideal[lab] += t_roof
+        flops_g[lab] += flops
     print("per group (ms):", {k: round(v, 3) for k, v in agg.items()}, "total %.3f" % sum(agg.values()))
-    for ms, lab, desc in sorted(rows, reverse=True)[:args.top]:
-        print("%8.3f ms  %-14s %s" % (ms, lab, desc))
+    print("per group roofline ms (max(FLOPs/2.5PF, bytes/8TB/s) per layer):", {k: round(v, 3) for k, v in ideal.items()},
+          "TFLOP/s:", {k: round(flops_g[k] / agg[k] / 1e9, 1) for k in agg})
+    for ms, lab, desc, tf, gb, fr in sorted(rows, reverse=True)[:args.top]:
+        print("%8.3f ms  %-14s %-58s %7.1f TFLOP/s %7.0f GB/s  roofline %.2f" % (ms, lab, desc, tf, gb, fr))
 
 
 if __name__ == "__main__":
