@@ -519,7 +519,7 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
     // pack_prob_rows: the prob conv (Conv3d(8, 1, k3), models/module.py:530) as prob_mfma_kernel's A operand
     // (k_regress.hip): rows m = 4 j + dz (output pixel row j of four, kernel depth dz), K = (voxel slot
     // sl = 3 r + kx of input row r = 0..5, channel), entry W[c][dz][ky = r - j][kx] when dz < 3, sl < 18 and
-    // 0 <= ky <= 2, else 0; [chunk][term][lane][8], the fp32 weight as three bf16 terms hi + mid + lo.
+    // 0 <= ky <= 2, else 0; [chunk][term][lane][8], the fp32 weight as kProbRowTerms bf16 terms (hi + lo).
     std::vector<uint16_t> pk((size_t)kProbRowChunks * kProbRowTerms * 64 * 8, 0);
     for (int k = 0; k < kProbRowChunks; ++k)
       for (int lane = 0; lane < 64; ++lane)

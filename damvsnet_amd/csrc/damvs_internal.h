@@ -170,7 +170,10 @@ hipError_t launch_prob_regress(hipStream_t s, int store, int B, int Cb, int D, i
                                float* conf, float* var, float* prob);
 size_t prob_regress_smem_bytes(int store, int Cb, int D);
 // MFMA prob conv + regression (bf16 storage, base 8; LDS bounds D): apack from pack_prob_rows (capi.cpp)
-constexpr int kProbRowChunks = 5, kProbRowTerms = 3;  // prob_mfma_kernel: 18 voxel slots x 8 channels, 3 bf16 terms
+#ifndef DAMVS_PROB_TERMS
+#define DAMVS_PROB_TERMS 2  // bf16 terms per fp32 prob-conv weight (3: exact fp32 weights; A/B builds)
+#endif
+constexpr int kProbRowChunks = 5, kProbRowTerms = DAMVS_PROB_TERMS;  // prob_mfma_kernel: 18 voxel slots x 8 channels
 hipError_t launch_prob_mfma(hipStream_t s, int B, int D, int h, int w, const void* feat, const void* apack,
                             const float* prob_init, const float* hyps, float* depth, float* conf, float* var,
                             float* prob);

@@ -285,15 +285,20 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
 //                 5 chunks of 32 (slots 18, 19 are zero weights),
 //   A[m][r,kx,c] = W[c][dz][ky = r - j][kx] when 0 <= ky <= 2 (pack_prob_rows, capi.cpp).
 // Lane group g of a B fragment is one slot = one 16-byte voxel read from LDS (16 lanes: 256 contiguous bytes).
-// The fp32 weights enter as three bf16 terms (hi, mid, lo: 24 mantissa bits) and bf16 x bf16 products are exact,
-// so the logits are the fp32 conv up to summation order. Lane (n, g) then holds rows 4g .. 4g+3 = pixel row g,
+// The fp32 weights enter as two bf16 terms (hi + lo: ~16 mantissa bits, a relative weight error below 2^-17, far
+// under the 2^-9 rounding of the bf16 activations they multiply; bf16 x bf16 products are exact). Three terms
+// (DAMVS_PROB_TERMS=3: 24 bits, the fp32 conv up to summation order) cost the kernel its fourth wave per SIMD:
+// stage 3 0.50 against 0.42 ms at B=4 (tools/gpu_r03_probab.sh). Lane (n, g) then holds rows 4g .. 4g+3 = pixel row g,
 // column n, partial logits of kernel depth 0, 1, 2: exactly the three sums prob_regress_kernel slides over the
 // planes; the same lane keeps its pixel's two open logits and later runs that pixel's regression from the LDS
-// logit column. Per plane and wave: 2 staging loads, 5 ds_read_b128 and 15 MFMAs (the VALU kernel: 118
+// logit column. Per plane and wave: 2 staging loads, 5 ds_read_b128 and 10 MFMAs (the VALU kernel: 118
 // packed FMAs per voxel).
 constexpr int kPRChunks = kProbRowChunks, kPRTerms = kProbRowTerms;
 constexpr int kPRVox = kHY * kHX;  // 340 staged voxels per plane
-constexpr int kPRAhead = 4;        // input planes in flight per block
+#ifndef DAMVS_PROB_AHEAD
+#define DAMVS_PROB_AHEAD 4  // (A/B builds only)
+#endif
+constexpr int kPRAhead = DAMVS_PROB_AHEAD;  // input planes in flight per block
 
 __global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int w, const bf16_t* __restrict__ feat,
                                                         const uint4* __restrict__ apack,
@@ -374,7 +379,9 @@ __global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[k][t]),
                                                            __builtin_bit_cast(bf16x8_t, bv), acc[t], 0, 0, 0);
       }
-      const f32x4_t sum = acc[0] + (acc[1] + acc[2]);  // hi + (mid + lo)
+      f32x4_t sum = acc[kPRTerms - 1];  // hi + lo (+ mid)
+#pragma unroll
+      for (int t = kPRTerms - 2; t >= 0; --t) sum = acc[t] + sum;
       if (pl >= 1) lg[(pl - 1) * 256 + pix] = am1 + sum[2];
       am1 = a0 + sum[1];
       a0 = sum[0];

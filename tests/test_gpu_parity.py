@@ -167,9 +167,9 @@ def test_block_channels_is_the_blocked_permutation(C, dtype):
 def test_prob_mfma_vs_split_path(s, D, W, with_init):
     """bf16 stage regression (prob conv on MFMA + regression, prob_mfma_kernel in k_regress.hip: the default for
     bf16 storage) against the split path on the same U-Net output (damvs_costreg_logits: fp32-weight VALU prob
-    conv, then damvs_regress). The MFMA form carries the fp32 weights as three bf16 terms and the bf16 voxels
-    exactly, so the two differ only in summation order. W = 72 / 104 leave ragged 32-pixel tiles; with_init adds
-    a prob_volume_init (models/cas_mvsnet.py:107-108) to the logits."""
+    conv, then damvs_regress). The MFMA form multiplies the bf16 voxels exactly by the fp32 weights carried as two
+    bf16 terms (relative weight error < 2^-17); W = 72 / 104 leave ragged 32-pixel tiles; with_init adds a
+    prob_volume_init (models/cas_mvsnet.py:107-108) to the logits."""
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import StageEngine, regress
     C = (32, 16, 8)[s]
@@ -187,12 +187,14 @@ def test_prob_mfma_vs_split_path(s, D, W, with_init):
         init = cuda(torch.randn(logits.shape, generator=g))
     depth, conf, var, prob = eng.forward(nhwc, cuda(P), hyps, prob_init=init)
     d2, c2, v2, p2 = regress(logits + init if with_init else logits, hyps)
-    assert rel_max(np_(depth), np_(d2)) < 2e-6
+    errs = (rel_max(np_(depth), np_(d2)), float(np.abs(np_(prob) - np_(p2)).max()), rel_max(np_(var), np_(v2)))
+    print("prob_mfma vs split: depth rel %.2e, prob abs %.2e, var rel %.2e" % errs)
+    assert errs[0] < 5e-6  # measured <= 1.0e-6 (prob abs <= 2.2e-5, var rel <= 1.8e-5) over these cases
     m = conf_mask_pair(np_(prob), np_(p2))  # the window index floor(sum p*i) may flip elsewhere
     assert m.mean() > 0.99
-    assert np.abs(np_(conf) - np_(c2))[m].max() < 2e-5
-    assert np.abs(np_(prob) - np_(p2)).max() < 2e-5
-    assert rel_max(np_(var), np_(v2)) < 1e-3
+    assert np.abs(np_(conf) - np_(c2))[m].max() < 1e-4
+    assert errs[1] < 1e-4
+    assert errs[2] < 1e-4
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
