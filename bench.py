@@ -338,7 +338,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--frontend", default="hip", choices=["hip", "torch"], help="2D front-end implementation")
     ap.add_argument("--cpu-budget", type=float, default=60.0)
-    ap.add_argument("--shard", choices=["depth", "rows"], default=None,
+    ap.add_argument("--shard", choices=["depth", "rows", "gather"], default=None,
                     help="measure the depth-sharded latency mode (one map over all ranks) instead of replicas")
     ap.add_argument("--emulate", type=int, default=1, help="with --shard on one GPU: P ranks as threads")
     ap.add_argument("--no-shard-latency", action="store_true",

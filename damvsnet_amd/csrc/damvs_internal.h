@@ -33,6 +33,10 @@ struct WarpArgs {
   // adaptive weight net, BN folded: a = relu(sum_c k1[c] x_c * s1 + t1); wt = relu(a * s2 + t2)
   float k1[32];
   float s1, t1, s2, t2;
+  // pixel-block shape (set by the warp launcher): tile_r = 0 -> a block is ppb consecutive pixels of the row-major
+  // computed rows; else a tile of tile_r rows x ppb / tile_r columns, tiles dealt strip by strip (tile_sw tiles wide,
+  // top to bottom), so the blocks in flight on one XCD cover a compact 2D region of the reference image
+  int tile_r, tile_sw, tiles_x;
 };
 
 // n / d for 0 <= n < 2^31 without a hardware divide: q = (umulhi(n, mul) + n) >> shift.

@@ -14,7 +14,9 @@
 // g = u / ((W-1)/2) - 1 (align-corners style normalisation), then grid_sample's
 // align_corners=False unnormalisation ix = ((g + 1) W - 1) / 2, bilinear, zero padding; the
 // normalise/unnormalise pair is folded algebraically (ix = u W/(W-1) - 1/2).
+#include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "damvs_device.h"
 
@@ -120,6 +122,23 @@ __device__ __forceinline__ Taps bilinear_taps(int h, int w, uint32_t rec, float 
   return t;
 }
 
+// Reference pixel (index into the computed rows) of thread slot i (0 .. ppb - 1) of pixel block pb, -1 outside them.
+__device__ __forceinline__ int warp_pixel(const WarpArgs& a, int pb, int i, int ppb) {
+  if (a.tile_r == 0) {
+    const int p = pb * ppb + i;
+    return p < a.rows * a.w ? p : -1;
+  }
+  const int tc = ppb / a.tile_r;
+  const int tiles_y = (a.rows + a.tile_r - 1) / a.tile_r;
+  const int per_strip = a.tile_sw * tiles_y;
+  const int strip = pb / per_strip, r = pb - strip * per_strip;
+  const int sw = min(a.tile_sw, a.tiles_x - strip * a.tile_sw);
+  const int ty = r / sw, tx = strip * a.tile_sw + (r - ty * sw);
+  const int tr = i / tc;
+  const int x = tx * tc + (i - tr * tc), yl = ty * a.tile_r + tr;
+  return (x < a.w && yl < a.rows) ? yl * a.w + x : -1;
+}
+
 // Work decomposition (locality): a block owns 256 consecutive pixels of one image row band and a
 // chunk of `dchunk` consecutive depth planes, and each thread walks its pixel through those planes.
 // Consecutive hypotheses of one pixel sample along one epipolar segment, so a block's gathers stay
@@ -140,7 +159,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
                                                              int npix_blocks, int dchunk, int ndchunks) {
   constexpr int E = Stor<T>::E, NQ = C / E;
   static_assert(NVC % 2 == 0 || NVC < 0, "the view pipeline alternates two register sets");
-  const int hw = a.h * a.w, ohw = a.rows * a.w;  // feature-map plane, computed rows (y0 .. y0 + rows - 1)
+  const int hw = a.h * a.w;  // feature-map plane (computed rows: y0 .. y0 + rows - 1)
   const int nblk = npix_blocks * ndchunks * a.B;
   const int bid = blockIdx.x, q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
   int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;  // bijective XCD remap
@@ -176,8 +195,8 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
 #else
   const float* __restrict__ cam = cams + (size_t)b * (a.N - 1) * 12;
 #endif
-  const int p = pb * 256 + threadIdx.x;
-  if (p >= ohw) return;
+  const int p = warp_pixel(a, pb, threadIdx.x, 256);
+  if (p < 0) return;
   const int yl = p / a.w, x = p - yl * a.w;
   const int y = a.y0 + yl, pg = y * a.w + x;  // reference-image row and pixel
   const float fx = (float)x, fy = (float)y;
@@ -415,7 +434,7 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
   constexpr int PPB = 256 / S;   // pixels per block
   static_assert(S == 2 || S == 4, "channel-split form: 2 or 4 chunks per pixel");
   static_assert(NVC % 2 == 0 || NVC < 0, "the view pipeline alternates two register sets");
-  const int hw = a.h * a.w, ohw = a.rows * a.w;
+  const int hw = a.h * a.w;
   const int bid = blockIdx.x;
   auto xcd_remap = [](int i, int n) {
     const int q8 = n / 8, r8 = n % 8, x = i % 8;
@@ -427,8 +446,8 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
   const int b = L / npix_blocks;
   const float* __restrict__ cam = cams + (size_t)b * (a.N - 1) * 12;
   const int q = threadIdx.x & (S - 1);                // this lane's channel chunk
-  const int p = pb * PPB + (int)(threadIdx.x / S);    // the S lanes of a pixel are consecutive: they exit together
-  if (p >= ohw) return;
+  const int p = warp_pixel(a, pb, (int)(threadIdx.x / S), PPB);  // the S lanes of a pixel are consecutive: they exit together
+  if (p < 0) return;
   const int yl = p / a.w, x = p - yl * a.w;
   const int y = a.y0 + yl, pg = y * a.w + x;
   const float fx = (float)x, fy = (float)y;
@@ -608,7 +627,7 @@ __global__ __launch_bounds__(256) void warp_pair_kernel(const WarpArgs a, const 
   constexpr int PPB = 256 / S;   // voxels (pixels) per block
   static_assert(CH == 1 || CH == 2 || CH == 4, "corner-pair form: 1, 2 or 4 chunks per pixel");
   static_assert(NVC % 2 == 0 || NVC < 0, "the view pipeline alternates two register sets");
-  const int hw = a.h * a.w, ohw = a.rows * a.w;
+  const int hw = a.h * a.w;
   const int bid = blockIdx.x;
   auto xcd_remap = [](int i, int n) {
     const int q8 = n / 8, r8 = n % 8, x = i % 8;
@@ -621,8 +640,8 @@ __global__ __launch_bounds__(256) void warp_pair_kernel(const WarpArgs a, const 
   const float* __restrict__ cam = cams + (size_t)b * (a.N - 1) * 12;
   const int q = threadIdx.x & (S - 1);
   const int col = q & 1, chunk = q >> 1;
-  const int p = pb * PPB + (int)(threadIdx.x / S);  // the S lanes of a pixel are consecutive: they exit together
-  if (p >= ohw) return;
+  const int p = warp_pixel(a, pb, (int)(threadIdx.x / S), PPB);  // the S lanes of a pixel are consecutive: they exit together
+  if (p < 0) return;
   const int yl = p / a.w, x = p - yl * a.w;
   const int y = a.y0 + yl, pg = y * a.w + x;
   const float fx = (float)x, fy = (float)y;
@@ -893,7 +912,26 @@ hipError_t launch_c(hipStream_t s, const WarpArgs& a0) {
     case 32: lanes = split_lanes<T, 32, BLK>(a); break;
   }
   const int ppb = 256 / lanes;
-  const int npb = (a.rows * a.w + ppb - 1) / ppb;
+  // DAMVS_WARP_TILE="R,SW" (A/B): blocks as R-row tiles dealt in strips SW pixels wide (R divides ppb; default:
+  // ppb consecutive pixels of the row-major computed rows)
+  static const int tile_env[2] = {[] {
+                                    const char* e = getenv("DAMVS_WARP_TILE");
+                                    return e ? atoi(e) : 0;
+                                  }(),
+                                  [] {
+                                    const char* e = getenv("DAMVS_WARP_TILE");
+                                    const char* c = e ? strchr(e, ',') : nullptr;
+                                    return c ? atoi(c + 1) : 0;
+                                  }()};
+  a.tile_r = 0;
+  int npb = (a.rows * a.w + ppb - 1) / ppb;
+  if (tile_env[0] > 0 && ppb % tile_env[0] == 0) {
+    const int tc = ppb / tile_env[0];
+    a.tile_r = tile_env[0];
+    a.tiles_x = (a.w + tc - 1) / tc;
+    a.tile_sw = tile_env[1] >= tc ? std::min(a.tiles_x, tile_env[1] / tc) : a.tiles_x;
+    npb = a.tiles_x * ((a.rows + a.tile_r - 1) / a.tile_r);
+  }
   // depth chunk: as long as possible (locality) while keeping >= ~4 blocks per CU in flight
   int dchunk = a.D;
   static const long long minblk = [] {

@@ -23,6 +23,11 @@ Per stage (DepthNet.forward, models/cas_mvsnet.py:18-134), on rank r of P:
 ``warp="rows"`` builds each rank's haloed slab of the volume directly (damvs_warp_aggregate_rows) and skips the
 all-to-all: the same voxels, with redundant warp work on the halo rows instead of communication.
 
+``warp="gather"`` is north_star's literal partitioning: the D-sharded volumes of step 1 are all-gathered along D
+(one all_gather_into_tensor over RCCL) before the U-Net, which then runs replicated on the whole volume, followed by
+the regression; no further communication. Only the warp is divided by P, the volume crosses xGMI once per rank
+(7/8 of it received at P = 8), and every rank ends with the stage output.
+
 Results equal the unsharded stage: every voxel of the warp and every output of a layer is computed by the same
 kernel arithmetic from the same inputs (tests/test_sharded.py, tests/test_gpu_sharded.py). The front-end
 (FeatureNet, GeoFeatureFusion) and the hypotheses run replicated on every rank.
@@ -263,12 +268,14 @@ def sharded_stage(comm: Comm, eng, feats, layout, rt, hyps, h: int, w: int, warp
     rt      proj_prepare output [B][N-1][12];  hyps: [B][D][h][w] float (every rank)
     Returns (depth, conf, var, prob) whole-image [B][h][w] (prob [B][D][h][w] or None) on every rank."""
     hook = hook or (lambda name: None)
-    if warp not in ("depth", "rows"):
-        raise ValueError("warp must be 'depth' or 'rows'")
+    if warp not in ("depth", "rows", "gather"):
+        raise ValueError("warp must be 'depth', 'rows' or 'gather'")
     r, P = comm.rank, comm.world
     B, D = hyps.shape[:2]
     C = eng.C
     dev, dt = hyps.device, eng.dtype
+    if warp == "gather":
+        return _gathered_stage(comm, eng, feats, layout, rt, hyps, h, w, want_prob, hook)
     ys = slab_rows(h, P)
     y0, y1 = ys[r], ys[r + 1]
     R = (y1 - y0) + 2 * HALO
@@ -328,6 +335,35 @@ def sharded_stage(comm: Comm, eng, feats, layout, rt, hyps, h: int, w: int, warp
     full = torch.cat([got[q][:, :, :ys[q + 1] - ys[q]] for q in range(P)], 2)
     depth, conf, var = full[:, 0].contiguous(), full[:, 1].contiguous(), full[:, 2].contiguous()
     prob = full[:, 3:].contiguous() if want_prob else None
+    hook("end")
+    return depth, conf, var, prob
+
+
+def _gathered_stage(comm: Comm, eng, feats, layout, rt, hyps, h: int, w: int, want_prob: bool, hook):
+    """warp="gather": D-sharded warp, all-gather of the volume along D, U-Net + regression replicated."""
+    r, P = comm.rank, comm.world
+    B, D = hyps.shape[:2]
+    ds = depth_planes(D, P)
+    d0, d1 = ds[r], ds[r + 1]
+    dmax = max(ds[q + 1] - ds[q] for q in range(P))
+    hook("warp")
+    # equal-size buffers for one collective: every shard padded to the deepest, planes outermost so a shard is
+    # one contiguous block ([dmax][B][h][w][C])
+    mine = torch.zeros(dmax, B, h, w, eng.C, device=hyps.device, dtype=eng.dtype)
+    if d1 > d0:
+        part = eng.warp_aggregate(feats, None, hyps[:, d0:d1].contiguous(), rt=rt, layout=layout)
+        mine[:d1 - d0].copy_(part.transpose(0, 1))
+        del part
+    hook("all_gather")
+    got = comm.all_gather(mine)
+    vol = torch.cat([got[q][:ds[q + 1] - ds[q]] for q in range(P)], 0).transpose(0, 1).contiguous()
+    del got, mine
+    hook("costreg")
+    c = eng.unet_buffers(B, D, h, w)
+    for layer, src, dst, _level in _STEPS:
+        eng.unet_layer(layer, D, h, w, vol if src == "v" else c[src], c[dst])
+    hook("regress")
+    depth, conf, var, prob = eng.regress_c0(c[0], hyps, want_prob=want_prob)
     hook("end")
     return depth, conf, var, prob
 

@@ -2,9 +2,10 @@
 
 Tolerances (BASELINE.json north_star: 1e-3 relative on the regressed depth map):
   * fp32 path: per-pixel |depth - ref| / ref <= 1e-3 everywhere; warp/U-Net pieces far tighter.
-  * bf16 path (storage bf16, fp32 accumulate / regression): stated looser gate — mean per-pixel
-    relative depth error <= 1e-2 and p99 <= 5e-2 (SURVEY.md section 7 measured 2.3e-3 mean /
-    2.6e-2 max for bf16 storage on the reference itself).
+  * bf16 path (storage bf16, fp32 accumulate / regression): stated gates about 1.5-2x the measured errors
+    (cfgB stage-isolated depth: mean <= 3e-3, p99 <= 1.2e-2 per pixel; warp 5e-3, U-Net 1.5e-2 relative max;
+    full size: tests/test_gpu_fullsize.py). SURVEY.md section 7 measured 2.3e-3 mean / 2.6e-2 max for bf16
+    storage on the reference itself.
   * photometric confidence: compared where the truncated index floor(sum p*i) is not within 1e-3 of
     an integer on the reference (elsewhere a last-bit difference may legitimately move the window).
 """
@@ -97,7 +98,8 @@ def test_homo_warping_vs_oracle(C, dtype):
     ref = O.homo_warping(src.to(dtype).float(), O.compose_proj(P[:, 3]), O.compose_proj(P[:, 0]), hyps, impl="gather")
     out = homo_warping(cuda(src.to(dtype)), cuda(O.compose_proj(P[:, 3])), cuda(O.compose_proj(P[:, 0])), cuda(hyps))
     # fp32: the sampling position carries ~1 ulp of |ix| (~1e-5 px at these sizes) of rounding
-    tol = 5e-5 if dtype == torch.float32 else 1e-2
+    # bf16: the gathered features and the output are bf16 (one storage rounding each); measured <= 2.8e-3
+    tol = 5e-5 if dtype == torch.float32 else 5e-3
     err = rel_max(np_(out), ref.numpy())
     print("homo_warping C=%d %s: rel_max %.3e" % (C, dtype, err))
     assert err < tol
@@ -238,7 +240,7 @@ def test_costregnet_golden(s, dtype):
     ref = golden("costreg")["logits%d" % s][:, 0]
     err = rel_max(np_(logits), ref)
     print("costregnet stage %d %s: rel_max %.3e" % (s, dtype, err))
-    assert err < (2e-5 if dtype == torch.float32 else 3e-2), err
+    assert err < (2e-5 if dtype == torch.float32 else 1.5e-2), err  # bf16 measured 8.5e-3 (stages 0-2)
 
 
 def test_costregnet_batch_and_shape_sweep():
@@ -402,12 +404,13 @@ def test_stage_isolated_fp32_gate(tag, H, W, N, ndepths, mode):
 
 
 def test_stage_isolated_bf16_stated_gate():
-    """bf16 storage (fp32 accumulate/regression): mean <= 5e-3, p99 <= 2e-2 per-pixel relative depth."""
+    """bf16 storage (fp32 accumulate/regression): mean <= 3e-3, p99 <= 1.2e-2 per-pixel relative depth."""
     for s, (ref, got) in enumerate(_stage_isolated("forward_cfgB_640x512", 512, 640, 5, (48, 32, 8), "adaptive",
                                                    torch.bfloat16)):
         pr = pixel_rel(np_(got["depth"]), ref["depth"].numpy())
         print("bf16 stage%d: mean %.3e p99 %.3e max %.3e" % (s + 1, pr.mean(), np.quantile(pr, 0.99), pr.max()))
-        assert pr.mean() < 5e-3 and np.quantile(pr, 0.99) < 2e-2, s
+        # measured (stage 1 / 2 / 3): mean 3.6e-4 / 7.2e-4 / 1.8e-3, p99 1.4e-3 / 2.7e-3 / 7.6e-3
+        assert pr.mean() < 3e-3 and np.quantile(pr, 0.99) < 1.2e-2, s
 
 
 COND_K = 2.5  # HIP fp32 vs fp64 may be this many times the reference's own fp32-vs-fp64 difference

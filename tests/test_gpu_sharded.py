@@ -43,7 +43,7 @@ def _stage_case(s, D, B, H, W, dtype, N=3):
     return net, nhwc, P.to(DEV), hyps.to(DEV)
 
 
-@pytest.mark.parametrize("warp", ["depth", "rows"])
+@pytest.mark.parametrize("warp", ["depth", "rows", "gather"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("s,D,B,H,W,P", [(1, 32, 2, 64, 80, 2), (1, 32, 1, 64, 80, 3), (2, 8, 2, 48, 56, 4),
                                          (0, 48, 1, 32, 48, 4)])

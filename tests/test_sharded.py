@@ -1,7 +1,7 @@
 """CPU: depth-sharded execution of one stage (damvsnet_amd/sharded.py) -- the shard, halo, all-to-all and
 all-gather bookkeeping -- with a float64 CPU stand-in for the HIP stage engine, against the unsharded oracle
 stage (oracle/mvs_oracle.py depthnet_stage, models/cas_mvsnet.py:18-134): in-process (ThreadGroup, P = 1..5,
-both warp partitionings) and over torch.distributed gloo (world 2 and 3, uneven slabs and depth shards).
+every warp partitioning, incl. north_star's literal volume all-gather) and over torch.distributed gloo (world 2 and 3, uneven slabs and depth shards).
 
 The stand-in runs each U-Net layer with torch's CPU conv on the whole haloed slab tensor, exactly as the HIP
 engine runs its whole-tensor kernel on it, so the sharded result must equal the whole-image one up to float64
@@ -114,7 +114,7 @@ def test_slab_and_plane_partitions():
 
 
 @pytest.mark.parametrize("P", [1, 2, 3, 5])
-@pytest.mark.parametrize("warp", ["depth", "rows"])
+@pytest.mark.parametrize("warp", ["depth", "rows", "gather"])
 def test_thread_group_matches_unsharded(P, warp):
     case = _case()
     ref = _unsharded(*case)
@@ -220,7 +220,8 @@ def test_gloo_world2_whole_cascade_every_stage_sharded():
 
 
 @pytest.mark.timeout(180)
-@pytest.mark.parametrize("world,warp,B", [(2, "depth", 1), (3, "depth", 1), (3, "rows", 1), (2, "depth", 2)])
+@pytest.mark.parametrize("world,warp,B", [(2, "depth", 1), (3, "depth", 1), (3, "rows", 1), (2, "depth", 2),
+                                                (3, "gather", 2)])
 def test_gloo_world_matches_unsharded(world, warp, B):
     """Real torch.distributed P2P (gloo, one process per rank): all-to-all, halo exchange, all-gather. B = 2 runs the
     U-Net as two batch halves with each half's halo transfer outstanding while the other half computes."""
