@@ -2,7 +2,7 @@
 roofline of the dominant kernel and the CPU baseline — one JSON line on rank 0.
 
   python bench.py [--gpus N --steps K --warmup W] [--config cfgC] [--batch B] [--no-cpu-baseline]
-                  [--shard depth|rows [--emulate P]] [--no-shard-latency]
+                  [--shard depth|rows|gather [--emulate P]] [--no-shard-latency]
 
 Workload (BASELINE.json configs[2]): DTU 1600x1184, 5 views, 3-stage 48/32/8 hypotheses, bf16 storage
 on 1x MI355X; synthetic seeded images/cameras, synthetic weights with calibrated BN statistics
@@ -415,21 +415,23 @@ def main():
     maps = args.steps * args.batch * world
     phases = {k: round(statistics.mean(v), 3) for k, v in timer.per_phase_ms().items()}
 
-    shard_block = None
+    shard_blocks = {}
     if world > 1 and not args.no_shard_latency:  # every rank takes part
         from damvsnet_amd.sharded import TorchComm
-        err = None
-        try:
-            shard_block = sharded_latency(net, H, W, N, device, comm=TorchComm())
-        except Exception as ex:  # reported, never fatal for the throughput line
-            err = repr(ex)[:300]
-        # every rank leaves the block knowing whether any rank failed (a failure after the last exchange would
-        # otherwise go unnoticed by the peers); a failure before an exchange ends at the collective timeout
-        flag = torch.tensor([1 if err else 0], device=device)
-        torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.SUM)
-        if int(flag.item()):
-            shard_block = {"error": err or "failed on %d other rank(s)" % int(flag.item()),
-                           "failed_ranks": int(flag.item())}
+        # "depth": the recommended all-to-all + H-slab U-Net; "gather": north_star's literal volume all-gather
+        for key, mode in (("depth_sharded", "depth"), ("depth_sharded_gather", "gather")):
+            err, blk = None, None
+            try:
+                blk = sharded_latency(net, H, W, N, device, comm=TorchComm(), warp=mode)
+            except Exception as ex:  # reported, never fatal for the throughput line
+                err = repr(ex)[:300]
+            # every rank leaves the block knowing whether any rank failed (a failure after the last exchange would
+            # otherwise go unnoticed by the peers); a failure before an exchange ends at the collective timeout
+            flag = torch.tensor([1 if err else 0], device=device)
+            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.SUM)
+            if int(flag.item()):
+                blk = {"error": err or "failed on %d other rank(s)" % int(flag.item()), "failed_ranks": int(flag.item())}
+            shard_blocks[key] = blk
 
     result = None
     if rank == 0:
@@ -479,8 +481,7 @@ def main():
             "hot_path_roofline": hp,
             "mfma_utilisation": pmc_mfma(args.config, args.batch) if native else None,
         }
-        if shard_block is not None:
-            result["depth_sharded"] = shard_block
+        result.update(shard_blocks)
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)
         print(json.dumps(result), flush=True)

@@ -752,18 +752,57 @@ hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a) {
 #define DAMVS_WIDE_DIAG 0  // diagnostic builds only (tools/build_diag_wide.sh): skip parts of the K loop
 #endif
 constexpr int WC = 64, WR = 2;  // q-tile columns x rows
-constexpr int WPER = 7;         // halo pieces per thread: up to 448 pixels
 
-template <bool TWO>
-__global__ __launch_bounds__(256) DAMVS_WAVES(3) void conv2d_wide_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int nsl,
-                                                          int dmin, int span) {
+// Input halo geometry of a WR x WC q-tile for taps spanning `span` input pixels (IS = input stride). Stride 1: rows of
+// WC + span - 1 pixels. Stride 2: 2 (WR - 1) + span rows of 2 (WC - 1) + span columns, each row stored as its even
+// columns then its odd columns (hcp pixels each), so the 16 lanes of an N-group (16 consecutive q-columns) read 16
+// consecutive LDS pixels at every tap, as at stride 1.
+template <int IS, int WRT = WR>
+struct WideHalo {
+  int pitch, hcp, rows, ncols, hp;
+  __host__ __device__ WideHalo(int span) {
+    if (IS == 1) {
+      ncols = WC + span - 1, hcp = ncols, pitch = ncols, rows = WRT + span - 1;
+    } else {
+      ncols = 2 * (WC - 1) + span, hcp = (ncols + 1) / 2, pitch = 2 * hcp, rows = 2 * (WRT - 1) + span;
+    }
+    hp = rows * pitch;
+  }
+  // LDS pixel of halo (row, column c)
+  __host__ __device__ int pix(int row, int c) const { return IS == 1 ? row * pitch + c : row * pitch + (c & 1) * hcp + (c >> 1); }
+  // halo (row, column) of LDS pixel p; column -1 for the odd half's padding slot
+  __device__ void rc(int p, int& row, int& c) const {
+    row = p / pitch;
+    const int r = p - row * pitch;
+    if (IS == 1) {
+      c = r;
+    } else {
+      const int par = r >= hcp;
+      c = 2 * (r - par * hcp) + par;
+      c = c < ncols ? c : -1;
+    }
+  }
+};
+
+// WM = 2: a block owns 128 output channels x a 2 x 64 q-tile, its 4 waves a 2 x 2 grid (cout half, q-row); WM = 1:
+// 64 output channels (cout 64 layers) x a 4 x 64 q-tile, the 4 waves one q-row each.
+template <bool TWO, int IS, int WM>
+__global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_kernel(const Conv2dArgs a, int tiles_x,
+                                                                                      int tiles_y, int nsl, int dmin, int span) {
   typedef uint4 raw;
   typedef BufIO<bf16_t> IO;
   constexpr uint32_t ES = 2;
+  constexpr int WPER = IS == 1 ? 7 : 11;  // halo pieces per thread: up to 448 / 704 pixels
+  constexpr int WRT = 4 / WM;              // q-tile rows
+  constexpr int AR = WM * 256;             // raws of one K chunk's A fragments (WM x 4 cout tiles)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  raw* abuf = reinterpret_cast<raw*>(smem);  // 2 x 512 raws (8 KB per chunk)
-  const int HC = WC + span - 1, HP = (WR + span - 1) * HC;
-  raw* hbuf = abuf + 2 * 512;                // 2 x HP * 4 raws
+  raw* abuf = reinterpret_cast<raw*>(smem);  // 2 x AR raws (WM x 4 KB per chunk)
+  const WideHalo<IS, WRT> hg(span);
+  const int HP = hg.hp;
+  // stride 1: the next slice's halo goes to the other of two buffers; stride 2 (2.5x the pixels): one buffer,
+  // rewritten between two barriers after the slice's last tap
+  constexpr int NHB = IS == 1 ? 2 : 1;
+  raw* hbuf = abuf + 2 * AR;                 // NHB x HP * 4 raws
 
   // logical block = (tile, phase), phase fastest, XCD-contiguous
   const int ntile = tiles_x * tiles_y * a.B;
@@ -773,14 +812,14 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void conv2d_wide_kernel(const C
   const int tl = L / a.nphase;
   const Conv2dPhase& ph = a.ph[L - tl * a.nphase];
   const int tx = tl % tiles_x, ty = (tl / tiles_x) % tiles_y, b = tl / (tiles_x * tiles_y);
-  const int qy0 = ty * WR, qx0 = tx * WC;
+  const int qy0 = ty * WRT, qx0 = tx * WC;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = WM == 2 ? wave >> 1 : 0, wn = WM == 2 ? wave & 1 : wave;
   const int n = lane & 15, g = lane >> 4;
-  const int mt0 = blockIdx.y * 8;
+  const int mt0 = blockIdx.y * 4 * WM;
 
   __shared__ int s_toff[32];  // tap offset inside the halo, in pixels
-  if (tid < 25) s_toff[tid] = tid < ph.ntaps ? (ph.tap[tid][0] - dmin) * HC + (ph.tap[tid][1] - dmin) : 0;
+  if (tid < 25) s_toff[tid] = tid < ph.ntaps ? hg.pix(ph.tap[tid][0] - dmin, ph.tap[tid][1] - dmin) : 0;
 
   const int nt = ph.ntaps;  // loop order (slice, tap); packed order chunk = tap * nsl + slice
   const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack) + ((size_t)ph.w_off * a.MTtot + mt0) * 64;
@@ -791,7 +830,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void conv2d_wide_kernel(const C
   const int npix = a.B * a.Hi * a.Wi;
   const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.in0, (long long)npix * a.c0 * ES);
   const __amdgpu_buffer_rsrc_t r1 = make_rsrc(TWO ? a.in1 : a.in0, TWO ? (long long)npix * a.c1 * ES : 0);
-  const int iy0 = qy0 + dmin, ix0 = qx0 + dmin, pb = b * a.Hi * a.Wi;
+  const int iy0 = IS * qy0 + dmin, ix0 = IS * qx0 + dmin, pb = b * a.Hi * a.Wi;
   // this thread's halo pieces: input pixel index (-1: outside the image or past the halo) and the 16-byte
   // chunk it fetches, the same for every slice
   int hpix[WPER], hch[WPER];
@@ -799,9 +838,10 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void conv2d_wide_kernel(const C
   for (int k = 0; k < WPER; ++k) {
     const int i = tid + k * 256;
     const int p = i >> 2, slot = i & 3;
-    const int row = p / HC, col = p - row * HC;
+    int row, col;
+    hg.rc(p, row, col);
     const int iy = iy0 + row, ix = ix0 + col;
-    const bool ok = p < HP && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+    const bool ok = p < HP && col >= 0 && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
     hpix[k] = ok ? pb + iy * a.Wi + ix : -1;
     hch[k] = (slot ^ ((p >> 2) & 3)) * 8;
   }
@@ -830,14 +870,15 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void conv2d_wide_kernel(const C
     for (int j = 0; j < 4; ++j) acc[m][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   // the fp32 depth plane's halo (zero outside the image) for the trailing plane chunk, staged once
-  float* gbuf = reinterpret_cast<float*>(hbuf + 2 * HP * 4);  // HP floats
+  float* gbuf = reinterpret_cast<float*>(hbuf + NHB * HP * 4);  // HP floats
   if (ph.gchunks > 0) {
     const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.geo[0], ((long long)(a.B - 1) * a.geo_bstride[0] + a.Hi * a.Wi) * 4);
     const int pg0 = b * (int)a.geo_bstride[0];
     for (int p = tid; p < HP; p += 256) {
-      const int row = p / HC, col = p - row * HC;
+      int row, col;
+      hg.rc(p, row, col);
       const int iy = iy0 + row, ix = ix0 + col;
-      const bool ok = (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+      const bool ok = col >= 0 && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
       gbuf[p] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, ok ? (uint32_t)(pg0 + iy * a.Wi + ix) * 4u : kOOB, 0, 0));
     }
   }
@@ -859,27 +900,27 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void conv2d_wide_kernel(const C
   auto wld = [&](raw& x0, raw& x1) {
     const uint32_t so = wbase + (uint32_t)(lt * nsl + lc) * cbytes;
     x0 = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)tid * 16u, so, 0));
-    x1 = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(tid + 256) * 16u, so, 0));
+    if (WM == 2) x1 = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(tid + 256) * 16u, so, 0));
     if (!(lc == nsl - 1 && lt == nt - 1)) next(lc, lt);
   };
   wld(p0, p1);
   wld(q0, q1);
   hload(0);
   abuf[tid] = p0;
-  abuf[tid + 256] = p1;
+  if (WM == 2) abuf[tid + 256] = p1;
   hstore(0);
   __syncthreads();
-  const int lanepix = wn * HC + n;
+  const int lanepix = wn * IS * hg.pitch + n;
   int k = 0;
   auto step = [&](int c, int t, raw& ld0, raw& ld1, const raw& st0, const raw& st1) {
     if (!(DAMVS_WIDE_DIAG & 8)) wld(ld0, ld1);
-    const raw* ab = abuf + (k & 1) * 512 + wm * 256 + lane;
+    const raw* ab = abuf + (k & 1) * AR + wm * 256 + lane;
     raw af[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) af[m] = ab[m * 64];
     // 16 pixels apart keeps (p >> 2) & 3: one swizzled address, the 4 N-groups at immediate offsets
     const int p0x = s_toff[t] + lanepix;
-    const raw* hb = hbuf + (c & 1) * HP * 4 + p0x * 4 + (g ^ ((p0x >> 2) & 3));
+    const raw* hb = hbuf + (NHB == 2 ? (c & 1) * HP * 4 : 0) + p0x * 4 + (g ^ ((p0x >> 2) & 3));
     raw bf[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) bf[j] = hb[j * 64];
@@ -891,11 +932,14 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void conv2d_wide_kernel(const C
     } else {
       acc[0][0][0] += __uint_as_float(af[0].x ^ bf[0].y);
     }
-    abuf[((k + 1) & 1) * 512 + tid] = st0;  // past the last chunk: a harmless copy
-    abuf[((k + 1) & 1) * 512 + tid + 256] = st1;
+    abuf[((k + 1) & 1) * AR + tid] = st0;  // past the last chunk: a harmless copy
+    if (WM == 2) abuf[((k + 1) & 1) * AR + tid + 256] = st1;
     if (!(DAMVS_WIDE_DIAG & 4)) {
       if (t == 0 && c + 1 < nsl) hload(c + 1);
-      if (t == nt - 1 && c + 1 < nsl) hstore((c + 1) & 1);
+      if (t == nt - 1 && c + 1 < nsl) {
+        if (NHB == 1) __syncthreads();  // every wave is done with slice c's halo
+        hstore(NHB == 2 ? (c + 1) & 1 : 0);
+      }
     }
     if (!(DAMVS_WIDE_DIAG & 2)) __syncthreads();
     ++k;
@@ -1016,13 +1060,48 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void conv2d_wide_kernel(const C
   }
 }
 
-// Returns hipErrorNotSupported when the wide kernel does not take the layer (bf16 callers only).
+template <int IS, int WM>
+hipError_t launch_wide_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span) {
+  constexpr int WRT = 4 / WM, AR = WM * 256;
+  const WideHalo<IS, WRT> hg(span);
+  constexpr int NHB = IS == 1 ? 2 : 1, WPER = IS == 1 ? 7 : 11;
+  if (hg.hp * 4 > WPER * 256) return hipErrorNotSupported;
+  const size_t below_plane = 2 * (size_t)AR * 16 + NHB * (size_t)hg.hp * 64;
+  if (below_plane < 4 * 32 * 68 * 4) return hipErrorNotSupported;  // the epilogue's staging tiles stay below the plane halo
+  const int tx = (a.Wq + WC - 1) / WC, ty = (a.Hq + WRT - 1) / WRT;
+  const int nsl = (a.c0 + a.c1) / 32;
+  const size_t smem = below_plane + (size_t)hg.hp * 4;  // A chunks, halo slices, plane halo
+  const long long nblk = (long long)tx * ty * a.B * a.nphase;
+  const dim3 grid((unsigned)nblk, (unsigned)(a.MTtot / (4 * WM)));
+  auto k = a.c1 > 0 ? conv2d_wide_kernel<true, IS, WM> : conv2d_wide_kernel<false, IS, WM>;
+  if (smem > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)smem);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, grid, dim3(256), smem, s, a, tx, ty, nsl, dmin, span);
+  return hipGetLastError();
+}
+
+// Returns hipErrorNotSupported when the wide kernel does not take the layer (bf16 callers only). Input stride 2
+// (the stride-2 GeoBlock convs, one phase) unless DAMVS_CONV2D_WIDE_S2=0; cout 64 at input stride 1 on the 64-channel
+// block (WM = 1) unless DAMVS_CONV2D_WIDE64=0.
 hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
   static const bool off = [] {
     const char* v = getenv("DAMVS_CONV2D_WIDE");
     return v && v[0] == '0';
   }();
-  if (off || a.in_stride != 1 || a.xpair || a.ngeo > 1 || a.MTtot % 8 || a.c0 % 32 || a.c1 % 32 || a.c0 + a.c1 < 64 ||
+  static const bool s2 = [] {
+    const char* v = getenv("DAMVS_CONV2D_WIDE_S2");
+    return !(v && v[0] == '0');
+  }();
+  static const bool w64 = [] {
+    const char* v = getenv("DAMVS_CONV2D_WIDE64");
+    return !(v && v[0] == '0');
+  }();
+  const bool stride_ok = a.in_stride == 1 || (a.in_stride == 2 && s2 && a.nphase == 1 && a.out_stride == 1);
+  const bool half = w64 && a.MTtot == 4 && a.in_stride == 1;  // 64 output channels
+  if (off || !stride_ok || a.xpair || a.ngeo > 1 || (a.MTtot % 8 && !half) || a.c0 % 32 || a.c1 % 32 || a.c0 + a.c1 < 64 ||
       a.cout % 32)  // the epilogue finishes whole 32-channel halves per lane
     return hipErrorNotSupported;
   int dmin = 0, dmax = 0;
@@ -1033,23 +1112,10 @@ hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
         dmax = a.ph[p].tap[t][d] > dmax ? a.ph[p].tap[t][d] : dmax;
       }
   const int span = dmax - dmin + 1;
-  const int HP = (WR + span - 1) * (WC + span - 1);
-  if (HP * 4 > WPER * 256) return hipErrorNotSupported;
   for (int p = 0; p < a.nphase; ++p)  // geo taps beyond one K chunk; fewer than 4 taps (halo schedule)
     if (a.ph[p].gchunks > 1 || a.ph[p].ntaps < 4) return hipErrorNotSupported;
-  const int tx = (a.Wq + WC - 1) / WC, ty = (a.Hq + WR - 1) / WR;
-  const int nsl = (a.c0 + a.c1) / 32;
-  const size_t smem = 2 * 512 * 16 + 2 * (size_t)HP * 64 + (size_t)HP * 4;  // A chunks, halo slices, plane halo
-  const long long nblk = (long long)tx * ty * a.B * a.nphase;
-  const dim3 grid((unsigned)nblk, (unsigned)(a.MTtot / 8));
-  auto k = a.c1 > 0 ? conv2d_wide_kernel<true> : conv2d_wide_kernel<false>;
-  if (smem > 64 * 1024) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)smem);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(k, grid, dim3(256), smem, s, a, tx, ty, nsl, dmin, span);
-  return hipGetLastError();
+  if (half) return launch_wide_t<1, 1>(s, a, dmin, span);
+  return a.in_stride == 1 ? launch_wide_t<1, 2>(s, a, dmin, span) : launch_wide_t<2, 2>(s, a, dmin, span);
 }
 
 // True when the layer is a plain 3x3 stride-1 padding-1 conv with dense row-major taps.

@@ -47,7 +47,7 @@ CASES = [
     (True, 3, 1, 1, 0, 16, 0, (), 8, True, False, 1),
     (True, 3, 1, 1, 0, 8, 0, (), 2, True, False, 0),                # rgb_decoder_output (cout 2)
     (False, 3, 1, 1, 0, 256, 0, (), 256, True, False, 0),           # wide layer (cout tiling)
-    (False, 3, 1, 1, 0, 32, 32, (64,), 64, True, True, 0),          # halo kernel: two inputs + plane
+    (False, 3, 1, 1, 0, 32, 32, (64,), 64, True, True, 0),          # two inputs + plane (wide, 64-channel block)
     (True, 5, 2, 2, 1, 128, 0, (), 32, True, False, 1),             # halo kernel: k5 s2 phases, cout 32
     (True, 3, 1, 1, 0, 64, 0, (), 128, True, True, 0),              # halo kernel: transposed k3 s1, MT 8
     (True, 4, 2, 1, 0, 16, 0, (), 8, False, False, 0),              # x-pair phases: FPN top (k4 s2), cout 8
@@ -61,6 +61,13 @@ CASES = [
     (False, 3, 1, 1, 0, 32, 0, (32,), 16, True, False, 0),          # halo, one slice, one cout tile
     (False, 3, 1, 1, 0, 0, 0, (0, 1, 2), 8, True, False, 0),         # planes: FeatureNet RGB conv 3->8
     (False, 5, 1, 2, 0, 0, 0, (0, 1), 8, True, False, 0),            # planes: depth_conv_init 2->8
+    # wide kernel at input stride 2 (GeoBlock conv1 of the 128 -> 256 levels), ragged q-tiles and an odd width
+    (False, 3, 2, 1, 0, 128, 128, (256,), 256, True, False, 0, (37, 151)),
+    (False, 3, 2, 1, 0, 128, 0, (128,), 256, True, False, 0, (20, 24)),
+    (False, 3, 2, 1, 0, 64, 32, (0,), 128, False, True, 0, (30, 260)),
+    # wide kernel's 64-channel block (4 x 64 q-tiles): GeoBlock 64+g -> 64, transposed k3 s1 128 -> 64
+    (False, 3, 1, 1, 0, 64, 0, (64,), 64, True, True, 0, (37, 151)),
+    (True, 3, 1, 1, 0, 128, 0, (), 64, True, False, 0, (30, 70)),
 ]
 
 
@@ -68,9 +75,9 @@ CASES = [
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_conv2d_layer_vs_torch(case, dtype):
     from damvsnet_amd.frontend_hip import HipConv2d, planes
-    tr, k, s, p, op, c0, c1, geo, cout, relu, pre, post_up = case
+    tr, k, s, p, op, c0, c1, geo, cout, relu, pre, post_up = case[:12]
     g = torch.Generator().manual_seed(hash(case) % 1000)
-    B, H, W = 2, 20, 24
+    B, (H, W) = 2, (case[12] if len(case) > 12 else (20, 24))
     cin = c0 + c1 + len(geo)
     conv = (nn.ConvTranspose2d(cin, cout, k, stride=s, padding=p, output_padding=op) if tr
             else nn.Conv2d(cin, cout, k, stride=s, padding=p))
