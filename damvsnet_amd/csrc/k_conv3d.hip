@@ -105,8 +105,11 @@ __device__ __forceinline__ void finish4(const ConvArgs& a, __amdgpu_buffer_rsrc_
 // voxel decomposition, range-checked buffer loads for the zero padding.
 // XP: x-parity-pair deconv phases (build_phases_xpair): MFMA row r = (x parity r >> 3, channel r & 7),
 // so lane group g stores channels (g & 1) * 4 .. +3 of output x = 2 qx + (g >> 1).
-template <typename T, int MT, bool XP>
-__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1)) void conv3d_mfma_kernel(const ConvArgs a, int nqblk) {
+// PIPE: chunk s + 1's weight fragments and input gathers are issued before chunk s's MFMAs (two register sets), so
+// each chunk waits only for loads that had a whole chunk of MFMAs to land (the deep-K mid-level layers: conv3 - conv7,
+// K = 27 x 16 .. 27 x 64).
+template <typename T, int MT, bool XP, bool PIPE = false>
+__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIPE ? 3 : 1)) void conv3d_mfma_kernel(const ConvArgs a, int nqblk) {
   typedef BufIO<T> IO;
   typedef typename IO::raw raw;
   constexpr int E = Stor<T>::E;  // input channels per lane per K-chunk
@@ -166,15 +169,14 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
   const int HW = a.Hi * a.Wi;
   int t = (g * E) / a.Cin, ci = g * E - t * a.Cin;  // this lane's (tap, channel) at k = s*KC + g*E
   const int qt = KC / a.Cin, rc = KC - qt * a.Cin;
-  for (int s = 0; s < ph.kchunks; ++s) {
-    raw wf[MT];
+  // loads of chunk s (the (t, ci) cursor is at chunk s and moves on to s + 1)
+  auto load = [&](int s, raw (&wf)[MT], raw (&xf)[kGroups]) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * MT + m) * 64];
     const bool tv = t < ph.ntaps;
     const int code = s_tap[tv ? t : 0];
     const int dz = (code & 0xff) - 8, dy = ((code >> 8) & 0xff) - 8, dx = ((code >> 16) & 0xff) - 8;
     const int tapoff = dz * HW + dy * a.Wi + dx;
-    raw xf[kGroups];
 #pragma unroll
     for (int j = 0; j < kGroups; ++j) {
       const int iz = zs[j] + dz, iy = ys[j] + dy, ix = xs[j] + dx;
@@ -182,13 +184,34 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
                       (unsigned)ix < (unsigned)a.Wi;
       xf[j] = IO::frag(r0, ok ? (uint32_t)((pin[j] + tapoff) * a.Cin + ci) * ES : kOOB);
     }
+    ci += rc;
+    t += qt;
+    if (ci >= a.Cin) { ci -= a.Cin; ++t; }
+  };
+  auto mma = [&](const raw (&wf)[MT], const raw (&xf)[kGroups]) {
 #pragma unroll
     for (int j = 0; j < kGroups; ++j)
 #pragma unroll
       for (int m = 0; m < MT; ++m) Frag<T>::mma(wf[m], xf[j], acc[j][m]);
-    ci += rc;
-    t += qt;
-    if (ci >= a.Cin) { ci -= a.Cin; ++t; }
+  };
+  if constexpr (PIPE) {
+    raw wa[MT], xa[kGroups], wb[MT], xb[kGroups];
+    const int nk = ph.kchunks;
+    load(0, wa, xa);
+    for (int s = 0; s < nk; s += 2) {
+      if (s + 1 < nk) load(s + 1, wb, xb);
+      mma(wa, xa);
+      if (s + 1 < nk) {
+        if (s + 2 < nk) load(s + 2, wa, xa);
+        mma(wb, xb);
+      }
+    }
+  } else {
+    for (int s = 0; s < ph.kchunks; ++s) {
+      raw wf[MT], xf[kGroups];
+      load(s, wf, xf);
+      mma(wf, xf);
+    }
   }
 
   if constexpr (XP && DAMVS_DIAG_SKIP_EPI == 0) {
@@ -1349,6 +1372,20 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
   if (a.xpair) {
     if (a.MT != 1 || a.Cout != 8) return hipErrorInvalidValue;
     hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, true>), grid, dim3(256), 0, s, a, nq);
+    return hipGetLastError();
+  }
+  // DAMVS_CONV3D_PIPE=0 (A/B): the gather kernel without the one-chunk-ahead loads
+  static const bool pipe = [] {
+    const char* v = getenv("DAMVS_CONV3D_PIPE");
+    return !(v && v[0] == '0');
+  }();
+  if (pipe) {
+    switch (a.MT) {
+      case 1: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, false, true>), grid, dim3(256), 0, s, a, nq); break;
+      case 2: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 2, false, true>), grid, dim3(256), 0, s, a, nq); break;
+      case 4: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 4, false, true>), grid, dim3(256), 0, s, a, nq); break;
+      default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
   }
   switch (a.MT) {

@@ -913,13 +913,14 @@ hipError_t launch_c(hipStream_t s, const WarpArgs& a0) {
   }
   const int ppb = 256 / lanes;
   // Pixel blocks as R-row tiles (R divides ppb) dealt across the full width, or in strips SW pixels wide:
-  // DAMVS_WARP_TILE="R,SW", default R = 16; "0": ppb consecutive pixels of the row-major computed rows. The
-  // 16-row tiles keep vertically adjacent pixels, whose bilinear footprints share source rows, on one CU: stage-2
+  // DAMVS_WARP_TILE="R,SW", default R = 8; "0": ppb consecutive pixels of the row-major computed rows. The
+  // 8-row tiles keep vertically adjacent pixels, whose bilinear footprints share source rows, on one CU: stage-2
   // L1 -> L2 requests -19 % and L2 hit 0.62 -> 0.71 already at 4 rows (profiles/r03/pmc_l2_tile.json); in the
-  // pipeline (B=4) stage 3 1.48 -> 1.24 ms, stage 2 2.00 -> 1.92 ms, stage 1 flat (profiles/r03/ab_warp_tile.jsonl).
+  // pipeline (B=4) stage 3 1.48 -> 1.24 ms, stage 2 2.00 -> 1.82 ms, stage 1 1.40 -> 1.31 ms; 16 / 32 / 64 rows
+  // slower again (profiles/r03/ab_warp_tile.jsonl).
   static const int tile_env[2] = {[] {
                                     const char* e = getenv("DAMVS_WARP_TILE");
-                                    return e ? atoi(e) : 16;
+                                    return e ? atoi(e) : 8;
                                   }(),
                                   [] {
                                     const char* e = getenv("DAMVS_WARP_TILE");
