@@ -730,6 +730,153 @@ __global__ __launch_bounds__(256) void conv3d_zslide_pair_kernel(const ConvArgs 
   }
 }
 
+// conv0 with each input plane's B fragments read from LDS once (round 3): input plane p feeds output planes p + 1,
+// p and p - 1 (kernel depths 0, 1, 2), so a block walks the INPUT planes and runs, per plane, the three depth
+// slices' MFMAs on the same B fragments into three rotating accumulator sets (outputs p + 1, p, p - 1); output p - 1
+// is complete after plane p and is written then. conv3d_zslide_pair_kernel reads every plane's fragments three times
+// (once per output plane it feeds): one ds_read_b128 per MFMA, which bound it by LDS bandwidth at CIN 32 (stage 1).
+// Per output plane and column group the MFMA chain is the same sequence (depth 0's chunks from plane z - 1, then
+// depth 1's from plane z, then depth 2's from plane z + 1, chunks ascending; zero planes outside the volume
+// included): bitwise the same results. Same tiles, ring (4 slots, loads two planes ahead) and weights.
+template <int CIN, int TXG>
+__global__ __launch_bounds__(256) void conv3d_zreuse_pair_kernel(const ConvArgs a, int tiles_x, int tiles_y,
+                                                                 int nzc, int zc, int ntiles) {
+  typedef uint4 raw;
+  constexpr int E = 8, KC = 32, CH = CIN / E;
+  constexpr int TX = 16 * TXG, PW = TX + 2, PH = LTH + 2;
+  constexpr int PLANE = PH * PW * CH;  // 16-byte chunks per halo plane
+  constexpr int NLD = (PLANE + 255) / 256;
+  constexpr int KCHUNKS = 36 * CIN / KC;
+  constexpr int NJ = KCHUNKS / 3;  // K chunks per kernel depth
+  static_assert(KC % CIN == 0 || CIN % KC == 0, "chunking");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  raw* ring = reinterpret_cast<raw*>(smem);
+
+  const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
+  int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tx = tt % tiles_x; tt /= tiles_x;
+  const int ty = tt % tiles_y; tt /= tiles_y;
+  const int tz = tt % nzc;
+  const int b = tt / nzc;
+  const int x0 = tx * TX, y0 = ty * LTH, zb = tz * zc;
+  const int zend = min(zb + zc, a.Do);
+
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * 2);
+  auto load_plane = [&](int iz, raw* v) {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * 256;
+      const int row = c / (PW * CH), col = c - row * (PW * CH);
+      const int iy = y0 - 1 + row, ix = x0 - 1 + col / CH;
+      const bool ok = c < PLANE && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+                      (unsigned)ix < (unsigned)a.Wi;
+      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16u;
+      v[i] = BufIO<bf16_t>::frag(rin, ok ? off : kOOB);
+    }
+  };
+  auto store_plane = [&](int iz, const raw* v) {
+    raw* dst = ring + ((iz + 4) & 3) * PLANE;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * 256;
+      if (c < PLANE) dst[c] = v[i];
+    }
+  };
+  raw wreg[KCHUNKS];
+  {
+    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack_pair) + (threadIdx.x & 63);
+#pragma unroll
+    for (int s = 0; s < KCHUNKS; ++s) wreg[s] = wsrc[(size_t)s * 64];
+  }
+  raw pa[NLD], pb[NLD];
+  load_plane(zb - 1, pa);
+  store_plane(zb - 1, pa);
+  load_plane(zb, pa);  // stored at the end of step zb - 1; from there on planes are fetched two steps ahead
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const int gi = (g * E) / CIN, gc = (g * E) % CIN / E;
+  const int lbase = (2 * wave * PW + n) * CH + gc;  // this lane's chunk at tap (dy' = 0, dx = 0)
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * 2;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
+  const int co = (g & 1) * 4, r = g >> 1;
+  float bias[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias[i] = co < a.Cout ? a.bias[co + i] : 0.f;
+  const int oy = y0 + 2 * wave + r;
+
+  f32x4_t an[TXG], ac[TXG], ap[TXG];  // outputs p + 1, p, p - 1 of step p
+#pragma unroll
+  for (int xg = 0; xg < TXG; ++xg) an[xg] = ac[xg] = ap[xg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  auto epilogue = [&](int z, const f32x4_t* acc) {
+#pragma unroll
+    for (int xg = 0; xg < TXG; ++xg) {
+      const int ox = x0 + 16 * xg + n;
+      const bool vok = oy < a.Ho && ox < a.Wo && co < a.Cout;
+      const uint32_t off = (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * a.Cout + co) * 2u;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = acc[xg][i] + bias[i];
+        if (a.relu) v[i] = fmaxf(v[i], 0.f);
+      }
+      BufIO<bf16_t>::stq(ro, vok ? off : kOOB, v);
+    }
+  };
+  // step p: plane p + 1 (in `cur`) goes to the ring after the MFMAs, plane p + 2 is fetched into `nxt` before them
+  auto step = [&](int p, raw* cur, raw* nxt) {
+    if (p + 2 <= zend) load_plane(p + 2, nxt);
+    const raw* src = ring + ((p + 4) & 3) * PLANE + lbase;
+    raw bv[NJ][TXG];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int kt = (j * KC) / CIN, kc = ((j * KC) % CIN) / E;
+      auto toff = [](int t) { return (((t / 3) % 4) * PW + t % 3) * CH; };
+      int off = toff(kt);
+      if (KC > CIN) {
+        off = gi == 1 ? toff(kt + 1) : off;
+        off = gi == 2 ? toff(kt + 2) : off;
+        off = gi == 3 ? toff(kt + 3) : off;
+      }
+#pragma unroll
+      for (int xg = 0; xg < TXG; ++xg) bv[j][xg] = src[off + kc + 16 * xg * CH];
+    }
+    if (p + 1 < zend) {  // output p + 1, kernel depth 0
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int xg = 0; xg < TXG; ++xg) Frag<bf16_t>::mma(wreg[j], bv[j][xg], an[xg]);
+    }
+    if (p >= zb && p < zend) {  // output p, kernel depth 1
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int xg = 0; xg < TXG; ++xg) Frag<bf16_t>::mma(wreg[NJ + j], bv[j][xg], ac[xg]);
+    }
+    if (p - 1 >= zb) {  // output p - 1, kernel depth 2: complete
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int xg = 0; xg < TXG; ++xg) Frag<bf16_t>::mma(wreg[2 * NJ + j], bv[j][xg], ap[xg]);
+      epilogue(p - 1, ap);
+    }
+#pragma unroll
+    for (int xg = 0; xg < TXG; ++xg) {
+      ap[xg] = ac[xg];
+      ac[xg] = an[xg];
+      an[xg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    }
+    if (p + 1 <= zend) store_plane(p + 1, cur);  // slot of plane p - 3, last read before the previous barrier
+    __syncthreads();
+  };
+  for (int p = zb - 1; p <= zend; p += 2) {
+    step(p, pa, pb);
+    if (p + 1 <= zend) step(p + 1, pb, pa);
+  }
+}
+
 bool zslide_disabled() {  // read per call: tests flip it between launches
   const char* v = getenv("DAMVS_CONV_NO_ZSLIDE");
   return v && v[0] == '1';
@@ -746,8 +893,15 @@ hipError_t launch_zslide_pair_t(hipStream_t s, const ConvArgs& a) {
   }();
   const int tx = (a.Wo + 16 * TXG - 1) / (16 * TXG), ty = (a.Ho + LTH - 1) / LTH, nzc = (a.Do + zc - 1) / zc;
   const long long nt = (long long)tx * ty * nzc * a.B;
-  hipLaunchKernelGGL((conv3d_zslide_pair_kernel<CIN, TXG>), dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc,
-                     (int)nt);
+  // DAMVS_CONV0_REUSE=0 (read per call, A/B and the bitwise test): the output-plane walk reading every input plane's
+  // fragments three times
+  const char* rv = getenv("DAMVS_CONV0_REUSE");
+  if (!(rv && rv[0] == '0'))
+    hipLaunchKernelGGL((conv3d_zreuse_pair_kernel<CIN, TXG>), dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc,
+                       (int)nt);
+  else
+    hipLaunchKernelGGL((conv3d_zslide_pair_kernel<CIN, TXG>), dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc,
+                       (int)nt);
   return hipGetLastError();
 }
 
