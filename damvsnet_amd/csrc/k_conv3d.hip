@@ -737,9 +737,10 @@ __global__ __launch_bounds__(256) void conv3d_zslide_pair_kernel(const ConvArgs 
 // (once per output plane it feeds): one ds_read_b128 per MFMA, which bound it by LDS bandwidth at CIN 32 (stage 1).
 // Per output plane and column group the MFMA chain is the same sequence (depth 0's chunks from plane z - 1, then
 // depth 1's from plane z, then depth 2's from plane z + 1, chunks ascending; zero planes outside the volume
-// included): bitwise the same results. Same tiles, ring (4 slots, loads two planes ahead) and weights.
+// included): bitwise the same results. Same weights; a 2-slot ring (loads two planes ahead) and, at CIN 32, 8 x 32
+// output windows (TXG 2: twice the MFMAs per plane step).
 template <int CIN, int TXG>
-__global__ __launch_bounds__(256) void conv3d_zreuse_pair_kernel(const ConvArgs a, int tiles_x, int tiles_y,
+__global__ __launch_bounds__(256) DAMVS_WAVES(CIN == 32 ? 2 : CIN == 16 ? 3 : 1) void conv3d_zreuse_pair_kernel(const ConvArgs a, int tiles_x, int tiles_y,
                                                                  int nzc, int zc, int ntiles) {
   typedef uint4 raw;
   constexpr int E = 8, KC = 32, CH = CIN / E;
@@ -775,7 +776,7 @@ __global__ __launch_bounds__(256) void conv3d_zreuse_pair_kernel(const ConvArgs 
     }
   };
   auto store_plane = [&](int iz, const raw* v) {
-    raw* dst = ring + ((iz + 4) & 3) * PLANE;
+    raw* dst = ring + ((iz + 2) & 1) * PLANE;  // two slots: plane p + 1 goes where plane p - 1 was
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int c = threadIdx.x + i * 256;
@@ -828,8 +829,8 @@ __global__ __launch_bounds__(256) void conv3d_zreuse_pair_kernel(const ConvArgs 
   // step p: plane p + 1 (in `cur`) goes to the ring after the MFMAs, plane p + 2 is fetched into `nxt` before them
   auto step = [&](int p, raw* cur, raw* nxt) {
     if (p + 2 <= zend) load_plane(p + 2, nxt);
-    const raw* src = ring + ((p + 4) & 3) * PLANE + lbase;
-    raw bv[NJ][TXG];
+    const raw* src = ring + ((p + 2) & 1) * PLANE + lbase;
+    const bool d0 = p + 1 < zend, d1 = p >= zb && p < zend, d2 = p - 1 >= zb;  // outputs p + 1, p, p - 1 here
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int kt = (j * KC) / CIN, kc = ((j * KC) % CIN) / E;
@@ -841,34 +842,21 @@ __global__ __launch_bounds__(256) void conv3d_zreuse_pair_kernel(const ConvArgs 
         off = gi == 3 ? toff(kt + 3) : off;
       }
 #pragma unroll
-      for (int xg = 0; xg < TXG; ++xg) bv[j][xg] = src[off + kc + 16 * xg * CH];
+      for (int xg = 0; xg < TXG; ++xg) {
+        const raw bv = src[off + kc + 16 * xg * CH];
+        if (d0) Frag<bf16_t>::mma(wreg[j], bv, an[xg]);           // kernel depth 0
+        if (d1) Frag<bf16_t>::mma(wreg[NJ + j], bv, ac[xg]);      // kernel depth 1
+        if (d2) Frag<bf16_t>::mma(wreg[2 * NJ + j], bv, ap[xg]);  // kernel depth 2
+      }
     }
-    if (p + 1 < zend) {  // output p + 1, kernel depth 0
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int xg = 0; xg < TXG; ++xg) Frag<bf16_t>::mma(wreg[j], bv[j][xg], an[xg]);
-    }
-    if (p >= zb && p < zend) {  // output p, kernel depth 1
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int xg = 0; xg < TXG; ++xg) Frag<bf16_t>::mma(wreg[NJ + j], bv[j][xg], ac[xg]);
-    }
-    if (p - 1 >= zb) {  // output p - 1, kernel depth 2: complete
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int xg = 0; xg < TXG; ++xg) Frag<bf16_t>::mma(wreg[2 * NJ + j], bv[j][xg], ap[xg]);
-      epilogue(p - 1, ap);
-    }
+    if (d2) epilogue(p - 1, ap);  // output p - 1 is complete
 #pragma unroll
     for (int xg = 0; xg < TXG; ++xg) {
       ap[xg] = ac[xg];
       ac[xg] = an[xg];
       an[xg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     }
-    if (p + 1 <= zend) store_plane(p + 1, cur);  // slot of plane p - 3, last read before the previous barrier
+    if (p + 1 <= zend) store_plane(p + 1, cur);  // slot of plane p - 1, last read before the previous barrier
     __syncthreads();
   };
   for (int p = zb - 1; p <= zend; p += 2) {
@@ -893,15 +881,21 @@ hipError_t launch_zslide_pair_t(hipStream_t s, const ConvArgs& a) {
   }();
   const int tx = (a.Wo + 16 * TXG - 1) / (16 * TXG), ty = (a.Ho + LTH - 1) / LTH, nzc = (a.Do + zc - 1) / zc;
   const long long nt = (long long)tx * ty * nzc * a.B;
-  // DAMVS_CONV0_REUSE=0 (read per call, A/B and the bitwise test): the output-plane walk reading every input plane's
-  // fragments three times
-  const char* rv = getenv("DAMVS_CONV0_REUSE");
-  if (!(rv && rv[0] == '0'))
-    hipLaunchKernelGGL((conv3d_zreuse_pair_kernel<CIN, TXG>), dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc,
-                       (int)nt);
-  else
-    hipLaunchKernelGGL((conv3d_zslide_pair_kernel<CIN, TXG>), dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc,
-                       (int)nt);
+  hipLaunchKernelGGL((conv3d_zslide_pair_kernel<CIN, TXG>), dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc,
+                     (int)nt);
+  return hipGetLastError();
+}
+
+// conv0 on the input-plane walk (conv3d_zreuse_pair_kernel, 2-slot ring)
+template <int CIN, int TXG>
+hipError_t launch_zreuse_pair_t(hipStream_t s, const ConvArgs& a) {
+  constexpr int PLANE = (LTH + 2) * (16 * TXG + 2) * (CIN / 8);
+  const size_t smem = 2 * PLANE * 16;
+  constexpr int zc = 16;
+  const int tx = (a.Wo + 16 * TXG - 1) / (16 * TXG), ty = (a.Ho + LTH - 1) / LTH, nzc = (a.Do + zc - 1) / zc;
+  const long long nt = (long long)tx * ty * nzc * a.B;
+  hipLaunchKernelGGL((conv3d_zreuse_pair_kernel<CIN, TXG>), dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc,
+                     (int)nt);
   return hipGetLastError();
 }
 
@@ -909,6 +903,11 @@ template <typename T, int CIN>
 hipError_t launch_lds_pair_t(hipStream_t s, const ConvArgs& a) {
   if constexpr (sizeof(T) == 2) {
     if (!a.resid && !zslide_disabled()) {
+      // DAMVS_CONV0_REUSE (read per call): 1 = the input-plane walk at every CIN, 0 = never; default: CIN 32 only
+      // (at CIN 8 / 16 its registers cost a wave per SIMD: stage 2 / 3 U-Net 2.09 / 1.89 -> 2.22 / 2.01 ms)
+      const char* rv = getenv("DAMVS_CONV0_REUSE");
+      const bool reuse = rv ? rv[0] == '1' : CIN == 32;
+      if (reuse) return launch_zreuse_pair_t<CIN, 2>(s, a);
       if constexpr (CIN == 32) return launch_zslide_pair_t<CIN, 1>(s, a);
       else return launch_zslide_pair_t<CIN, 2>(s, a);
     }
@@ -1528,10 +1527,11 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
     hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, true>), grid, dim3(256), 0, s, a, nq);
     return hipGetLastError();
   }
-  // DAMVS_CONV3D_PIPE=0 (A/B): the gather kernel without the one-chunk-ahead loads
+  // DAMVS_CONV3D_PIPE=1 (A/B): the gather kernel with one-chunk-ahead loads (measured flat in the pipeline:
+  // U-Net 1.185 / 2.218 / 2.020 against 1.187 / 2.227 / 2.023 ms per stage, at one wave per SIMD less)
   static const bool pipe = [] {
     const char* v = getenv("DAMVS_CONV3D_PIPE");
-    return !(v && v[0] == '0');
+    return v && v[0] == '1';
   }();
   if (pipe) {
     switch (a.MT) {
