@@ -21,9 +21,9 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WANT = ["SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_BUSY_CYCLES", "SQ_WAVES", "GRBM_GUI_ACTIVE"]
-FAMILIES = (("unet_conv3d", ("conv3d", "deconv_", "conv_s2_c8", "conv_s1_c16")), ("frontend_conv2d", ("conv2d",)),
+FAMILIES = (("unet_conv3d", ("conv3d", "deconv_", "conv_s2_c8", "conv_s1_c16")), ("frontend_conv2d", ("conv2d", "fpn_top")),
             ("prob_regress", ("prob_mfma", "prob_regress", "prob_conv", "regress_kernel")),
-            ("warp_aggregate", ("warp_aggregate",)))
+            ("warp_aggregate", ("warp_aggregate", "warp_split", "warp_pair")))
 
 
 def family(name):
