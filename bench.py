@@ -43,6 +43,7 @@ CONFIGS = {
     "cfgD": (1184, 1600, 7, (64, 32, 8), torch.bfloat16, "DTU 1600x1184, 7 views, 3-stage 64/32/8, bf16"),
     "cfgE": (1056, 1920, 11, (64, 32, 8), torch.bfloat16, "T&T 1920x1056, 11 views, 3-stage 64/32/8, bf16"),
 }
+SHARD_GUARD_S = 240  # N > 1: seconds the depth-sharded blocks may take before the line goes out without them
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -415,24 +416,6 @@ def main():
     maps = args.steps * args.batch * world
     phases = {k: round(statistics.mean(v), 3) for k, v in timer.per_phase_ms().items()}
 
-    shard_blocks = {}
-    if world > 1 and not args.no_shard_latency:  # every rank takes part
-        from damvsnet_amd.sharded import TorchComm
-        # "depth": the recommended all-to-all + H-slab U-Net; "gather": north_star's literal volume all-gather
-        for key, mode in (("depth_sharded", "depth"), ("depth_sharded_gather", "gather")):
-            err, blk = None, None
-            try:
-                blk = sharded_latency(net, H, W, N, device, comm=TorchComm(), warp=mode)
-            except Exception as ex:  # reported, never fatal for the throughput line
-                err = repr(ex)[:300]
-            # every rank leaves the block knowing whether any rank failed (a failure after the last exchange would
-            # otherwise go unnoticed by the peers); a failure before an exchange ends at the collective timeout
-            flag = torch.tensor([1 if err else 0], device=device)
-            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.SUM)
-            if int(flag.item()):
-                blk = {"error": err or "failed on %d other rank(s)" % int(flag.item()), "failed_ranks": int(flag.item())}
-            shard_blocks[key] = blk
-
     result = None
     if rank == 0:
         lat = latency_b1(net, imgs, proj, dv, ins)
@@ -481,12 +464,49 @@ def main():
             "hot_path_roofline": hp,
             "mfma_utilisation": pmc_mfma(args.config, args.batch) if native else None,
         }
+    import threading
+    guard, printed = None, threading.Event()
+    if world > 1 and not args.no_shard_latency:
+        # The depth-sharded modes below are the run's only RCCL P2P traffic. Should one of them hang (the NCCL
+        # watchdog would abort the process at the collective timeout, losing the throughput line), a timer prints
+        # rank 0's line without them (unless it is out already) and ends the process first.
+        line = json.dumps(dict(result, depth_sharded={"error": "timed out after %d s" % SHARD_GUARD_S})) if rank == 0 else None
+
+        def _guard():
+            if line is not None and not printed.is_set():
+                print(line, flush=True)
+            os._exit(0)
+        guard = threading.Timer(SHARD_GUARD_S, _guard)
+        guard.daemon = True
+        guard.start()
+    shard_blocks = {}
+    if world > 1 and not args.no_shard_latency:  # every rank takes part
+        from damvsnet_amd.sharded import TorchComm
+        # "depth": the recommended all-to-all + H-slab U-Net; "gather": north_star's literal volume all-gather
+        for key, mode in (("depth_sharded", "depth"), ("depth_sharded_gather", "gather")):
+            err, blk = None, None
+            try:
+                blk = sharded_latency(net, H, W, N, device, comm=TorchComm(), warp=mode)
+            except Exception as ex:  # reported, never fatal for the throughput line
+                err = repr(ex)[:300]
+            # every rank leaves the block knowing whether any rank failed (a failure after the last exchange would
+            # otherwise go unnoticed by the peers); a failure before an exchange ends at the collective timeout
+            flag = torch.tensor([1 if err else 0], device=device)
+            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.SUM)
+            if int(flag.item()):
+                blk = {"error": err or "failed on %d other rank(s)" % int(flag.item()), "failed_ranks": int(flag.item())}
+            shard_blocks[key] = blk
+
+    if rank == 0:
         result.update(shard_blocks)
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)
+        printed.set()
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+    if guard is not None:
+        guard.cancel()
 
 
 if __name__ == "__main__":
