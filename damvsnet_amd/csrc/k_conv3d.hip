@@ -108,8 +108,10 @@ __device__ __forceinline__ void finish4(const ConvArgs& a, __amdgpu_buffer_rsrc_
 // PIPE: chunk s + 1's weight fragments and input gathers are issued before chunk s's MFMAs (two register sets), so
 // each chunk waits only for loads that had a whole chunk of MFMAs to land (the deep-K mid-level layers: conv3 - conv7,
 // K = 27 x 16 .. 27 x 64).
-template <typename T, int MT, bool XP, bool PIPE = false>
-__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIPE ? 3 : 1)) void conv3d_mfma_kernel(const ConvArgs a, int nqblk) {
+// KG: 16-voxel column groups per wave (kGroups = 4 by default; 1 for the small deep-K level-3 layers, whose grid
+// would otherwise leave most CUs idle).
+template <typename T, int MT, bool XP, bool PIPE = false, int KG = kGroups>
+__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIPE && KG == kGroups ? 3 : 1)) void conv3d_mfma_kernel(const ConvArgs a, int nqblk) {
   typedef BufIO<T> IO;
   typedef typename IO::raw raw;
   constexpr int E = Stor<T>::E;  // input channels per lane per K-chunk
@@ -133,14 +135,14 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIP
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
   const int Qtot = a.B * a.Dq * a.Hq * a.Wq;
-  const int base = (qblk * 4 + wave) * (kGroups * 16);
+  const int base = (qblk * 4 + wave) * (KG * 16);
   if (base >= Qtot) return;
 
   const int IS = a.in_stride, OS = a.out_stride;
-  int zs[kGroups], ys[kGroups], xs[kGroups], pin[kGroups], pout[kGroups];
-  bool valid[kGroups];
+  int zs[KG], ys[KG], xs[KG], pin[KG], pout[KG];
+  bool valid[KG];
 #pragma unroll
-  for (int j = 0; j < kGroups; ++j) {
+  for (int j = 0; j < KG; ++j) {
     int q = base + j * 16 + n;
     valid[j] = q < Qtot;
     q = valid[j] ? q : 0;
@@ -152,9 +154,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIP
     pout[j] = ((b * a.Do + qz * OS + ph.pd) * a.Ho + qy * OS + ph.ph) * a.Wo + qx * OS + (XP ? (g >> 1) : ph.pw);
   }
 
-  f32x4_t acc[kGroups][MT];
+  f32x4_t acc[KG][MT];
 #pragma unroll
-  for (int j = 0; j < kGroups; ++j)
+  for (int j = 0; j < KG; ++j)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
@@ -170,7 +172,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIP
   int t = (g * E) / a.Cin, ci = g * E - t * a.Cin;  // this lane's (tap, channel) at k = s*KC + g*E
   const int qt = KC / a.Cin, rc = KC - qt * a.Cin;
   // loads of chunk s (the (t, ci) cursor is at chunk s and moves on to s + 1)
-  auto load = [&](int s, raw (&wf)[MT], raw (&xf)[kGroups]) {
+  auto load = [&](int s, raw (&wf)[MT], raw (&xf)[KG]) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * MT + m) * 64];
     const bool tv = t < ph.ntaps;
@@ -178,7 +180,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIP
     const int dz = (code & 0xff) - 8, dy = ((code >> 8) & 0xff) - 8, dx = ((code >> 16) & 0xff) - 8;
     const int tapoff = dz * HW + dy * a.Wi + dx;
 #pragma unroll
-    for (int j = 0; j < kGroups; ++j) {
+    for (int j = 0; j < KG; ++j) {
       const int iz = zs[j] + dz, iy = ys[j] + dy, ix = xs[j] + dx;
       const bool ok = valid[j] && tv && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
                       (unsigned)ix < (unsigned)a.Wi;
@@ -188,14 +190,14 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIP
     t += qt;
     if (ci >= a.Cin) { ci -= a.Cin; ++t; }
   };
-  auto mma = [&](const raw (&wf)[MT], const raw (&xf)[kGroups]) {
+  auto mma = [&](const raw (&wf)[MT], const raw (&xf)[KG]) {
 #pragma unroll
-    for (int j = 0; j < kGroups; ++j)
+    for (int j = 0; j < KG; ++j)
 #pragma unroll
       for (int m = 0; m < MT; ++m) Frag<T>::mma(wf[m], xf[j], acc[j][m]);
   };
   if constexpr (PIPE) {
-    raw wa[MT], xa[kGroups], wb[MT], xb[kGroups];
+    raw wa[MT], xa[KG], wb[MT], xb[KG];
     const int nk = ph.kchunks;
     load(0, wa, xa);
     for (int s = 0; s < nk; s += 2) {
@@ -208,7 +210,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIP
     }
   } else {
     for (int s = 0; s < ph.kchunks; ++s) {
-      raw wf[MT], xf[kGroups];
+      raw wf[MT], xf[KG];
       load(s, wf, xf);
       mma(wf, xf);
     }
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIP
 #pragma unroll
     for (int i = 0; i < 8; ++i) b8[i] = a.bias[i];
 #pragma unroll
-    for (int j = 0; j < kGroups; ++j) {
+    for (int j = 0; j < KG; ++j) {
       float r[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -249,7 +251,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIP
       // gfx950, nondeterministically: tools/diag_unet_repro.py)
       const bool lead = (g & 1) == 0;
 #pragma unroll
-      for (int j = 0; j < kGroups; ++j) {
+      for (int j = 0; j < KG; ++j) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           float r[8];
@@ -284,7 +286,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIP
     for (int i = 0; i < 4; ++i) bias[m][i] = cok[m] ? a.bias[co + i] : 0.f;
   }
   const __amdgpu_buffer_rsrc_t rq = DAMVS_DIAG_SKIP_EPI == 2 ? ro : rr;
-  typename IO::quad q[kGroups][MT];
+  typename IO::quad q[KG][MT];
   auto load_skip = [&](int j) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
@@ -294,10 +296,10 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIP
   };
   if (DAMVS_DIAG_SKIP_EPI == 4) {
 #pragma unroll
-    for (int j = 0; j < kGroups; ++j) load_skip(j);
+    for (int j = 0; j < KG; ++j) load_skip(j);
   }
 #pragma unroll
-  for (int j = 0; j < kGroups; ++j) {
+  for (int j = 0; j < KG; ++j) {
     if (DAMVS_DIAG_SKIP_EPI != 4) load_skip(j);
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
@@ -1525,6 +1527,24 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
   if (a.xpair) {
     if (a.MT != 1 || a.Cout != 8) return hipErrorInvalidValue;
     hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, true>), grid, dim3(256), 0, s, a, nq);
+    return hipGetLastError();
+  }
+  // small grids (fewer than ~4 blocks per CU: the level-3 convs conv5 / conv6 and the 2-plane levels) take one
+  // 16-voxel group per wave: 4x the waves for the same MFMAs (DAMVS_CONV3D_KG1=0: off, 1: always)
+  static const int kg1 = [] {
+    const char* v = getenv("DAMVS_CONV3D_KG1");
+    return v ? atoi(v) : -1;
+  }();
+  if (kg1 == 1 || (kg1 != 0 && (long long)nq * a.nphase < 1024)) {
+    const long long pb1 = 4LL * 16;
+    const int nq1 = (int)((Qtot + pb1 - 1) / pb1);
+    const dim3 grid1((unsigned)(nq1 * a.nphase));
+    switch (a.MT) {
+      case 1: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, false, false, 1>), grid1, dim3(256), 0, s, a, nq1); break;
+      case 2: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 2, false, false, 1>), grid1, dim3(256), 0, s, a, nq1); break;
+      case 4: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 4, false, false, 1>), grid1, dim3(256), 0, s, a, nq1); break;
+      default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
   }
   // DAMVS_CONV3D_PIPE=1 (A/B): the gather kernel with one-chunk-ahead loads (measured flat in the pipeline:

@@ -6,7 +6,7 @@ set -u
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd "$R" && mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_streams.py > gpurun_out/pytest_pipe.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_pipe.log; [ $rc -eq 0 ] || exit $rc
-for v in X=1 DAMVS_CONV0_REUSE=1 DAMVS_CONV0_REUSE=0 DAMVS_WARP_PAIR=1 X=1 DAMVS_CONV0_REUSE=1 DAMVS_CONV0_REUSE=0 DAMVS_WARP_PAIR=1; do
+for v in X=1 DAMVS_CONV3D_KG1=0 X=1 DAMVS_CONV3D_KG1=0; do
   env $v timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/bench_ab.json 2> gpurun_out/bench_ab.err || { echo "bench $v failed"; tail -3 gpurun_out/bench_ab.err; exit 1; }
   python - "$v" gpurun_out/bench_ab.json <<'PY' | tee -a gpurun_out/ab_unet.jsonl
 import json, sys
