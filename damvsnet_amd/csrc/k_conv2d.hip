@@ -1231,6 +1231,86 @@ __global__ __launch_bounds__(256) void conv2d_planes_kernel(const Conv2dArgs a, 
   }
 }
 
+// Plane-only layers (as conv2d_planes_kernel) with 4 consecutive output columns x 2 rows per thread: each input row
+// arrives as three aligned 16-byte loads per plane (columns x0 - 4 .. x0 + 7) instead of K scalar loads per pixel
+// column, a quarter of the load instructions for the same fused multiply-adds (same order per output: bitwise the
+// one-column kernel). Needs Wi % 4 == 0 and 16-byte aligned planes (launch_planes checks); COUT 8.
+template <typename T, int COUT, int K, int NG>
+__global__ __launch_bounds__(256) void conv2d_planes4_kernel(const Conv2dArgs a, const float* __restrict__ wg) {
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  constexpr int P = K / 2;
+  const int Hp = (a.Ho + 1) / 2, Wg = a.Wo / 4;
+  const int Qtot = a.B * Hp * Wg;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Qtot) return;
+  const int ox0 = (q % Wg) * 4;
+  const int oy0 = (q / Wg) % Hp * 2;
+  const int b = q / (Wg * Hp);
+  f32x2_t acc[2][4][COUT / 2];  // [output row][column][channel pair]
+#pragma unroll
+  for (int c = 0; c < COUT / 2; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[0][j][c] = acc[1][j][c] = (f32x2_t){a.bias[2 * c], a.bias[2 * c + 1]};
+  __amdgpu_buffer_rsrc_t rg[NG];
+  uint32_t gb[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    rg[g] = make_rsrc(a.geo[g], ((long long)(a.B - 1) * a.geo_bstride[g] + (long long)a.Hi * a.Wi) * 4);
+    gb[g] = (uint32_t)((long long)b * a.geo_bstride[g]) * 4u;
+  }
+  const int cp = a.cout_pad;
+#pragma unroll 1
+  for (int r = 0; r <= K; ++r) {
+    const int iy = oy0 - P + r;
+    const bool oky = (unsigned)iy < (unsigned)a.Hi;
+    float v[NG][12];  // columns ox0 - 4 .. ox0 + 7
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int h = 0; h < 3; ++h) {
+        const int ix = ox0 - 4 + 4 * h;
+        const bool ok = oky && ix >= 0 && ix < a.Wi;  // whole 16-byte groups: Wi % 4 == 0
+        const float4 f = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                        rg[g], ok ? (uint32_t)(iy * a.Wi + ix) * 4u : kOOB, gb[g], 0));
+        v[g][4 * h] = f.x; v[g][4 * h + 1] = f.y; v[g][4 * h + 2] = f.z; v[g][4 * h + 3] = f.w;
+      }
+    auto row = [&](const float* w, f32x2_t (*acc_r)[COUT / 2]) {
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          const float* wt = w + (kx * NG + g) * cp;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float xv = v[g][4 - P + j + kx];
+            const f32x2_t x = {xv, xv};
+#pragma unroll
+            for (int c = 0; c < COUT / 2; ++c)
+              acc_r[j][c] = __builtin_elementwise_fma((f32x2_t){wt[2 * c], wt[2 * c + 1]}, x, acc_r[j][c]);
+          }
+        }
+    };
+    if (r < K) row(wg + (size_t)r * K * NG * cp, acc[0]);
+    if (r > 0) row(wg + (size_t)(r - 1) * K * NG * cp, acc[1]);
+  }
+  const bool two = oy0 + 1 < a.Ho;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float o0[COUT], o1[COUT];
+#pragma unroll
+    for (int c = 0; c < COUT / 2; ++c) {
+      o0[2 * c] = acc[0][j][c].x; o0[2 * c + 1] = acc[0][j][c].y;
+      o1[2 * c] = acc[1][j][c].x; o1[2 * c + 1] = acc[1][j][c].y;
+    }
+#pragma unroll
+    for (int c0 = 0; c0 < COUT; c0 += 4) {
+      if (c0 >= a.cout) break;
+      tail4<T>(a, b, oy0, ox0 + j, c0, o0 + c0);
+      if (two) tail4<T>(a, b, oy0 + 1, ox0 + j, c0, o1 + c0);
+    }
+  }
+}
+
 // Any other plane-only layer (stride 2, transposed; no production layer): one thread per output
 // pixel of a phase, all (<= 16) output channels.
 template <typename T>
@@ -1266,6 +1346,29 @@ bool planes_fast_ok(const Conv2dArgs& a, int K) {
   return true;
 }
 
+template <typename T, int K>
+hipError_t launch_planes4_k(hipStream_t st, const Conv2dArgs& a) {
+  const long long Qtot = (long long)a.B * ((a.Ho + 1) / 2) * (a.Wo / 4);
+  dim3 grid((unsigned)((Qtot + 255) / 256));
+  switch (a.ngeo) {
+    case 1: hipLaunchKernelGGL((conv2d_planes4_kernel<T, 8, K, 1>), grid, dim3(256), 0, st, a, a.wgeo); break;
+    case 2: hipLaunchKernelGGL((conv2d_planes4_kernel<T, 8, K, 2>), grid, dim3(256), 0, st, a, a.wgeo); break;
+    case 3: hipLaunchKernelGGL((conv2d_planes4_kernel<T, 8, K, 3>), grid, dim3(256), 0, st, a, a.wgeo); break;
+    default: hipLaunchKernelGGL((conv2d_planes4_kernel<T, 8, K, 4>), grid, dim3(256), 0, st, a, a.wgeo); break;
+  }
+  return hipGetLastError();
+}
+
+// conv2d_planes4_kernel's conditions: 4-column groups of whole 16-byte plane pieces (DAMVS_PLANES4=0, read per call:
+// the one-column kernel)
+bool planes4_ok(const Conv2dArgs& a) {
+  const char* v = getenv("DAMVS_PLANES4");
+  if ((v && v[0] == '0') || a.cout > 8 || a.Wi % 4 || a.Wo != a.Wi) return false;
+  for (int g = 0; g < a.ngeo; ++g)
+    if (reinterpret_cast<uintptr_t>(a.geo[g]) % 16 || a.geo_bstride[g] % 4) return false;
+  return true;
+}
+
 template <typename T, int COUT, int K>
 hipError_t launch_planes_k(hipStream_t st, const Conv2dArgs& a) {
   const long long Qtot = (long long)a.B * ((a.Ho + 1) / 2) * a.Wo;
@@ -1285,6 +1388,7 @@ hipError_t launch_planes(hipStream_t st, const Conv2dArgs& a) {
   const int K = a.ph[0].ntaps == 9 ? 3 : a.ph[0].ntaps == 25 ? 5 : 0;
   if (K == 0 || a.ngeo < 1 || a.ngeo > 4 || a.cout > 16 || a.cout_pad < 16 || !planes_fast_ok(a, K))
     return hipErrorNotSupported;
+  if (planes4_ok(a)) return K == 3 ? launch_planes4_k<T, 3>(st, a) : launch_planes4_k<T, 5>(st, a);
   if (a.cout <= 8) return K == 3 ? launch_planes_k<T, 8, 3>(st, a) : launch_planes_k<T, 8, 5>(st, a);
   return K == 3 ? launch_planes_k<T, 16, 3>(st, a) : launch_planes_k<T, 16, 5>(st, a);
 }

@@ -1529,13 +1529,14 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
     hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, true>), grid, dim3(256), 0, s, a, nq);
     return hipGetLastError();
   }
-  // small grids (fewer than ~4 blocks per CU: the level-3 convs conv5 / conv6 and the 2-plane levels) take one
-  // 16-voxel group per wave: 4x the waves for the same MFMAs (DAMVS_CONV3D_KG1=0: off, 1: always)
+  // DAMVS_CONV3D_KG1 (A/B; 1: always, 2: grids below 1024 blocks, i.e. the level-3 convs conv5 / conv6): one 16-voxel
+  // group per wave, 4x the waves for the same MFMAs. Measured on conv5 / conv6: stage-1 U-Net 1.137 -> 1.125 ms but
+  // stage 3 1.867 -> 1.91 ms, 206.0 -> 205.2 maps/s (profiles/r03/ab_unet.jsonl); off by default
   static const int kg1 = [] {
     const char* v = getenv("DAMVS_CONV3D_KG1");
-    return v ? atoi(v) : -1;
+    return v ? atoi(v) : 0;
   }();
-  if (kg1 == 1 || (kg1 != 0 && (long long)nq * a.nphase < 1024)) {
+  if (kg1 == 1 || (kg1 == 2 && (long long)nq * a.nphase < 1024)) {
     const long long pb1 = 4LL * 16;
     const int nq1 = (int)((Qtot + pb1 - 1) / pb1);
     const dim3 grid1((unsigned)(nq1 * a.nphase));

@@ -314,3 +314,26 @@ def test_fpn_top_fused_vs_torch(B, H, W):
     with pytest.raises(_capi.DamvsError):  # odd sizes are refused
         _capi.check(lib.damvs_fpn_top_forward(_capi.stream_ptr(o.device), B, H - 1, W, c0d.data_ptr(),
                                               fd.data_ptr(), fd.data_ptr(), fd.data_ptr(), o.data_ptr()))
+
+
+@pytest.mark.parametrize("k,ng,relu,pre", [(3, 3, True, False), (5, 4, True, False), (5, 2, True, True), (3, 1, False, False)])
+def test_planes_four_columns_bitwise(k, ng, relu, pre, monkeypatch):
+    """The 4-column plane-only kernel (conv2d_planes4_kernel: FeatureNet's RGB conv, GeoFF's RGB+depth and depth init
+    convs) against the one-column kernel it replaces: same fused multiply-adds per output, so bitwise equal (odd H,
+    first / last column groups at the image edges, with and without a residual)."""
+    from damvsnet_amd.frontend_hip import HipConv2d, planes
+    g = torch.Generator().manual_seed(7 * k + ng)
+    B, H, W, cout = 2, 21, 36, 8
+    conv = nn.Conv2d(ng, cout, k, padding=k // 2)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.2)
+        conv.bias.copy_(torch.randn(conv.bias.shape, generator=g) * 0.1)
+    gp = planes(torch.randn(B, ng, H, W, generator=g).to(DEV))
+    res = torch.randn(B, H, W, cout, generator=g).to(DEV, torch.bfloat16) if pre else None
+    L = HipConv2d(conv, torch.bfloat16, relu, geo_at=tuple(range(ng)), c0=0, c1=0, c1_at=0)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DAMVS_PLANES4", flag)
+        outs.append(L(B, H, W, None, None, geo=gp, res_pre=res).clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
