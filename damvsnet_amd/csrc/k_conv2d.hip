@@ -1388,7 +1388,9 @@ hipError_t launch_planes(hipStream_t st, const Conv2dArgs& a) {
   const int K = a.ph[0].ntaps == 9 ? 3 : a.ph[0].ntaps == 25 ? 5 : 0;
   if (K == 0 || a.ngeo < 1 || a.ngeo > 4 || a.cout > 16 || a.cout_pad < 16 || !planes_fast_ok(a, K))
     return hipErrorNotSupported;
-  if (planes4_ok(a)) return K == 3 ? launch_planes4_k<T, 3>(st, a) : launch_planes4_k<T, 5>(st, a);
+  // 5x5 only: GeoFF stage-3 init convs 5.21-5.28 against 5.30-5.43 ms; at 3x3 (FeatureNet's RGB conv, half of each
+  // 12-column window unused, a quarter of the threads) features 2.86-2.89 against 2.77 ms (profiles/r03/ab_planes4.jsonl)
+  if (K == 5 && planes4_ok(a)) return launch_planes4_k<T, 5>(st, a);
   if (a.cout <= 8) return K == 3 ? launch_planes_k<T, 8, 3>(st, a) : launch_planes_k<T, 8, 5>(st, a);
   return K == 3 ? launch_planes_k<T, 16, 3>(st, a) : launch_planes_k<T, 16, 5>(st, a);
 }

@@ -1,0 +1,19 @@
+#!/usr/bin/env bash
+# Round-3 re-check of the tunable defaults after the warp tiles and the new conv kernels. Kernel-selection switch sweep (DESIGN.md section 4 switch table): every variant runs twice, each time
+# right after a default run, so drift and run-to-run spread show up beside the deltas. B=4, 20 steps.
+set -u
+R="${GRAFT_REPO_ROOT:-$(pwd)}"
+cd "$R" && mkdir -p gpurun_out
+run() {  # run <label> [VAR=value ...]
+  local label=$1; shift
+  env "$@" timeout -k 10 150 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-shard-latency \
+    > gpurun_out/sw.log 2>&1 || { echo "$label failed"; tail -3 gpurun_out/sw.log; exit 1; }
+  echo "$label $(tail -1 gpurun_out/sw.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+}
+for cfg in "DAMVS_ZSLIDE_ZC=8" "DAMVS_ZSLIDE_ZC=32" "DAMVS_CONV2D_WANT_TILES=600" "DAMVS_CONV2D_WANT_TILES=1400" \
+           "DAMVS_WARP_MINBLK=1024" "DAMVS_WARP_MINBLK=8192" "DAMVS_CONV2D_HALO=8" "DAMVS_CONV2D_MAXMT=4"; do
+  for rep in 1 2; do
+    run "default" X=1
+    run "$cfg" "$cfg"
+  done
+done
