@@ -305,10 +305,10 @@ __global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int
                                                         const float* __restrict__ prob_init,
                                                         const float* __restrict__ hyps, float* __restrict__ depth,
                                                         float* __restrict__ conf, float* __restrict__ var,
-                                                        float* __restrict__ prob) {
+                                                        float* __restrict__ prob, int vec_ok) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint4* tile = reinterpret_cast<uint4*>(smem);                 // 2 x 340 voxels (double buffer)
-  float* lg = reinterpret_cast<float*>(tile + 2 * kPRVox);      // [D - 1][256] logits, column per pixel
+  float* lg = reinterpret_cast<float*>(tile + 2 * kPRVox);      // [D][256] logits, column per pixel
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, g = lane >> 4;
   const int y0 = blockIdx.y * kTY, x0 = blockIdx.x * kTX;
@@ -394,8 +394,11 @@ __global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int
   float last = am1;  // plane D - 1
 
   const int y = y0 + R0 + g, x = x0 + C0 + n;
-  if (y >= h || x >= w) return;
   const size_t hw = (size_t)h * w, p = (size_t)y * w + x;
+  // w % 4 == 0: the probabilities go out as 16-byte runs of 4 pixels of a tile row from the LDS column (below)
+  // instead of one 4-byte store per pixel and plane
+  const bool vec = prob && vec_ok;
+  if (y < h && x < w) {
   const float* hy = hyps + (size_t)b * D * hw + p;
   const float* pin = prob_init ? prob_init + (size_t)b * D * hw + p : nullptr;
   float* lcol = lg + pix;
@@ -430,7 +433,7 @@ __global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int
   int ii = (int)idx;
   ii = ii < 0 ? 0 : (ii > D - 1 ? D - 1 : ii);
   float c = 0.f, vs = 0.f;
-  float* po = prob ? prob + (size_t)b * D * hw + p : nullptr;
+  float* po = prob && !vec ? prob + (size_t)b * D * hw + p : nullptr;
   for (int d0 = 0; d0 < D; d0 += 8) {
     float hv[8];
 #pragma unroll
@@ -447,9 +450,21 @@ __global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int
       }
     }
   }
+  if (vec) lg[(D - 1) * 256 + pix] = last;  // the column's last plane
   depth[(size_t)b * hw + p] = dep;
   conf[(size_t)b * hw + p] = c;
   var[(size_t)b * hw + p] = 3.f * sqrtf(vs);
+  }
+  if (vec) {
+    __syncthreads();  // every pixel's normalised column is in LDS
+    for (int i = tid; i < D * 64; i += 256) {
+      const int d = i >> 6, r = (i >> 3) & 7, c4 = i & 7;
+      const int yy = y0 + r, xx = x0 + 4 * c4;
+      if (yy < h && xx < w)
+        *reinterpret_cast<float4*>(prob + ((size_t)(b * D + d) * h + yy) * w + xx) =
+            *reinterpret_cast<const float4*>(lg + d * 256 + r * kTX + 4 * c4);
+    }
+  }
 }
 
 template <typename T, int CB>
@@ -541,7 +556,7 @@ hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float
 
 namespace damvs {
 
-size_t prob_mfma_smem(int D) { return 2 * (size_t)kPRVox * 16 + (size_t)(D > 0 ? D - 1 : 0) * 256 * 4; }
+size_t prob_mfma_smem(int D) { return 2 * (size_t)kPRVox * 16 + (size_t)(D > 0 ? D : 0) * 256 * 4; }
 
 hipError_t launch_prob_mfma(hipStream_t s, int B, int D, int h, int w, const void* feat, const void* apack,
                             const float* prob_init, const float* hyps, float* depth, float* conf, float* var,
@@ -555,8 +570,11 @@ hipError_t launch_prob_mfma(hipStream_t s, int B, int D, int h, int w, const voi
     if (e != hipSuccess) return e;
   }
   const dim3 grid((w + kTX - 1) / kTX, (h + kTY - 1) / kTY, B);
+  // 16-byte probability stores need w % 4 == 0 (DAMVS_PROB_VEC=0, read per call: one 4-byte store per pixel and plane)
+  const char* pv = getenv("DAMVS_PROB_VEC");
+  const int vec_ok = (w & 3) == 0 && !(pv && pv[0] == '0');
   hipLaunchKernelGGL(prob_mfma_kernel, grid, dim3(256), smem, s, B, D, h, w, reinterpret_cast<const bf16_t*>(feat),
-                     reinterpret_cast<const uint4*>(apack), prob_init, hyps, depth, conf, var, prob);
+                     reinterpret_cast<const uint4*>(apack), prob_init, hyps, depth, conf, var, prob, vec_ok);
   return hipGetLastError();
 }
 

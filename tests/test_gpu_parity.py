@@ -164,13 +164,14 @@ def test_block_channels_is_the_blocked_permutation(C, dtype):
         assert torch.equal(got, src.view(B, h, w, C // E, E).permute(0, 3, 1, 2, 4).contiguous())
 
 
-@pytest.mark.parametrize("s,D,W", [(0, 48, 80), (1, 32, 80), (0, 64, 80), (2, 8, 72), (1, 16, 104)])
+@pytest.mark.parametrize("s,D,W", [(0, 48, 80), (1, 32, 80), (0, 64, 80), (2, 8, 72), (1, 16, 104), (1, 16, 70)])
 @pytest.mark.parametrize("with_init", [False, True])
 def test_prob_mfma_vs_split_path(s, D, W, with_init):
     """bf16 stage regression (prob conv on MFMA + regression, prob_mfma_kernel in k_regress.hip: the default for
     bf16 storage) against the split path on the same U-Net output (damvs_costreg_logits: fp32-weight VALU prob
     conv, then damvs_regress). The MFMA form multiplies the bf16 voxels exactly by the fp32 weights carried as two
-    bf16 terms (relative weight error < 2^-17); W = 72 / 104 leave ragged 32-pixel tiles; with_init adds a
+    bf16 terms (relative weight error < 2^-17); W = 72 / 104 leave ragged 32-pixel tiles, W = 70 takes the 4-byte
+    probability stores (W % 4 != 0); with_init adds a
     prob_volume_init (models/cas_mvsnet.py:107-108) to the logits."""
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import StageEngine, regress
