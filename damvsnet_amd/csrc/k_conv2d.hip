@@ -785,7 +785,8 @@ struct WideHalo {
 };
 
 // WM = 2: a block owns 128 output channels x a 2 x 64 q-tile, its 4 waves a 2 x 2 grid (cout half, q-row); WM = 1:
-// 64 output channels (cout 64 layers) x a 4 x 64 q-tile, the 4 waves one q-row each.
+// 64 output channels (cout 64 layers) x a 4 x 64 q-tile, the 4 waves one q-row each; WM = 1 at input stride 2 (the
+// 4-row halo would not fit): a 2 x 64 q-tile, the 4 waves a 2 x 2 grid (q-row, 32-column half).
 template <bool TWO, int IS, int WM>
 __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_kernel(const Conv2dArgs a, int tiles_x,
                                                                                       int tiles_y, int nsl, int dmin, int span) {
@@ -793,7 +794,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
   typedef BufIO<bf16_t> IO;
   constexpr uint32_t ES = 2;
   constexpr int WPER = IS == 1 ? 7 : 11;  // halo pieces per thread: up to 448 / 704 pixels
-  constexpr int WRT = 4 / WM;              // q-tile rows
+  constexpr bool HALFW = WM == 1 && IS == 2;     // waves of 32 q-columns
+  constexpr int NGW = HALFW ? 2 : 4;             // 16-column N-groups per wave
+  constexpr int WRT = HALFW ? 2 : 4 / WM;        // q-tile rows
   constexpr int AR = WM * 256;             // raws of one K chunk's A fragments (WM x 4 cout tiles)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   raw* abuf = reinterpret_cast<raw*>(smem);  // 2 x AR raws (WM x 4 KB per chunk)
@@ -814,7 +817,8 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
   const int tx = tl % tiles_x, ty = (tl / tiles_x) % tiles_y, b = tl / (tiles_x * tiles_y);
   const int qy0 = ty * WRT, qx0 = tx * WC;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = WM == 2 ? wave >> 1 : 0, wn = WM == 2 ? wave & 1 : wave;
+  const int wm = WM == 2 ? wave >> 1 : 0, wn = WM == 2 ? wave & 1 : HALFW ? wave >> 1 : wave;
+  const int wc = HALFW ? (wave & 1) * 32 : 0;  // the wave's first q-column in the tile
   const int n = lane & 15, g = lane >> 4;
   const int mt0 = blockIdx.y * 4 * WM;
 
@@ -863,11 +867,11 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
     }
   };
 
-  f32x4_t acc[4][4];  // [cout tile][N-group: 16 columns of the wave's q-row]
+  f32x4_t acc[4][NGW];  // [cout tile][N-group: 16 columns of the wave's q-row]
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[m][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NGW; ++j) acc[m][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   // the fp32 depth plane's halo (zero outside the image) for the trailing plane chunk, staged once
   float* gbuf = reinterpret_cast<float*>(hbuf + NHB * HP * 4);  // HP floats
@@ -910,7 +914,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
   if (WM == 2) abuf[tid + 256] = p1;
   hstore(0);
   __syncthreads();
-  const int lanepix = wn * IS * hg.pitch + n;
+  const int lanepix = wn * IS * hg.pitch + wc + n;
   int k = 0;
   auto step = [&](int c, int t, raw& ld0, raw& ld1, const raw& st0, const raw& st1) {
     if (!(DAMVS_WIDE_DIAG & 8)) wld(ld0, ld1);
@@ -921,14 +925,14 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
     // 16 pixels apart keeps (p >> 2) & 3: one swizzled address, the 4 N-groups at immediate offsets
     const int p0x = s_toff[t] + lanepix;
     const raw* hb = hbuf + (NHB == 2 ? (c & 1) * HP * 4 : 0) + p0x * 4 + (g ^ ((p0x >> 2) & 3));
-    raw bf[4];
+    raw bf[NGW];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bf[j] = hb[j * 64];
+    for (int j = 0; j < NGW; ++j) bf[j] = hb[j * 64];
     if (!(DAMVS_WIDE_DIAG & 1)) {
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Frag2<bf16_t>::mma(af[m], bf[j], acc[m][j]);
+        for (int j = 0; j < NGW; ++j) Frag2<bf16_t>::mma(af[m], bf[j], acc[m][j]);
     } else {
       acc[0][0][0] += __uint_as_float(af[0].x ^ bf[0].y);
     }
@@ -970,17 +974,17 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
   const __amdgpu_buffer_rsrc_t rpost = make_rsrc(a.res_post ? a.res_post : a.out, a.res_post ? nout / (up * up) * ES : 0);
   // the fp32 plane as a trailing K chunk (tap x plane), B from the staged plane halo
   if (ph.gchunks > 0) {
-    float v[4][8];
+    float v[NGW][8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int tt = g * 8 + e;
       const bool tv = tt < nt;
       const int po = s_toff[tv ? tt : 0] + lanepix;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j][e] = tv ? gbuf[po + j * 16] : 0.f;
+      for (int j = 0; j < NGW; ++j) v[j][e] = tv ? gbuf[po + j * 16] : 0.f;
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NGW; ++j) {
       const raw xf = pack_vals<bf16_t>(v[j]);
 #pragma unroll
       for (int m = 0; m < 4; ++m) Frag2<bf16_t>::mma(ag[m], xf, acc[m][j]);
@@ -1011,7 +1015,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
       }
     };
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NGW / 2; ++h) {
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
@@ -1021,7 +1025,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
         }
       asm volatile("" ::: "memory");  // one wave's LDS accesses complete in order: only the compiler must keep it
       const int j = 2 * h + (lp >> 4);
-      const int qx = qx0 + j * 16 + (lp & 15);
+      const int qx = qx0 + wc + j * 16 + (lp & 15);
       const int oy = qyw * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
       const int pout = (b * a.Ho + oy) * a.Wo + ox;
       const int ppost = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
@@ -1062,7 +1066,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
 
 template <int IS, int WM>
 hipError_t launch_wide_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span) {
-  constexpr int WRT = 4 / WM, AR = WM * 256;
+  constexpr int WRT = WM == 1 && IS == 2 ? 2 : 4 / WM, AR = WM * 256;
   const WideHalo<IS, WRT> hg(span);
   constexpr int NHB = IS == 1 ? 2 : 1, WPER = IS == 1 ? 7 : 11;
   if (hg.hp * 4 > WPER * 256) return hipErrorNotSupported;
@@ -1100,7 +1104,7 @@ hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
     return !(v && v[0] == '0');
   }();
   const bool stride_ok = a.in_stride == 1 || (a.in_stride == 2 && s2 && a.nphase == 1 && a.out_stride == 1);
-  const bool half = w64 && a.MTtot == 4 && a.in_stride == 1;  // 64 output channels
+  const bool half = w64 && a.MTtot == 4;  // 64 output channels
   if (off || !stride_ok || a.xpair || a.ngeo > 1 || (a.MTtot % 8 && !half) || a.c0 % 32 || a.c1 % 32 || a.c0 + a.c1 < 64 ||
       a.cout % 32)  // the epilogue finishes whole 32-channel halves per lane
     return hipErrorNotSupported;
@@ -1114,7 +1118,7 @@ hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
   const int span = dmax - dmin + 1;
   for (int p = 0; p < a.nphase; ++p)  // geo taps beyond one K chunk; fewer than 4 taps (halo schedule)
     if (a.ph[p].gchunks > 1 || a.ph[p].ntaps < 4) return hipErrorNotSupported;
-  if (half) return launch_wide_t<1, 1>(s, a, dmin, span);
+  if (half) return a.in_stride == 1 ? launch_wide_t<1, 1>(s, a, dmin, span) : launch_wide_t<2, 1>(s, a, dmin, span);
   return a.in_stride == 1 ? launch_wide_t<1, 2>(s, a, dmin, span) : launch_wide_t<2, 2>(s, a, dmin, span);
 }
 

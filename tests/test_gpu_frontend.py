@@ -68,6 +68,9 @@ CASES = [
     # wide kernel's 64-channel block (4 x 64 q-tiles): GeoBlock 64+g -> 64, transposed k3 s1 128 -> 64
     (False, 3, 1, 1, 0, 64, 0, (64,), 64, True, True, 0, (37, 151)),
     (True, 3, 1, 1, 0, 128, 0, (), 64, True, False, 0, (30, 70)),
+    # 64-channel block at input stride 2 (2 x 64 q-tiles, 32-column waves): GeoBlock conv1 32+32+g -> 64, 32+g -> 64
+    (False, 3, 2, 1, 0, 32, 32, (64,), 64, True, False, 0, (37, 151)),
+    (False, 3, 2, 1, 0, 32, 0, (32,), 64, True, True, 0, (64, 130)),
 ]
 
 
