@@ -164,15 +164,36 @@ def test_block_channels_is_the_blocked_permutation(C, dtype):
         assert torch.equal(got, src.view(B, h, w, C // E, E).permute(0, 3, 1, 2, 4).contiguous())
 
 
-@pytest.mark.parametrize("s,D,W", [(0, 48, 80), (1, 32, 80), (0, 64, 80), (2, 8, 72), (1, 16, 104), (1, 16, 70)])
+def test_prob_mfma_vector_stores_match(monkeypatch):
+    """prob_mfma's 16-byte probability stores (through the LDS column) against its one-store-per-pixel form
+    (DAMVS_PROB_VEC=0): the same values, bitwise, on ragged tiles."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine
+    net = CascadeMVSNet(ndepths=[48, 32, 8], compute_dtype=torch.bfloat16)
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    s, D, W = 1, 32, 72
+    feats, P, hyps = depthnet_inputs(B=2, N=3, H=40, W=W, D=D, stage_idx=s, C=16)
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.bfloat16,
+                      torch.device(DEV))
+    nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats]
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DAMVS_PROB_VEC", flag)
+        outs.append([t.clone() for t in eng.forward(nhwc, cuda(P), cuda(hyps))])
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("s,D,W", [(0, 48, 80), (1, 32, 80), (0, 64, 80), (2, 8, 72), (1, 16, 104)])
 @pytest.mark.parametrize("with_init", [False, True])
 def test_prob_mfma_vs_split_path(s, D, W, with_init):
     """bf16 stage regression (prob conv on MFMA + regression, prob_mfma_kernel in k_regress.hip: the default for
     bf16 storage) against the split path on the same U-Net output (damvs_costreg_logits: fp32-weight VALU prob
     conv, then damvs_regress). The MFMA form multiplies the bf16 voxels exactly by the fp32 weights carried as two
-    bf16 terms (relative weight error < 2^-17); W = 72 / 104 leave ragged 32-pixel tiles, W = 70 takes the 4-byte
-    probability stores (W % 4 != 0); with_init adds a
-    prob_volume_init (models/cas_mvsnet.py:107-108) to the logits."""
+    bf16 terms (relative weight error < 2^-17); W = 72 / 104 leave ragged 32-pixel tiles; with_init adds a
+    prob_volume_init (models/cas_mvsnet.py:107-108) to the logits. The probabilities leave as 16-byte runs (the stage
+    width is a multiple of 8); test_prob_mfma_vector_stores_match covers the 4-byte form."""
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import StageEngine, regress
     C = (32, 16, 8)[s]
