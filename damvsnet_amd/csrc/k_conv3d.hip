@@ -1234,6 +1234,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void deconv_xpair_zslide_kernel
 // group g = channel block g) in registers; per q-plane and half (pd) each wave issues its 8 skip
 // records first, then the 4 (py, px) phases x 2 q-rows, then the 16-byte epilogue (lane group g + 1
 // hands its 4 channels to group g). Same K order and weights as the gather kernel.
+template <bool AHEAD>
 __global__ __launch_bounds__(256) void deconv_c16_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y, int nzc,
                                                                 int zc, int ntiles) {
   typedef uint4 raw;
@@ -1301,23 +1302,33 @@ __global__ __launch_bounds__(256) void deconv_c16_zslide_kernel(const ConvArgs a
   const int qx = qx0 + n;
   constexpr int WOFF[8] = {0, 1, 3, 5, 9, 11, 15, 19};  // build_phases chunk offsets (Cin 32)
 
+  // the 8 skip records of output half (qz, pd): requested one half ahead of their use (the next half's while this
+  // half's MFMAs run); half (qz, pd) writes plane 2 qz + pd, the prefetched half reads plane 2 qz + pd + 1
+  auto skip_load = [&](int qz, int pd, uint32_t* off, raw* rq) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // k = (py, px, r)
+      const int py = k >> 2, px = (k >> 1) & 1, r = k & 1;
+      const int qy = qy0 + 2 * wave + r;
+      const bool ok = lead && qy < a.Hi && qx < a.Wi;
+      const int oz = 2 * qz + pd, oy = 2 * qy + py, ox = 2 * qx + px;
+      off[k] = ok ? (uint32_t)((((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * 16 + (co & 8)) * 2u : kOOB;
+      rq[k] = BufIO<bf16_t>::frag(rr, off[k]);
+    }
+  };
+  uint32_t offA[8], offB[8];
+  raw rqA[8], rqB[8];
+  if (AHEAD) skip_load(zb, 0, offA, rqA);
   auto step = [&](int qz, raw* cur, raw* nxt) {
     if (qz + 2 < zend) load_plane(qz + 3, nxt);
     const raw* p0 = ring + (qz & 3) * PLANE + lbase;
     const raw* p1 = ring + ((qz + 1) & 3) * PLANE + lbase;
 #pragma unroll
     for (int pd = 0; pd < 2; ++pd) {
-      uint32_t off[8];
-      raw rq[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {  // k = (py, px, r)
-        const int py = k >> 2, px = (k >> 1) & 1, r = k & 1;
-        const int qy = qy0 + 2 * wave + r;
-        const bool ok = lead && qy < a.Hi && qx < a.Wi;
-        const int oz = 2 * qz + pd, oy = 2 * qy + py, ox = 2 * qx + px;
-        off[k] = ok ? (uint32_t)((((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * 16 + (co & 8)) * 2u : kOOB;
-        rq[k] = BufIO<bf16_t>::frag(rr, off[k]);
-      }
+      const uint32_t* off = AHEAD ? (pd ? offB : offA) : offA;
+      const raw* rq = AHEAD ? (pd ? rqB : rqA) : rqA;
+      if (!AHEAD) skip_load(qz, pd, offA, rqA);  // (DAMVS_DECONV_SKIP_AHEAD=0) this half's records, right before use
+      else if (pd == 0) skip_load(qz, 1, offB, rqB);
+      else if (qz + 1 < zend) skip_load(qz + 1, 0, offA, rqA);
       f32x4_t acc[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
@@ -1521,7 +1532,11 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
     const int tx = (a.Wi + 15) / 16, ty = (a.Hi + 7) / 8, nzc = (a.Di + zc - 1) / zc;
     const long long nt = (long long)tx * ty * nzc * a.B;
     const size_t smem = 4 * 9 * 17 * 4 * 16;
-    hipLaunchKernelGGL(deconv_c16_zslide_kernel, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
+    const char* ah = getenv("DAMVS_DECONV_SKIP_AHEAD");  // read per call (A/B)
+    if (ah && ah[0] == '0')
+      hipLaunchKernelGGL(deconv_c16_zslide_kernel<false>, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
+    else
+      hipLaunchKernelGGL(deconv_c16_zslide_kernel<true>, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
     return hipGetLastError();
   }
   if (a.xpair) {
