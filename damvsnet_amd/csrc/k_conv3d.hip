@@ -1234,8 +1234,8 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void deconv_xpair_zslide_kernel
 // group g = channel block g) in registers; per q-plane and half (pd) each wave issues its 8 skip
 // records first, then the 4 (py, px) phases x 2 q-rows, then the 16-byte epilogue (lane group g + 1
 // hands its 4 channels to group g). Same K order and weights as the gather kernel.
-template <bool AHEAD>
-__global__ __launch_bounds__(256) void deconv_c16_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y, int nzc,
+template <bool AHEAD, bool ALDS>
+__global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y, int nzc,
                                                                 int zc, int ntiles) {
   typedef uint4 raw;
   constexpr int CH = 4, QX = 16, QY = 8, PW = QX + 1, PH = QY + 1;
@@ -1274,8 +1274,13 @@ __global__ __launch_bounds__(256) void deconv_c16_zslide_kernel(const ConvArgs a
       if (c < PLANE) dst[c] = v[i];
     }
   };
-  raw wreg[27];
-  {
+  // ALDS: the 27 A fragments in LDS after the ring (27 KB) instead of 108 VGPRs, for two waves per SIMD
+  raw wreg[ALDS ? 1 : 27];
+  raw* aw = ring + 4 * PLANE;
+  if constexpr (ALDS) {
+    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack);
+    for (int i = threadIdx.x; i < 27 * 64; i += 256) aw[i] = wsrc[i];
+  } else {
     const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack) + (threadIdx.x & 63);
 #pragma unroll
     for (int s = 0; s < 27; ++s) wreg[s] = wsrc[(size_t)s * 64];
@@ -1346,7 +1351,8 @@ __global__ __launch_bounds__(256) void deconv_c16_zslide_kernel(const ConvArgs a
               for (int ic = 0; ic < nc; ++ic) {
                 const int zo = pd ? (ia == 0 ? 1 : 0) : 0, yo = py ? (ib == 0 ? 1 : 0) : 0;
                 const int xo = px ? (ic == 0 ? 1 : 0) : 0;
-                const raw w = wreg[WOFF[ph] + (ia * nb + ib) * nc + ic];
+                const raw w = ALDS ? aw[(WOFF[ph] + (ia * nb + ib) * nc + ic) * 64 + (threadIdx.x & 63)]
+                                   : wreg[ALDS ? 0 : WOFF[ph] + (ia * nb + ib) * nc + ic];
                 const raw* src = (zo ? p1 : p0) + (yo * PW + xo) * CH;
 #pragma unroll
                 for (int r = 0; r < 2; ++r)
@@ -1532,11 +1538,23 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
     const int tx = (a.Wi + 15) / 16, ty = (a.Hi + 7) / 8, nzc = (a.Di + zc - 1) / zc;
     const long long nt = (long long)tx * ty * nzc * a.B;
     const size_t smem = 4 * 9 * 17 * 4 * 16;
-    const char* ah = getenv("DAMVS_DECONV_SKIP_AHEAD");  // read per call (A/B)
-    if (ah && ah[0] == '0')
-      hipLaunchKernelGGL(deconv_c16_zslide_kernel<false>, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
-    else
-      hipLaunchKernelGGL(deconv_c16_zslide_kernel<true>, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
+    // read per call (A/B): DAMVS_DECONV_SKIP_AHEAD=1 requests each half's skip records one half earlier (measured
+    // flat: U-Net 1.154-1.159 / 2.060-2.079 / 1.870-1.892 against 1.144-1.151 / 2.061-2.076 / 1.886-1.893 ms,
+    // profiles/r03/ab_conv9.jsonl); DAMVS_DECONV_A_LDS=1 keeps the A fragments in LDS (2 waves per SIMD)
+    const char* ah = getenv("DAMVS_DECONV_SKIP_AHEAD");
+    const char* al = getenv("DAMVS_DECONV_A_LDS");
+    const bool ahead = ah && ah[0] == '1', alds = al && al[0] == '1';
+    const size_t sm = alds ? smem + 27 * 64 * 16 : smem;
+    if (alds) {
+      if (ahead)
+        hipLaunchKernelGGL((deconv_c16_zslide_kernel<true, true>), dim3((unsigned)nt), dim3(256), sm, s, a, tx, ty, nzc, zc, (int)nt);
+      else
+        hipLaunchKernelGGL((deconv_c16_zslide_kernel<false, true>), dim3((unsigned)nt), dim3(256), sm, s, a, tx, ty, nzc, zc, (int)nt);
+    } else if (ahead) {
+      hipLaunchKernelGGL((deconv_c16_zslide_kernel<true, false>), dim3((unsigned)nt), dim3(256), sm, s, a, tx, ty, nzc, zc, (int)nt);
+    } else {
+      hipLaunchKernelGGL((deconv_c16_zslide_kernel<false, false>), dim3((unsigned)nt), dim3(256), sm, s, a, tx, ty, nzc, zc, (int)nt);
+    }
     return hipGetLastError();
   }
   if (a.xpair) {

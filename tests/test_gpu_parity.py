@@ -524,7 +524,7 @@ def test_conv0_zslide_matches_tile_kernel(s, D, H, W, monkeypatch):
     """The z-streaming kernels (bf16) against the kernels they replace, each on the same U-Net:
     conv0's ring-buffer row-pair kernel vs the 4x8x16-tile row-pair kernel, conv0's input-plane walk (each plane's
     fragments read once for three output planes) vs the output-plane walk, conv9 with its skip records requested one
-    half ahead vs right before use, and conv11's z-streamed
+    half ahead vs right before use and with its A fragments in LDS vs registers, and conv11's z-streamed
     x-pair deconv vs the x-pair gather kernel. Same K order and accumulation chains, so the logits
     agree bitwise (partial tiles included)."""
     from damvsnet_amd.cascade import CascadeMVSNet
@@ -537,8 +537,9 @@ def test_conv0_zslide_matches_tile_kernel(s, D, H, W, monkeypatch):
                       torch.device(DEV))
     nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats]
     vol = eng.warp_aggregate(nhwc, cuda(P), cuda(hyps))
-    for knob in ("DAMVS_CONV_NO_ZSLIDE", "DAMVS_DECONV_NO_ZSLIDE", "DAMVS_CONV0_REUSE", "DAMVS_DECONV_SKIP_AHEAD"):
-        on, off = ("1", "0") if knob in ("DAMVS_CONV0_REUSE", "DAMVS_DECONV_SKIP_AHEAD") else ("0", "1")
+    for knob in ("DAMVS_CONV_NO_ZSLIDE", "DAMVS_DECONV_NO_ZSLIDE", "DAMVS_CONV0_REUSE", "DAMVS_DECONV_SKIP_AHEAD",
+                 "DAMVS_DECONV_A_LDS"):
+        on, off = ("1", "0") if knob.startswith(("DAMVS_CONV0", "DAMVS_DECONV_SKIP", "DAMVS_DECONV_A")) else ("0", "1")
         monkeypatch.setenv(knob, on)
         a = eng.costreg_logits(vol).clone()
         monkeypatch.setenv(knob, off)
