@@ -1540,10 +1540,12 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
     const size_t smem = 4 * 9 * 17 * 4 * 16;
     // read per call (A/B): DAMVS_DECONV_SKIP_AHEAD=1 requests each half's skip records one half earlier (measured
     // flat: U-Net 1.154-1.159 / 2.060-2.079 / 1.870-1.892 against 1.144-1.151 / 2.061-2.076 / 1.886-1.893 ms,
-    // profiles/r03/ab_conv9.jsonl); DAMVS_DECONV_A_LDS=1 keeps the A fragments in LDS (2 waves per SIMD)
+    // profiles/r03/ab_conv9.jsonl); the A fragments sit in LDS (27 KB) instead of 108 VGPRs, two waves per SIMD
+    // instead of one: U-Net 1.136-1.149 / 2.071-2.102 / 1.879-1.884 -> 1.128-1.129 / 2.020-2.024 / 1.826-1.837 ms
+    // (same file; DAMVS_DECONV_A_LDS=0 restores the register form)
     const char* ah = getenv("DAMVS_DECONV_SKIP_AHEAD");
     const char* al = getenv("DAMVS_DECONV_A_LDS");
-    const bool ahead = ah && ah[0] == '1', alds = al && al[0] == '1';
+    const bool ahead = ah && ah[0] == '1', alds = !(al && al[0] == '0');
     const size_t sm = alds ? smem + 27 * 64 * 16 : smem;
     if (alds) {
       if (ahead)

@@ -540,6 +540,8 @@ def test_conv0_zslide_matches_tile_kernel(s, D, H, W, monkeypatch):
     for knob in ("DAMVS_CONV_NO_ZSLIDE", "DAMVS_DECONV_NO_ZSLIDE", "DAMVS_CONV0_REUSE", "DAMVS_DECONV_SKIP_AHEAD",
                  "DAMVS_DECONV_A_LDS"):
         on, off = ("1", "0") if knob.startswith(("DAMVS_CONV0", "DAMVS_DECONV_SKIP", "DAMVS_DECONV_A")) else ("0", "1")
+        if knob == "DAMVS_DECONV_SKIP_AHEAD":
+            on, off = off, on  # default off: compare the opt-in form against it
         monkeypatch.setenv(knob, on)
         a = eng.costreg_logits(vol).clone()
         monkeypatch.setenv(knob, off)
