@@ -11,6 +11,9 @@
 //  sparse_pool  : GeoFeatureFusion's depth pyramid, models/geometry.py:90-96 (normalised depth and
 //                 valid mask) and SparseDownSampleClose(stride 2), models/geometry.py:443-455, one
 //                 launch per level instead of ~10 elementwise/max-pool launches.
+#include <cstdint>
+#include <cstdlib>
+
 #include "damvs_device.h"
 
 namespace damvs {
@@ -105,21 +108,13 @@ __device__ __forceinline__ float bilerp(const float* m, int wp, int y0, int y1, 
   return ly0 * (lx0 * m[y0 * wp + x0] + lx1 * m[y0 * wp + x1]) + ly1 * (lx0 * m[y1 * wp + x0] + lx1 * m[y1 * wp + x1]);
 }
 
-__global__ void hyp_refine_kernel(int B, int D, int H, int W, int scale, const float* __restrict__ pd,
-                                  const float* __restrict__ pv, int hp, int wp, float* __restrict__ out) {
-  const int h = H / scale, w = W / scale;
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
-  int b = blockIdx.y;
-  if (p >= h * w) return;
-  int y = p / w, x = p % w;
+// The full-resolution points feeding output pixel (y, x) (1 or scale^2 = 4 of them), with their softmax constants.
+__device__ __forceinline__ void hyp_points(int D, int H, int W, int scale, int y, int x, const float* md, const float* mv,
+                                           int hp, int wp, FullResPoint* P) {
   const float eps = 1e-12f;
   const float sh = (float)hp / (float)H, sw = (float)wp / (float)W;
-  const float* md = pd + (size_t)b * hp * wp;
-  const float* mv = pv + (size_t)b * hp * wp;
   const float rden = (float)D - 1.f;
-
-  FullResPoint P[4];
-  const int n = scale * scale;  // 1 or 4 full-resolution points feed this output
+  const int n = scale * scale;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (k >= n) break;
@@ -142,18 +137,57 @@ __global__ void hyp_refine_kernel(int B, int D, int H, int W, int scale, const f
     q.rsum = 1.f / s;
     P[k] = q;
   }
+}
+
+// Hypothesis i of an output pixel from its points (the trilinear x1/2 average of 4 full-resolution values at scale 2).
+__device__ __forceinline__ float hyp_value(const FullResPoint* P, int scale, int i) {
+  const float eps = 1e-12f;
+  const int n = scale * scale;
+  float v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k >= n) break;
+    const FullResPoint& q = P[k];
+    const float off = __expf((q.low + q.step * (float)i) * q.k3 - q.mx) * q.rsum;
+    v[k] = (q.cur + q.low + q.step * (float)i + eps) + off * q.step;
+  }
+  return (scale == 1) ? v[0] : 0.5f * (0.5f * v[0] + 0.5f * v[1]) + 0.5f * (0.5f * v[2] + 0.5f * v[3]);
+}
+
+__global__ void hyp_refine_kernel(int B, int D, int H, int W, int scale, const float* __restrict__ pd,
+                                  const float* __restrict__ pv, int hp, int wp, float* __restrict__ out) {
+  const int h = H / scale, w = W / scale;
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  int b = blockIdx.y;
+  if (p >= h * w) return;
+  int y = p / w, x = p % w;
+  FullResPoint P[4];
+  hyp_points(D, H, W, scale, y, x, pd + (size_t)b * hp * wp, pv + (size_t)b * hp * wp, hp, wp, P);
+  float* o = out + (size_t)b * D * h * w + p;
+  for (int i = 0; i < D; ++i) o[(size_t)i * h * w] = hyp_value(P, scale, i);
+}
+
+// PX consecutive output pixels per thread, written as one PX x 4-byte store per plane (w % PX == 0): the same values
+// as hyp_refine_kernel (the per-pixel arithmetic is shared), a quarter / half of the store instructions.
+template <int PX>
+__global__ void hyp_refine_vec_kernel(int B, int D, int H, int W, int scale, const float* __restrict__ pd,
+                                      const float* __restrict__ pv, int hp, int wp, float* __restrict__ out) {
+  typedef float fvec __attribute__((ext_vector_type(PX)));
+  const int h = H / scale, w = W / scale;
+  const int p = (blockIdx.x * blockDim.x + threadIdx.x) * PX;
+  const int b = blockIdx.y;
+  if (p >= h * w) return;
+  const int y = p / w, x = p % w;
+  FullResPoint P[PX][4];
+#pragma unroll
+  for (int j = 0; j < PX; ++j)
+    hyp_points(D, H, W, scale, y, x + j, pd + (size_t)b * hp * wp, pv + (size_t)b * hp * wp, hp, wp, P[j]);
   float* o = out + (size_t)b * D * h * w + p;
   for (int i = 0; i < D; ++i) {
-    float v[4];
+    fvec r;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (k >= n) break;
-      const FullResPoint& q = P[k];
-      const float off = __expf((q.low + q.step * (float)i) * q.k3 - q.mx) * q.rsum;
-      v[k] = (q.cur + q.low + q.step * (float)i + eps) + off * q.step;
-    }
-    float r = (scale == 1) ? v[0] : 0.5f * (0.5f * v[0] + 0.5f * v[1]) + 0.5f * (0.5f * v[2] + 0.5f * v[3]);
-    o[(size_t)i * h * w] = r;
+    for (int j = 0; j < PX; ++j) r[j] = hyp_value(P[j], scale, i);
+    *reinterpret_cast<fvec*>(o + (size_t)i * h * w) = r;
   }
 }
 
@@ -243,6 +277,20 @@ hipError_t launch_hyp_linear(hipStream_t s, int B, int D, int h, int w, const fl
 hipError_t launch_hyp_refine(hipStream_t s, int B, int D, int H, int W, int scale, const float* pd, const float* pv,
                              int hp, int wp, float* out) {
   int hw = (H / scale) * (W / scale);
+  // vector stores: 4 pixels per thread at scale 1, 2 at scale 2 (register budget of 4 / 8 points), when rows and the
+  // output are aligned for them (DAMVS_HYP_VEC=0, read per call: one pixel per thread)
+  const char* hv = getenv("DAMVS_HYP_VEC");
+  const int px = scale == 1 ? 4 : 2;
+  if (!(hv && hv[0] == '0') && (W / scale) % px == 0 && reinterpret_cast<uintptr_t>(out) % (4 * px) == 0) {
+    const int nt = hw / px;
+    if (px == 4)
+      hipLaunchKernelGGL(hyp_refine_vec_kernel<4>, dim3((nt + 255) / 256, B), dim3(256), 0, s, B, D, H, W, scale, pd, pv,
+                         hp, wp, out);
+    else
+      hipLaunchKernelGGL(hyp_refine_vec_kernel<2>, dim3((nt + 255) / 256, B), dim3(256), 0, s, B, D, H, W, scale, pd, pv,
+                         hp, wp, out);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(hyp_refine_kernel, dim3((hw + 255) / 256, B), dim3(256), 0, s, B, D, H, W, scale, pd, pv, hp, wp,
                      out);
   return hipGetLastError();

@@ -339,6 +339,27 @@ def test_hypotheses_vs_oracle(stage):
     assert rel_max(np_(out), ref.numpy()) < 2e-6
 
 
+@pytest.mark.parametrize("stage,W", [(1, 96), (2, 96), (1, 100), (2, 98)])
+def test_hypotheses_vector_stores_bitwise(stage, W, monkeypatch):
+    """hyp_refine with 4 (stage 3) / 2 (stage 2) output pixels per thread and vector stores against one pixel per
+    thread: the same per-pixel arithmetic, bitwise (W = 100 / 98 leave row widths the vector form does not take at one
+    of the scales and fall back)."""
+    from damvsnet_amd.engine import hypotheses
+    from damvsnet_amd import synth
+    B, H = 2, 64
+    nd, scale, ps = (48, 32, 8)[stage], (4, 2, 1)[stage], (4, 2)[stage - 1]
+    _, _, dv = synth.cameras(B, 2, H, W)
+    g = torch.Generator().manual_seed(10 + stage)
+    pd = cuda(600 + 100 * torch.rand(B, H // ps, W // ps, generator=g))
+    pv = cuda(1 + 40 * torch.rand(B, H // ps, W // ps, generator=g))
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DAMVS_HYP_VEC", flag)
+        outs.append(hypotheses(cuda(torch.from_numpy(dv)), nd, H, W, scale, pd, pv).clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
 # ----------------------------------------------------------------------------- DepthNet (A1)
 
 @pytest.mark.parametrize("mode", ["adaptive", "variance"])
