@@ -277,11 +277,13 @@ hipError_t launch_hyp_linear(hipStream_t s, int B, int D, int h, int w, const fl
 hipError_t launch_hyp_refine(hipStream_t s, int B, int D, int H, int W, int scale, const float* pd, const float* pv,
                              int hp, int wp, float* out) {
   int hw = (H / scale) * (W / scale);
-  // vector stores: 4 pixels per thread at scale 1, 2 at scale 2 (register budget of 4 / 8 points), when rows and the
-  // output are aligned for them (DAMVS_HYP_VEC=0, read per call: one pixel per thread)
+  // DAMVS_HYP_VEC=1 (read per call, A/B): 4 pixels per thread at scale 1, 2 at scale 2 with vector stores, when rows
+  // and the output are aligned for them. Measured slower (stage 2 / 3 hypotheses 0.113-0.117 / 0.073-0.074 ms ->
+  // 0.124-0.128 / 0.082-0.084, profiles/r03/ab_hyp.jsonl): the per-point softmax sums, not the stores, set the time,
+  // and a quarter of the threads hides less of them. Off by default.
   const char* hv = getenv("DAMVS_HYP_VEC");
   const int px = scale == 1 ? 4 : 2;
-  if (!(hv && hv[0] == '0') && (W / scale) % px == 0 && reinterpret_cast<uintptr_t>(out) % (4 * px) == 0) {
+  if (hv && hv[0] == '1' && (W / scale) % px == 0 && reinterpret_cast<uintptr_t>(out) % (4 * px) == 0) {
     const int nt = hw / px;
     if (px == 4)
       hipLaunchKernelGGL(hyp_refine_vec_kernel<4>, dim3((nt + 255) / 256, B), dim3(256), 0, s, B, D, H, W, scale, pd, pv,
