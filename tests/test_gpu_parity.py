@@ -360,6 +360,26 @@ def test_hypotheses_vector_stores_bitwise(stage, W, monkeypatch):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("W,D", [(96, 32), (98, 32), (100, 24)])
+def test_hypotheses_quad_lanes_bitwise(W, D, monkeypatch):
+    """Stage-2 hypotheses (scale 2) with one lane per full-resolution point (hyp_refine_quad_kernel: cached softmax
+    terms, the quad's values combined by DPP) against one lane per output pixel: bitwise, incl. a partial last block
+    and D < 32."""
+    from damvsnet_amd.engine import hypotheses
+    from damvsnet_amd import synth
+    B, H = 2, 64
+    _, _, dv = synth.cameras(B, 2, H, W)
+    g = torch.Generator().manual_seed(W + D)
+    pd = cuda(600 + 100 * torch.rand(B, H // 4, W // 4, generator=g))
+    pv = cuda(1 + 40 * torch.rand(B, H // 4, W // 4, generator=g))
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DAMVS_HYP_QUAD", flag)
+        outs.append(hypotheses(cuda(torch.from_numpy(dv)), D, H, W, 2, pd, pv).clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
 # ----------------------------------------------------------------------------- DepthNet (A1)
 
 @pytest.mark.parametrize("mode", ["adaptive", "variance"])
