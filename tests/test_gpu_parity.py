@@ -361,10 +361,10 @@ def test_hypotheses_vector_stores_bitwise(stage, W, monkeypatch):
 
 
 @pytest.mark.parametrize("W,D", [(96, 32), (98, 32), (100, 24)])
-def test_hypotheses_quad_lanes_bitwise(W, D, monkeypatch):
-    """Stage-2 hypotheses (scale 2) with one lane per full-resolution point (hyp_refine_quad_kernel: cached softmax
-    terms, the quad's values combined by DPP) against one lane per output pixel: bitwise, incl. a partial last block
-    and D < 32."""
+def test_hypotheses_quad_lanes(W, D, monkeypatch):
+    """Stage-2 hypotheses (scale 2) with one lane per full-resolution point (opt-in hyp_refine_quad_kernel: cached
+    softmax terms, the quad's values combined by DPP) against one lane per output pixel, incl. a partial last block and
+    D < 32: within 1e-6 relative (floating-point contraction differs between the two forms; the oracle gate is 2e-6)."""
     from damvsnet_amd.engine import hypotheses
     from damvsnet_amd import synth
     B, H = 2, 64
@@ -377,7 +377,7 @@ def test_hypotheses_quad_lanes_bitwise(W, D, monkeypatch):
         monkeypatch.setenv("DAMVS_HYP_QUAD", flag)
         outs.append(hypotheses(cuda(torch.from_numpy(dv)), D, H, W, 2, pd, pv).clone())
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
+    assert rel_max(np_(outs[0]), np_(outs[1])) < 1e-6
 
 
 # ----------------------------------------------------------------------------- DepthNet (A1)
