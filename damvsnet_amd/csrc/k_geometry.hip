@@ -167,98 +167,6 @@ __global__ void hyp_refine_kernel(int B, int D, int H, int W, int scale, const f
   for (int i = 0; i < D; ++i) o[(size_t)i * h * w] = hyp_value(P, scale, i);
 }
 
-// PX consecutive output pixels per thread, written as one PX x 4-byte store per plane (w % PX == 0): the same values
-// as hyp_refine_kernel (the per-pixel arithmetic is shared), a quarter / half of the store instructions.
-template <int PX>
-__global__ void hyp_refine_vec_kernel(int B, int D, int H, int W, int scale, const float* __restrict__ pd,
-                                      const float* __restrict__ pv, int hp, int wp, float* __restrict__ out) {
-  typedef float fvec __attribute__((ext_vector_type(PX)));
-  const int h = H / scale, w = W / scale;
-  const int p = (blockIdx.x * blockDim.x + threadIdx.x) * PX;
-  const int b = blockIdx.y;
-  if (p >= h * w) return;
-  const int y = p / w, x = p % w;
-  FullResPoint P[PX][4];
-#pragma unroll
-  for (int j = 0; j < PX; ++j)
-    hyp_points(D, H, W, scale, y, x + j, pd + (size_t)b * hp * wp, pv + (size_t)b * hp * wp, hp, wp, P[j]);
-  float* o = out + (size_t)b * D * h * w + p;
-  for (int i = 0; i < D; ++i) {
-    fvec r;
-#pragma unroll
-    for (int j = 0; j < PX; ++j) r[j] = hyp_value(P[j], scale, i);
-    *reinterpret_cast<fvec*>(o + (size_t)i * h * w) = r;
-  }
-}
-
-// Scale 2 (stage 2) with one lane per full-resolution point: the 4 lanes of a quad own the 4 points of an output pixel,
-// each keeps its point's D <= 32 softmax terms from the sum loop (hyp_refine_kernel evaluates every term twice) and
-// the quad combines its values in the reference's order by DPP quad permutes; lane k stores planes i = k (mod 4).
-// Same per-point expressions and combination as hyp_refine_kernel; the unrolled code contracts some of them into FMAs
-// differently, so the two agree to ~1 ulp, not bitwise (opt-in, see launch_hyp_refine).
-template <int CTRL>
-__device__ __forceinline__ float qperm(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-
-__global__ __launch_bounds__(256) void hyp_refine_quad_kernel(int B, int D, int H, int W, const float* __restrict__ pd,
-                                                              const float* __restrict__ pv, int hp, int wp,
-                                                              float* __restrict__ out) {
-  constexpr int DM = 32;
-  const int h = H / 2, w = W / 2;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int p = t >> 2, k = t & 3;  // output pixel, point (dy, dx) = (k >> 1, k & 1)
-  const int b = blockIdx.y;
-  const bool valid = p < h * w;      // the quad's lanes stay together (whole quads share p)
-  const int pp = valid ? p : 0;
-  const int y = pp / w, x = pp % w;
-  const float eps = 1e-12f;
-  const float sh = (float)hp / (float)H, sw = (float)wp / (float)W;
-  const float* md = pd + (size_t)b * hp * wp;
-  const float* mv = pv + (size_t)b * hp * wp;
-  const float rden = (float)D - 1.f;
-  int y0, y1, x0, x1;
-  float ly0, ly1, lx0, lx1;
-  src_index(sh, y * 2 + (k >> 1), hp, y0, y1, ly0, ly1);
-  src_index(sw, x * 2 + (k & 1), wp, x0, x1, lx0, lx1);
-  FullResPoint q;
-  q.cur = bilerp(md, wp, y0, y1, x0, x1, ly0, ly1, lx0, lx1);
-  q.var = bilerp(mv, wp, y0, y1, x0, x1, ly0, ly1, lx0, lx1);
-  q.low = -fminf(q.cur, q.var);
-  q.step = (q.var - q.low) / rden;
-  q.k3 = 3.f / (q.var + eps);
-  q.mx = fmaxf(q.low * q.k3, (q.low + q.step * (float)(D - 1)) * q.k3);
-  float e[DM];
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < DM; ++i) {
-    e[i] = i < D ? __expf((q.low + q.step * (float)i) * q.k3 - q.mx) : 0.f;
-    if (i < D) s += e[i];
-  }
-  q.rsum = 1.f / s;
-  float* o = out + (size_t)b * D * h * w + pp;
-#pragma unroll
-  for (int i0 = 0; i0 < DM; i0 += 4) {
-    if (i0 >= D) break;
-    float r[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = i0 + u;
-      const float off = e[i] * q.rsum;
-      const float v = (q.cur + q.low + q.step * (float)i + eps) + off * q.step;
-      // the quad's 4 values in point order: lane k holds v_k; v_j comes from lane k ^ (k ^ j)
-      const float x1v = qperm<0xB1>(v), x2v = qperm<0x4E>(v), x3v = qperm<0x1B>(v);  // quad lanes k ^ 1, k ^ 2, k ^ 3
-      const float v0 = k == 0 ? v : k == 1 ? x1v : k == 2 ? x2v : x3v;
-      const float v1 = k == 1 ? v : k == 0 ? x1v : k == 3 ? x2v : x3v;
-      const float v2 = k == 2 ? v : k == 3 ? x1v : k == 0 ? x2v : x3v;
-      const float v3 = k == 3 ? v : k == 2 ? x1v : k == 1 ? x2v : x3v;
-      r[u] = 0.5f * (0.5f * v0 + 0.5f * v1) + 0.5f * (0.5f * v2 + 0.5f * v3);
-    }
-    const int i = i0 + k;
-    if (valid && i < D) o[(size_t)i * h * w] = k == 0 ? r[0] : k == 1 ? r[1] : k == 2 ? r[2] : r[3];
-  }
-}
-
 // One 2x2 stride-2 window of SparseDownSampleClose: the pooled max of encode = -(1-m)*600 - d (scanned
 // row-major with aten's max_pool "v > max || isnan(v)" update, so ties and NaNs resolve identically)
 // and of the mask; d_out = -max(encode) - (1 - max(mask)) * 600. Every product is exact (m is 0 or 1).
@@ -345,31 +253,9 @@ hipError_t launch_hyp_linear(hipStream_t s, int B, int D, int h, int w, const fl
 hipError_t launch_hyp_refine(hipStream_t s, int B, int D, int H, int W, int scale, const float* pd, const float* pv,
                              int hp, int wp, float* out) {
   int hw = (H / scale) * (W / scale);
-  // DAMVS_HYP_VEC=1 (read per call, A/B): 4 pixels per thread at scale 1, 2 at scale 2 with vector stores, when rows
-  // and the output are aligned for them. Measured slower (stage 2 / 3 hypotheses 0.113-0.117 / 0.073-0.074 ms ->
-  // 0.124-0.128 / 0.082-0.084, profiles/r03/ab_hyp.jsonl): the per-point softmax sums, not the stores, set the time,
-  // and a quarter of the threads hides less of them. Off by default.
-  const char* hv = getenv("DAMVS_HYP_VEC");
-  const int px = scale == 1 ? 4 : 2;
-  if (hv && hv[0] == '1' && (W / scale) % px == 0 && reinterpret_cast<uintptr_t>(out) % (4 * px) == 0) {
-    const int nt = hw / px;
-    if (px == 4)
-      hipLaunchKernelGGL(hyp_refine_vec_kernel<4>, dim3((nt + 255) / 256, B), dim3(256), 0, s, B, D, H, W, scale, pd, pv,
-                         hp, wp, out);
-    else
-      hipLaunchKernelGGL(hyp_refine_vec_kernel<2>, dim3((nt + 255) / 256, B), dim3(256), 0, s, B, D, H, W, scale, pd, pv,
-                         hp, wp, out);
-    return hipGetLastError();
-  }
-  // DAMVS_HYP_QUAD=1 (read per call, opt-in): scale 2, D <= 32 with one lane per full-resolution point. Not bitwise
-  // the one-lane kernel (the unrolled form's floating-point contraction differs: within 1e-6 relative, the oracle gate
-  // holds), and not yet timed in the pipeline, so the default stays one lane per output pixel.
-  const char* hq = getenv("DAMVS_HYP_QUAD");
-  if (scale == 2 && D <= 32 && hq && hq[0] == '1') {
-    hipLaunchKernelGGL(hyp_refine_quad_kernel, dim3((4 * hw + 255) / 256, B), dim3(256), 0, s, B, D, H, W, pd, pv, hp,
-                       wp, out);
-    return hipGetLastError();
-  }
+  // (measured and dropped in round 3, profiles/r03/ab_hyp*.jsonl: 4 / 2 output pixels per thread with vector stores,
+  // 0.113-0.117 -> 0.124-0.128 ms at stage 2; one lane per full-resolution point with the softmax terms kept,
+  // 0.110-0.113 -> 0.212-0.216 ms. One lane per output pixel stays.)
   hipLaunchKernelGGL(hyp_refine_kernel, dim3((hw + 255) / 256, B), dim3(256), 0, s, B, D, H, W, scale, pd, pv, hp, wp,
                      out);
   return hipGetLastError();

@@ -339,47 +339,6 @@ def test_hypotheses_vs_oracle(stage):
     assert rel_max(np_(out), ref.numpy()) < 2e-6
 
 
-@pytest.mark.parametrize("stage,W", [(1, 96), (2, 96), (1, 100), (2, 98)])
-def test_hypotheses_vector_stores_bitwise(stage, W, monkeypatch):
-    """hyp_refine with 4 (stage 3) / 2 (stage 2) output pixels per thread and vector stores against one pixel per
-    thread: the same per-pixel arithmetic, bitwise (W = 100 / 98 leave row widths the vector form does not take at one
-    of the scales and fall back)."""
-    from damvsnet_amd.engine import hypotheses
-    from damvsnet_amd import synth
-    B, H = 2, 64
-    nd, scale, ps = (48, 32, 8)[stage], (4, 2, 1)[stage], (4, 2)[stage - 1]
-    _, _, dv = synth.cameras(B, 2, H, W)
-    g = torch.Generator().manual_seed(10 + stage)
-    pd = cuda(600 + 100 * torch.rand(B, H // ps, W // ps, generator=g))
-    pv = cuda(1 + 40 * torch.rand(B, H // ps, W // ps, generator=g))
-    outs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("DAMVS_HYP_VEC", flag)
-        outs.append(hypotheses(cuda(torch.from_numpy(dv)), nd, H, W, scale, pd, pv).clone())
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
-
-
-@pytest.mark.parametrize("W,D", [(96, 32), (98, 32), (100, 24)])
-def test_hypotheses_quad_lanes(W, D, monkeypatch):
-    """Stage-2 hypotheses (scale 2) with one lane per full-resolution point (opt-in hyp_refine_quad_kernel: cached
-    softmax terms, the quad's values combined by DPP) against one lane per output pixel, incl. a partial last block and
-    D < 32: within 1e-6 relative (floating-point contraction differs between the two forms; the oracle gate is 2e-6)."""
-    from damvsnet_amd.engine import hypotheses
-    from damvsnet_amd import synth
-    B, H = 2, 64
-    _, _, dv = synth.cameras(B, 2, H, W)
-    g = torch.Generator().manual_seed(W + D)
-    pd = cuda(600 + 100 * torch.rand(B, H // 4, W // 4, generator=g))
-    pv = cuda(1 + 40 * torch.rand(B, H // 4, W // 4, generator=g))
-    outs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("DAMVS_HYP_QUAD", flag)
-        outs.append(hypotheses(cuda(torch.from_numpy(dv)), D, H, W, 2, pd, pv).clone())
-    torch.cuda.synchronize()
-    assert rel_max(np_(outs[0]), np_(outs[1])) < 1e-6
-
-
 # ----------------------------------------------------------------------------- DepthNet (A1)
 
 @pytest.mark.parametrize("mode", ["adaptive", "variance"])
