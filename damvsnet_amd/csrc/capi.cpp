@@ -59,6 +59,7 @@ struct LayerPlan {
   int nphase_pair = 0;
   ConvPhase ph_pair[4];
   float* bias = nullptr;
+  float wscale = 1.f;  // fp32: 2^-k of the split-f16 weights (split_weights)
 };
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -221,8 +222,37 @@ void pack_layer_xpair(LayerPlan& P, const std::vector<float>& wf, int E, std::ve
   }
 }
 
+int upload(const void* host, size_t bytes, void** dev);
 float cvt_f32(float v) { return v; }
 uint16_t cvt_bf16(float v) { return to_bf16(v); }
+
+// fp32 layers compute on split-f16 MFMAs (damvs_device.h, mma_split16): the per-layer exponent k that puts the largest
+// |w| * 2^k in (2^13, 2^14], so every lo piece that matters is a normal f16 (0 for an all-zero layer).
+int split_exponent(const std::vector<float>& w) {
+  float mx = 0.f;
+  for (float v : w) mx = std::max(mx, std::fabs(v));
+  if (!(mx > 0.f) || !std::isfinite(mx)) return 0;
+  int e;
+  std::frexp(mx, &e);  // mx = f * 2^e, f in [0.5, 1)
+  return 14 - e;
+}
+// A fragments packed as fp32 (4 values per lane and chunk) -> [hi0..hi3 | lo0..lo3] f16 of w * 2^k
+std::vector<uint16_t> split_weights(const std::vector<float>& pk, int k) {
+  std::vector<uint16_t> out(pk.size() * 2);
+  for (size_t q = 0; q < pk.size() / 4; ++q)
+    for (int e = 0; e < 4; ++e) {
+      const float v = std::ldexp(pk[q * 4 + e], k);
+      const _Float16 hi = (_Float16)v;
+      const _Float16 lo = (_Float16)(v - (float)hi);
+      std::memcpy(&out[q * 8 + e], &hi, 2);
+      std::memcpy(&out[q * 8 + 4 + e], &lo, 2);
+    }
+  return out;
+}
+int upload_split(const std::vector<float>& pk, int k, void** dev) {
+  const std::vector<uint16_t> h = split_weights(pk, k);
+  return upload(h.data(), h.size() * 2, dev);
+}
 
 int fold_bn(const damvs_bn& bn, int c, std::vector<float>& scale, std::vector<float>& shift) {
   if (!bn.weight || !bn.bias || !bn.running_mean || !bn.running_var) return fail(DAMVS_E_ARG, "null BatchNorm tensor");
@@ -342,6 +372,7 @@ ConvArgs conv_args(const damvs_stage* st, int li, int B, const Shapes& S, int li
     a.out_stride = 1;
   }
   a.relu = 1;
+  a.wscale = P.wscale;
   a.nphase = P.nphase;
   std::memcpy(a.ph, P.ph, sizeof(a.ph));
   if (P.kind == DECONV_S2 && P.wpack_pair && P.cout == 8 && !conv_xpair_disabled()) {
@@ -475,6 +506,8 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
           const float v = P.kind == DECONV_S2 ? W[((size_t)ci * P.cout + co) * 27 + t] : W[((size_t)co * P.cin + ci) * 27 + t];
           wf[((size_t)co * P.cin + ci) * 27 + t] = v * scale[co];
         }
+    const int kexp = dtype == DAMVS_BF16 ? 0 : split_exponent(wf);
+    P.wscale = std::ldexp(1.f, -kexp);
     if (dtype == DAMVS_BF16) {
       std::vector<uint16_t> pk;
       pack_layer<uint16_t>(P, wf, E, pk, cvt_bf16);
@@ -482,7 +515,7 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
     } else {
       std::vector<float> pk;
       pack_layer<float>(P, wf, E, pk, cvt_f32);
-      rc = upload(pk.data(), pk.size() * 4, &P.wpack);
+      rc = upload_split(pk, kexp, &P.wpack);
     }
     if (rc == DAMVS_OK && P.kind == DECONV_S2 && P.cout <= 8) {
       build_phases_xpair(P, 4 * E);
@@ -493,7 +526,7 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
       } else {
         std::vector<float> pk;
         pack_layer_xpair<float>(P, wf, E, pk, cvt_f32);
-        rc = upload(pk.data(), pk.size() * 4, &P.wpack_pair);
+        rc = upload_split(pk, kexp, &P.wpack_pair);
       }
     }
     if (rc == DAMVS_OK && P.kind == CONV_S1 && P.cout <= 8) {
@@ -504,7 +537,7 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
       } else {
         std::vector<float> pk;
         pack_layer_pair<float>(P, wf, E, pk, cvt_f32);
-        rc = upload(pk.data(), pk.size() * 4, &P.wpack_pair);
+        rc = upload_split(pk, kexp, &P.wpack_pair);
       }
     }
     if (rc == DAMVS_OK) rc = upload(shift.data(), shift.size() * 4, reinterpret_cast<void**>(&P.bias));
@@ -781,6 +814,7 @@ struct damvs_conv2d {
   damvs_conv2d_desc d;
   int dtype = 0, cout_pad = 0, cout_store = 0, MTtot = 0, nphase = 0, kchunk_k = 0;
   int xpair = 0;  // x-parity-pair phases (build_phases_2d_xpair / pack_2d_xpair)
+  float wscale = 1.f;  // fp32: 2^-k of the split-f16 weights (split_weights)
   Conv2dPhase ph[4];
   void* wpack = nullptr;
   float* wgeo = nullptr;
@@ -994,7 +1028,9 @@ int damvs_conv2d_create(const damvs_conv2d_desc* desc, const float* weight, cons
       std::vector<float> pk;
       if (L->xpair) pack_2d_xpair<float>(L, weight, pk, cvt_f32);
       else pack_2d<float>(L, weight, pk, cvt_f32);
-      rc = upload(pk.data(), pk.size() * 4, &L->wpack);
+      const int kexp = split_exponent(pk);
+      L->wscale = std::ldexp(1.f, -kexp);
+      rc = upload_split(pk, kexp, &L->wpack);
     }
   }
   if (rc == DAMVS_OK && d.ngeo > 0) {
@@ -1149,6 +1185,7 @@ int damvs_conv2d_forward(const damvs_conv2d* L, void* stream, int B, int Hi, int
   }
   if (res_post && (a.Ho % a.post_up || a.Wo % a.post_up)) return fail(DAMVS_E_SHAPE, "bad upsample shape");
   a.relu = d.relu;
+  a.wscale = L->wscale;
   a.nphase = L->nphase;
   a.xpair = L->xpair;
   a.div_wq = make_fastdiv(a.Wq);

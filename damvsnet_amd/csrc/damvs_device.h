@@ -14,6 +14,62 @@ typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 __device__ __forceinline__ float bf2f(uint32_t u16) { return __uint_as_float(u16 << 16); }
 __device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 
+// ---------------------------------------------------------------- fp32 convolutions as split-f16 MFMAs
+// The fp32 path stores fp32 and computes every conv product on f16 matrix cores: x = xh + xl with xh = f16(x) and
+// xl = f16(x - xh) (round to nearest even, subnormals kept; x - xh is exact), and
+//   w * x ~ wl*xh + wh*xl + wh*xh          (three v_mfma_f32_16x16x16_f16, fp32 accumulation)
+// leaving out only wl*xl (~2^-22 relative) and the pieces' own rounding (~2^-22): per product ~2^-21, inside the
+// fp32 FMA chain's accumulation error over the K of these layers. Measured against float64 (tools/mfma_f16,
+// profiles/r04/mfma_f16.json): max error / sum|w x| 2.7e-7 / 3.8e-7 / 5.7e-7 at K = 64 / 288 / 864 against the exact
+// fp32 MFMA's 2.4e-7 / 4.8e-7 / 7.7e-7; subnormal pieces pass through the MFMA exactly. The cascade-level model
+// (tools/split_precision_model.py: every conv of the oracle forward emulated this way) keeps the end-to-end
+// fp32-vs-fp64 statistics at 0.86-1.36x the reference's own. Rate: three 16-cycle MFMAs per 16 K instead of four
+// 32-cycle exact-fp32 ones (v_mfma_f32_16x16x16_f16 runs at half the FLOP rate of 16x16x32 but keeps the fp32
+// kernels' 4-channel K fragments). Weights are split on the host, scaled by 2^k per layer so the largest |w| lies in
+// (2^13, 2^14] (normal-range lo pieces); the epilogues multiply by wscale = 2^-k. A 16-byte fragment holds
+// [hi0..hi3 | lo0..lo3]. |x| must stay below 65504 (f16 range): larger activations turn into inf / NaN outputs.
+typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2v_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float4 split_f16(const float4& x) {
+  const f16x4_t h = {(_Float16)x.x, (_Float16)x.y, (_Float16)x.z, (_Float16)x.w};
+  const f16x4_t l = {(_Float16)(x.x - (float)h[0]), (_Float16)(x.y - (float)h[1]), (_Float16)(x.z - (float)h[2]),
+                     (_Float16)(x.w - (float)h[3])};
+  const f32x2v_t hv = __builtin_bit_cast(f32x2v_t, h), lv = __builtin_bit_cast(f32x2v_t, l);
+  return make_float4(hv[0], hv[1], lv[0], lv[1]);
+}
+// acc += A (pre-split weights w) * B (pre-split activations xs), one 16 x 16 x 16 K step
+__device__ __forceinline__ void mma_split16(const float4& w, const float4& xs, f32x4_t& acc) {
+  const f16x4_t wh = __builtin_bit_cast(f16x4_t, (f32x2v_t){w.x, w.y}), wl = __builtin_bit_cast(f16x4_t, (f32x2v_t){w.z, w.w});
+  const f16x4_t xh = __builtin_bit_cast(f16x4_t, (f32x2v_t){xs.x, xs.y}), xl = __builtin_bit_cast(f16x4_t, (f32x2v_t){xs.z, xs.w});
+  acc = __builtin_amdgcn_mfma_f32_16x16x16f16(wl, xh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x16f16(wh, xl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x16f16(wh, xh, acc, 0, 0, 0);
+}
+
+// MFMA K-fragment traits shared by the conv kernels. raw: one lane's 16-byte K fragment (A or B).
+//   mma(w, x, acc):     x as loaded from the activation tensor (fp32: split here, per use)
+//   stage(x):           the form an LDS tile keeps (fp32: split once when the tile is filled)
+//   mma_staged(w, s, acc): x from such a tile
+template <typename T> struct MmaFrag;
+template <> struct MmaFrag<float> {
+  typedef float4 raw;
+  __device__ __forceinline__ static raw stage(const raw& x) { return split_f16(x); }
+  __device__ __forceinline__ static void mma_staged(const raw& w, const raw& xs, f32x4_t& acc) { mma_split16(w, xs, acc); }
+  __device__ __forceinline__ static void mma(const raw& w, const raw& x, f32x4_t& acc) { mma_split16(w, split_f16(x), acc); }
+  __device__ __forceinline__ static raw zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+};
+template <> struct MmaFrag<bf16_t> {
+  typedef uint4 raw;
+  __device__ __forceinline__ static raw stage(const raw& x) { return x; }
+  __device__ __forceinline__ static void mma(const raw& w, const raw& x, f32x4_t& acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, w), __builtin_bit_cast(bf16x8_t, x),
+                                                  acc, 0, 0, 0);
+  }
+  __device__ __forceinline__ static void mma_staged(const raw& w, const raw& x, f32x4_t& acc) { mma(w, x, acc); }
+  __device__ __forceinline__ static raw zero() { return make_uint4(0u, 0u, 0u, 0u); }
+};
+
 // Storage traits: E = elements per 16-byte chunk.
 template <typename T> struct Stor;
 template <> struct Stor<float> {
@@ -168,8 +224,13 @@ template <> struct Vox8<float> {
 // load(c). Loads are issued BATCH at a time before their ds_writes, so each lane keeps BATCH HBM
 // reads in flight (a plain strided `lds[c] = load(c)` loop waits for every load before its write:
 // one read in flight per lane). Past-the-end chunks re-load chunk N - 1 and are not written.
-template <int N, int BATCH, typename Raw, typename F>
-__device__ __forceinline__ void stage_chunks(Raw* lds, F&& load) {
+// `post` maps a loaded chunk to the form the tile keeps (MmaFrag<T>::stage), applied at the ds_write so that the
+// batch's loads are all in flight first.
+struct StageIdentity {
+  template <typename Raw> __device__ __forceinline__ Raw operator()(const Raw& r) const { return r; }
+};
+template <int N, int BATCH, typename Raw, typename F, typename P = StageIdentity>
+__device__ __forceinline__ void stage_chunks(Raw* lds, F&& load, P post = P()) {
   constexpr int PER = (N + 255) / 256;
 #pragma unroll
   for (int i0 = 0; i0 < PER; i0 += BATCH) {
@@ -182,7 +243,7 @@ __device__ __forceinline__ void stage_chunks(Raw* lds, F&& load) {
 #pragma unroll
     for (int i = 0; i < BATCH; ++i) {
       const int c = threadIdx.x + (i0 + i) * 256;
-      if (i0 + i < PER && c < N) lds[c] = r[i];
+      if (i0 + i < PER && c < N) lds[c] = post(r[i]);
     }
   }
 }

@@ -85,6 +85,7 @@ struct ConvArgs {
   int relu;
   int nphase;
   int xpair;  // deconv phases are (pz, py) with both x parities in the MFMA rows (Cout <= 8)
+  float wscale;  // accumulator scale of the epilogue: 2^-k of the split-f16 fp32 weights (damvs_device.h), 1 for bf16
   FastDiv div_wq, div_hq, div_dq;  // set by launch_conv3d
   ConvPhase ph[kMaxPhases];
 };
@@ -118,6 +119,7 @@ struct Conv2dArgs {
   int B, Hi, Wi, Hq, Wq, Ho, Wo, in_stride, out_stride, relu, nphase;
   FastDiv div_wq, div_hq;   // output-grid decomposition q -> (b, qy, qx)
   int xpair;                // transposed stride 2, cout 8: both x parities in one phase's 16 MFMA rows
+  float wscale;             // accumulator scale of the epilogue (see ConvArgs)
   Conv2dPhase ph[4];
 };
 

@@ -17,25 +17,7 @@ namespace damvs {
 
 namespace {
 
-template <typename T> struct Frag2;
-template <> struct Frag2<float> {
-  typedef float4 raw;
-  __device__ __forceinline__ static void mma(const raw& w, const raw& x, f32x4_t& acc) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, x.w, acc, 0, 0, 0);
-  }
-  __device__ __forceinline__ static raw zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
-};
-template <> struct Frag2<bf16_t> {
-  typedef uint4 raw;
-  __device__ __forceinline__ static void mma(const raw& w, const raw& x, f32x4_t& acc) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, w), __builtin_bit_cast(bf16x8_t, x),
-                                                  acc, 0, 0, 0);
-  }
-  __device__ __forceinline__ static raw zero() { return make_uint4(0u, 0u, 0u, 0u); }
-};
+template <typename T> using Frag2 = MmaFrag<T>;
 
 template <typename T>
 __device__ __forceinline__ void ld4(const T* p, float* r);
@@ -280,8 +262,8 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
       float r[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        r[i] = acc[j][0][i] + b8[i];
-        r[4 + i] = __shfl_down(acc[j][0][i], 16) + b8[4 + i];
+        r[i] = fmaf(acc[j][0][i], a.wscale, b8[i]);
+        r[4 + i] = fmaf(__shfl_down(acc[j][0][i], 16), a.wscale, b8[4 + i]);
       }
       if (!lead) continue;
       const bool ok = valid[j];
@@ -318,7 +300,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
     for (int m = 0; m < MT; ++m) {
       float r[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) r[i] = acc[j][m][i] + bias[m][i];
+      for (int i = 0; i < 4; ++i) r[i] = fmaf(acc[j][m][i], a.wscale, bias[m][i]);
       if (a.res_pre) IO::addq(qpre[m], r);
       if (a.relu) {
 #pragma unroll
@@ -375,7 +357,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) != 2 ? 1 : CIN == 32 ? 
     const bool ok = (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
     const uint32_t off = (uint32_t)(((pin0 + iy * a.Wi + x0 - 1) * CH + col) * 16);
     return IO::frag(rin, ok ? off : kOOB);
-  });
+  }, [](const raw& r) { return Frag2<T>::stage(r); });
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -414,7 +396,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) != 2 ? 1 : CIN == 32 ? 
 #pragma unroll
     for (int j = 0; j < L2H; ++j)
 #pragma unroll
-      for (int m = 0; m < MT; ++m) Frag2<T>::mma(wa[m], xa[j], acc[j][m]);
+      for (int m = 0; m < MT; ++m) Frag2<T>::mma_staged(wa[m], xa[j], acc[j][m]);
     if (s + 1 < KCHUNKS) {
 #pragma unroll
       for (int j = 0; j < L2H; ++j) xa[j] = xb[j];
@@ -458,7 +440,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) != 2 ? 1 : CIN == 32 ? 
     for (int m = 0; m < MT; ++m) {
       float r[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) r[i] = acc[j][m][i] + bias[m][i];
+      for (int i = 0; i < 4; ++i) r[i] = fmaf(acc[j][m][i], a.wscale, bias[m][i]);
       if (a.res_pre) IO::addq(qpre[m], r);
       if (a.relu) {
 #pragma unroll
@@ -541,7 +523,7 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int i = threadIdx.x + k * 256;
-      if ((i >> 2) < HP) buf[bi * HP * 4 + i] = regs[k];
+      if ((i >> 2) < HP) buf[bi * HP * 4 + i] = Frag2<T>::stage(regs[k]);
     }
   };
 
@@ -579,7 +561,7 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
 #pragma unroll
       for (int j = 0; j < GW; ++j)
 #pragma unroll
-        for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf[j], acc[j][m]);
+        for (int m = 0; m < MT; ++m) Frag2<T>::mma_staged(wf[m], xf[j], acc[j][m]);
       if (t + 1 < nt) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) wf[m] = wn[m];
@@ -658,7 +640,7 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
     for (int m = 0; m < MT; ++m) {
       float r[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) r[i] = acc[j][m][i] + bias[m][i];
+      for (int i = 0; i < 4; ++i) r[i] = fmaf(acc[j][m][i], a.wscale, bias[m][i]);
       if (a.res_pre) IO::addq(qpre[m], r);
       if (a.relu) {
 #pragma unroll

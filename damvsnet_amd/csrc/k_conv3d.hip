@@ -25,25 +25,7 @@ namespace damvs {
 
 namespace {
 
-template <typename T> struct Frag;
-template <> struct Frag<float> {
-  typedef float4 raw;
-  __device__ __forceinline__ static void mma(const raw& w, const raw& x, f32x4_t& acc) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, x.w, acc, 0, 0, 0);
-  }
-  __device__ __forceinline__ static raw zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
-};
-template <> struct Frag<bf16_t> {
-  typedef uint4 raw;
-  __device__ __forceinline__ static void mma(const raw& w, const raw& x, f32x4_t& acc) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, w), __builtin_bit_cast(bf16x8_t, x),
-                                                  acc, 0, 0, 0);
-  }
-  __device__ __forceinline__ static raw zero() { return make_uint4(0u, 0u, 0u, 0u); }
-};
+template <typename T> using Frag = MmaFrag<T>;
 
 template <typename T>
 __device__ __forceinline__ void store4(T* p, const float* r);
@@ -92,7 +74,7 @@ __device__ __forceinline__ void finish4(const ConvArgs& a, __amdgpu_buffer_rsrc_
   float r[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    r[i] = acc[i] + bias[i];
+    r[i] = fmaf(acc[i], a.wscale, bias[i]);
     if (a.relu) r[i] = fmaxf(r[i], 0.f);
   }
   if (has_res) BufIO<T>::addq(q, r);
@@ -234,7 +216,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIP
       if (!lead) continue;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        r[i] += b8[i];
+        r[i] = fmaf(r[i], a.wscale, b8[i]);
         if (a.relu) r[i] = fmaxf(r[i], 0.f);
       }
       const uint32_t off = valid[j] ? (uint32_t)(pout[j] * 8) * ES : kOOB;
@@ -363,7 +345,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
     const bool ok = (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
     const uint32_t off = (uint32_t)(((vin0 + (iz * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16);
     return BufIO<T>::frag(rin, ok ? off : kOOB);
-  });
+  }, [](const raw& r) { return Frag<T>::stage(r); });
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -429,7 +411,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
 #pragma unroll
         for (int j = 0; j < kLdsGroups; ++j)
 #pragma unroll
-          for (int m = 0; m < MT; ++m) Frag<T>::mma(wa[m], xa[j], acc[j][m]);
+          for (int m = 0; m < MT; ++m) Frag<T>::mma_staged(wa[m], xa[j], acc[j][m]);
         if (more) {
 #pragma unroll
           for (int j = 0; j < kLdsGroups; ++j) xa[j] = xb[j];
@@ -444,7 +426,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
     for (int s = 0; s < KCHUNKS; ++s) {
       fetch(s, xa, wa);
 #pragma unroll
-      for (int j = 0; j < kLdsGroups; ++j) Frag<T>::mma(wa[0], xa[j], acc[j][0]);
+      for (int j = 0; j < kLdsGroups; ++j) Frag<T>::mma_staged(wa[0], xa[j], acc[j][0]);
     }
   } else {
     // software-pipelined one chunk ahead: chunk s+1's fragments are read while chunk s's MFMAs run
@@ -456,7 +438,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
 #pragma unroll
       for (int j = 0; j < kLdsGroups; ++j)
 #pragma unroll
-        for (int m = 0; m < MT; ++m) Frag<T>::mma(wa[m], xa[j], acc[j][m]);
+        for (int m = 0; m < MT; ++m) Frag<T>::mma_staged(wa[m], xa[j], acc[j][m]);
       if (s + 1 < KCHUNKS) {
         __builtin_amdgcn_sched_group_barrier(0x100, kLdsGroups, 0);       // DS reads
         __builtin_amdgcn_sched_group_barrier(0x008, kLdsGroups * MT, 0);  // MFMA
@@ -543,7 +525,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, 
     const bool ok = (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
     const uint32_t off = (uint32_t)(((vin0 + (iz * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16);
     return BufIO<T>::frag(rin, ok ? off : kOOB);
-  });
+  }, [](const raw& r) { return Frag<T>::stage(r); });
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -576,7 +558,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, 
     raw xb[NP], wb;
     if (s + 1 < KCHUNKS) fetch(s + 1, xb, wb);
 #pragma unroll
-    for (int j = 0; j < NP; ++j) Frag<T>::mma(wa, xa[j], acc[j]);
+    for (int j = 0; j < NP; ++j) Frag<T>::mma_staged(wa, xa[j], acc[j]);
     if (s + 1 < KCHUNKS) {
 #pragma unroll
       for (int j = 0; j < NP; ++j) xa[j] = xb[j];
