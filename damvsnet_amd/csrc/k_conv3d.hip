@@ -87,13 +87,9 @@ __device__ __forceinline__ void finish4(const ConvArgs& a, __amdgpu_buffer_rsrc_
 // voxel decomposition, range-checked buffer loads for the zero padding.
 // XP: x-parity-pair deconv phases (build_phases_xpair): MFMA row r = (x parity r >> 3, channel r & 7),
 // so lane group g stores channels (g & 1) * 4 .. +3 of output x = 2 qx + (g >> 1).
-// PIPE: chunk s + 1's weight fragments and input gathers are issued before chunk s's MFMAs (two register sets), so
-// each chunk waits only for loads that had a whole chunk of MFMAs to land (the deep-K mid-level layers: conv3 - conv7,
-// K = 27 x 16 .. 27 x 64).
-// KG: 16-voxel column groups per wave (kGroups = 4 by default; 1 for the small deep-K level-3 layers, whose grid
-// would otherwise leave most CUs idle).
-template <typename T, int MT, bool XP, bool PIPE = false, int KG = kGroups>
-__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIPE && KG == kGroups ? 3 : 1)) void conv3d_mfma_kernel(const ConvArgs a, int nqblk) {
+template <typename T, int MT, bool XP>
+__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1)) void conv3d_mfma_kernel(const ConvArgs a, int nqblk) {
+  constexpr int KG = kGroups;  // 16-voxel column groups per wave
   typedef BufIO<T> IO;
   typedef typename IO::raw raw;
   constexpr int E = Stor<T>::E;  // input channels per lane per K-chunk
@@ -178,24 +174,10 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !PIP
 #pragma unroll
       for (int m = 0; m < MT; ++m) Frag<T>::mma(wf[m], xf[j], acc[j][m]);
   };
-  if constexpr (PIPE) {
-    raw wa[MT], xa[KG], wb[MT], xb[KG];
-    const int nk = ph.kchunks;
-    load(0, wa, xa);
-    for (int s = 0; s < nk; s += 2) {
-      if (s + 1 < nk) load(s + 1, wb, xb);
-      mma(wa, xa);
-      if (s + 1 < nk) {
-        if (s + 2 < nk) load(s + 2, wa, xa);
-        mma(wb, xb);
-      }
-    }
-  } else {
-    for (int s = 0; s < ph.kchunks; ++s) {
-      raw wf[MT], xf[KG];
-      load(s, wf, xf);
-      mma(wf, xf);
-    }
+  for (int s = 0; s < ph.kchunks; ++s) {
+    raw wf[MT], xf[KG];
+    load(s, wf, xf);
+    mma(wf, xf);
   }
 
   if constexpr (XP && DAMVS_DIAG_SKIP_EPI == 0) {
@@ -1544,40 +1526,6 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
   if (a.xpair) {
     if (a.MT != 1 || a.Cout != 8) return hipErrorInvalidValue;
     hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, true>), grid, dim3(256), 0, s, a, nq);
-    return hipGetLastError();
-  }
-  // DAMVS_CONV3D_KG1 (A/B; 1: always, 2: grids below 1024 blocks, i.e. the level-3 convs conv5 / conv6): one 16-voxel
-  // group per wave, 4x the waves for the same MFMAs. Measured on conv5 / conv6: stage-1 U-Net 1.137 -> 1.125 ms but
-  // stage 3 1.867 -> 1.91 ms, 206.0 -> 205.2 maps/s (profiles/r03/ab_unet.jsonl); off by default
-  static const int kg1 = [] {
-    const char* v = getenv("DAMVS_CONV3D_KG1");
-    return v ? atoi(v) : 0;
-  }();
-  if (kg1 == 1 || (kg1 == 2 && (long long)nq * a.nphase < 1024)) {
-    const long long pb1 = 4LL * 16;
-    const int nq1 = (int)((Qtot + pb1 - 1) / pb1);
-    const dim3 grid1((unsigned)(nq1 * a.nphase));
-    switch (a.MT) {
-      case 1: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, false, false, 1>), grid1, dim3(256), 0, s, a, nq1); break;
-      case 2: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 2, false, false, 1>), grid1, dim3(256), 0, s, a, nq1); break;
-      case 4: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 4, false, false, 1>), grid1, dim3(256), 0, s, a, nq1); break;
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
-  // DAMVS_CONV3D_PIPE=1 (A/B): the gather kernel with one-chunk-ahead loads (measured flat in the pipeline:
-  // U-Net 1.185 / 2.218 / 2.020 against 1.187 / 2.227 / 2.023 ms per stage, at one wave per SIMD less)
-  static const bool pipe = [] {
-    const char* v = getenv("DAMVS_CONV3D_PIPE");
-    return v && v[0] == '1';
-  }();
-  if (pipe) {
-    switch (a.MT) {
-      case 1: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, false, true>), grid, dim3(256), 0, s, a, nq); break;
-      case 2: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 2, false, true>), grid, dim3(256), 0, s, a, nq); break;
-      case 4: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 4, false, true>), grid, dim3(256), 0, s, a, nq); break;
-      default: return hipErrorInvalidValue;
-    }
     return hipGetLastError();
   }
   switch (a.MT) {

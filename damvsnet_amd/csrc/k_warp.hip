@@ -602,271 +602,38 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
   }
 }
 
-// Corner-pair form (NHWC maps of CH = C * sizeof(T) / 16 = 1, 2 or 4 chunks per pixel): S = 2 CH lanes share one
-// voxel, lane q = 2 chunk + col loading chunk `chunk` of the left (col 0) or right (col 1) bilinear corner of the
-// top and the bottom row. The 2 CH lanes of a voxel read the two adjacent pixel records of a corner row -- 32 CH
-// contiguous bytes -- in ONE instruction, so a wave's gather instruction spans half as many source pixels as in
-// the channel-split form (consecutive voxels' corner pairs overlap: ~17 distinct source pixels per 16 voxels
-// instead of ~33 per 32) and 2 loads per lane per sample replace 4. Each lane forms its column's partial
-// (top w + bottom w) for the 8 / 4 channels of its chunk, keeps half of them (half = col) and trades the other half
-// with its col partner (DPP quad_perm 1,0,3,2), so every channel's bilinear sum is (left partial) + (right
-// partial) -- the reference's four corner products, summed in that grouping -- and each lane finishes E / 2
-// channels: its reference values, variance / adaptive terms and an 8-byte (bf16) store. The adaptive weight
-// net's channel dot product is summed over the S lanes (DPP xor 1, 2; ds_swizzle xor 4 for S = 8).
-__device__ __forceinline__ float swz_xor4(float v) {
-  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x101F));  // and 0x1F, xor 4
-}
-
-template <typename T, int C, int MODE, int NVC>
-__global__ __launch_bounds__(256) void warp_pair_kernel(const WarpArgs a, const float* __restrict__ cams,
-                                                        int npix_blocks, int dchunk, int ndchunks) {
-  constexpr int E = Stor<T>::E;  // channels per 16-byte chunk
-  constexpr int CH = C / E;      // chunks per pixel
-  constexpr int S = 2 * CH;      // lanes per voxel
-  constexpr int H = E / 2;       // channels finished per lane
-  constexpr int PPB = 256 / S;   // voxels (pixels) per block
-  static_assert(CH == 1 || CH == 2 || CH == 4, "corner-pair form: 1, 2 or 4 chunks per pixel");
-  static_assert(NVC % 2 == 0 || NVC < 0, "the view pipeline alternates two register sets");
-  const int hw = a.h * a.w;
-  const int bid = blockIdx.x;
-  auto xcd_remap = [](int i, int n) {
-    const int q8 = n / 8, r8 = n % 8, x = i % 8;
-    return (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + i / 8;
-  };
-  int L = xcd_remap(bid, npix_blocks * ndchunks * a.B);
-  const int dc = L % ndchunks; L /= ndchunks;
-  const int pb = L % npix_blocks;
-  const int b = L / npix_blocks;
-  const float* __restrict__ cam = cams + (size_t)b * (a.N - 1) * 12;
-  const int q = threadIdx.x & (S - 1);
-  const int col = q & 1, chunk = q >> 1;
-  const int p = warp_pixel(a, pb, (int)(threadIdx.x / S), PPB);  // the S lanes of a pixel are consecutive: they exit together
-  if (p < 0) return;
-  const int yl = p / a.w, x = p - yl * a.w;
-  const int y = a.y0 + yl, pg = y * a.w + x;
-  const float fx = (float)x, fy = (float)y;
-  const float kx = (float)a.w / (float)(a.w - 1), ky = (float)a.h / (float)(a.h - 1);
-  constexpr uint32_t rec = C * sizeof(T);
-  const uint32_t bbytes = (uint32_t)hw * rec;
-  const uint32_t sb = (uint32_t)b * bbytes;
-  const uint32_t qoff = (uint32_t)chunk * 16u;
-  const long long fbytes = (long long)a.B * bbytes;
-  const int c0 = chunk * E + col * H;  // first channel this lane finishes
-
-  float ref[H];
-  if (MODE != AGG_WARP_ONLY) {
-    const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.feats[0], fbytes);
-    const uint2 rr = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r0, (uint32_t)pg * rec + c0 * (uint32_t)sizeof(T), sb, 0));
-    if constexpr (sizeof(T) == 2) {
-      ref[0] = __uint_as_float(rr.x << 16); ref[1] = __uint_as_float(rr.x & 0xffff0000u);
-      ref[2] = __uint_as_float(rr.y << 16); ref[3] = __uint_as_float(rr.y & 0xffff0000u);
-    } else {
-      ref[0] = __uint_as_float(rr.x); ref[1] = __uint_as_float(rr.y);
-    }
-  }
-  float kq[H];  // this lane's channels of the weight net's first 1x1 conv (selects, no dynamic kernarg indexing)
-#pragma unroll
-  for (int e = 0; e < H; ++e) {
-    float k = a.k1[e];
-#pragma unroll
-    for (int j = 1; j < S; ++j) k = q == j ? a.k1[(j >> 1) * E + (j & 1) * H + e] : k;
-    kq[e] = k;
-  }
-  const float inv_n = 1.f / (float)a.N, inv_n1 = 1.f / (float)(a.N - 1);
-  const int d0 = dc * dchunk, d1 = min(a.D, d0 + dchunk);
-  auto vox_of = [&](int d) { return (((size_t)b * a.D + d) * a.out_rows + a.out_y) * a.w + p; };
-
-  // rv[0] / rv[1]: this lane's chunk of its column's top / bottom corner; wt: their weights
-  auto reduce = [&](const uint4* rv, const float* wt, float* acc, float* sq) {
-    float v0[E], v1[E];
-    Rec16<T>::unpack(rv[0], v0);
-    Rec16<T>::unpack(rv[1], v1);
-    float part[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) part[e] = v0[e] * wt[0] + v1[e] * wt[1];
-    float s[H];
-#pragma unroll
-    for (int e = 0; e < H; ++e) {
-      const float keep = col ? part[H + e] : part[e];
-      const float send = col ? part[e] : part[H + e];
-      s[e] = keep + dpp_xor1(send);  // (left partial) + (right partial) in both lanes of the pair
-    }
-    if (MODE == AGG_WARP_ONLY) {
-#pragma unroll
-      for (int e = 0; e < H; ++e) acc[e] = s[e];
-    } else if (MODE == AGG_VARIANCE) {
-#pragma unroll
-      for (int e = 0; e < H; ++e) { acc[e] += s[e]; sq[e] += s[e] * s[e]; }
-    } else {
-      float dot = 0.f;
-#pragma unroll
-      for (int e = 0; e < H; ++e) {
-        const float df = ref[e] - s[e];
-        sq[e] = df * df;
-        dot += kq[e] * sq[e];
-      }
-      dot += dpp_xor1(dot);
-      if (S >= 4) dot += dpp_xor2(dot);
-      if (S >= 8) dot += swz_xor4(dot);
-      const float a1 = fmaxf(dot * a.s1 + a.t1, 0.f);
-      const float wv = fmaxf(a1 * a.s2 + a.t2, 0.f) + 1.f;
-#pragma unroll
-      for (int e = 0; e < H; ++e) acc[e] += wv * sq[e];
-    }
-  };
-  auto finish = [&](int d, float* acc, float* sq) {
-    float o[H];
-#pragma unroll
-    for (int e = 0; e < H; ++e) {
-      if (MODE == AGG_VARIANCE) {
-        const float mean = acc[e] * inv_n;
-        o[e] = sq[e] * inv_n - mean * mean;
-      } else if (MODE == AGG_ADAPTIVE) {
-        o[e] = acc[e] * inv_n1;
-      } else {
-        o[e] = acc[e];
-      }
-    }
-    T* dst = reinterpret_cast<T*>(a.out) + vox_of(d) * C + c0;
-    if constexpr (sizeof(T) == 2)
-      *reinterpret_cast<uint2*>(dst) = make_uint2((uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16),
-                                                  (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16));
-    else
-      *reinterpret_cast<float2*>(dst) = make_float2(o[0], o[1]);
-  };
-  auto init = [&](float* acc, float* sq) {
-#pragma unroll
-    for (int e = 0; e < H; ++e) {
-      acc[e] = (MODE == AGG_VARIANCE) ? ref[e] : 0.f;
-      sq[e] = (MODE == AGG_VARIANCE) ? ref[e] * ref[e] : 0.f;
-    }
-  };
-
-  constexpr int NH = NVC > 0 ? NVC : 1;
-  const int nv = NVC > 0 ? NVC : a.N - 1;
-  float rx[NH], ry[NH], rz[NH], tx[NH], ty[NH], tz[NH];
-  __amdgpu_buffer_rsrc_t rs[NH];
-  if constexpr (NVC > 0) {
-#pragma unroll
-    for (int v = 0; v < NVC; ++v) {
-      const float* m = cam + v * 12;
-      rx[v] = m[0] * fx + m[1] * fy + m[2];
-      ry[v] = m[3] * fx + m[4] * fy + m[5];
-      rz[v] = m[6] * fx + m[7] * fy + m[8];
-      tx[v] = m[9];
-      ty[v] = m[10];
-      tz[v] = m[11];
-      rs[v] = make_rsrc(a.feats[v + 1], fbytes);
-    }
-  }
-  auto taps = [&](int v, float hyp) {
-    float qx, qy, qz;
-    if constexpr (NVC > 0) {
-      qx = rx[v] * hyp + tx[v], qy = ry[v] * hyp + ty[v], qz = rz[v] * hyp + tz[v];
-    } else {
-      const float* m = cam + v * 12;
-      const float vx = m[0] * fx + m[1] * fy + m[2];
-      const float vy = m[3] * fx + m[4] * fy + m[5];
-      const float vz = m[6] * fx + m[7] * fy + m[8];
-      qx = vx * hyp + m[9], qy = vy * hyp + m[10], qz = vz * hyp + m[11];
-    }
-    const float iz = __builtin_amdgcn_rcpf(qz);
-    return bilinear_taps(a.h, a.w, rec, qx * iz * kx - 0.5f, qy * iz * ky - 0.5f);
-  };
-  auto issue = [&](int v, const Taps& t, uint4* rv, float* wt) {
-    __amdgpu_buffer_rsrc_t r;
-    if constexpr (NVC > 0) r = rs[v];
-    else r = make_rsrc(a.feats[v + 1], fbytes);
-    const uint32_t ot = col ? t.off[1] : t.off[0], ob = col ? t.off[3] : t.off[2];
-    rv[0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, ot + qoff, sb, 0));
-    rv[1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, ob + qoff, sb, 0));
-    wt[0] = col ? t.wt[1] : t.wt[0];
-    wt[1] = col ? t.wt[3] : t.wt[2];
-  };
-  uint4 ra[2], rb[2];
-  float wa[2], wb[2];
-  float hyp = a.hyps[vox_of(d0)];
-  float hyp_n = a.hyps[vox_of(min(d0 + 1, d1 - 1))];
-  issue(0, taps(0, hyp), ra, wa);
-  for (int d = d0; d < d1; ++d) {
-    const float hyp_nn = a.hyps[vox_of(min(d + 2, d1 - 1))];
-    float acc[H], sq[H];
-    init(acc, sq);
-    auto step = [&](int v, const uint4* cur, const float* wcur, uint4* nxt, float* wnxt) {
-      if (v + 1 < nv) issue(v + 1, taps(v + 1, hyp), nxt, wnxt);
-      else issue(0, taps(0, hyp_n), nxt, wnxt);
-      reduce(cur, wcur, acc, sq);
-    };
-    if constexpr (NVC > 0) {
-#pragma unroll
-      for (int v = 0; v < NVC; v += 2) {
-        step(v, ra, wa, rb, wb);
-        step(v + 1, rb, wb, ra, wa);
-      }
-    } else {
-#pragma unroll 1
-      for (int v = 0; v < nv; v += 2) {
-        step(v, ra, wa, rb, wb);
-        step(v + 1, rb, wb, ra, wa);
-      }
-    }
-    hyp = hyp_n;
-    hyp_n = hyp_nn;
-    finish(d, acc, sq);
-  }
-}
-
-// Lanes per voxel of the corner-pair kernel for C-channel NHWC maps of 1, 2 or 4 16-byte chunks per pixel (0: not
-// taken). DAMVS_WARP_PAIR=1 enables it (A/B; read once per process).
-template <typename T, int C, bool BLK>
-int pair_lanes(const WarpArgs& a) {
-  static const bool on = [] {
-    const char* v = getenv("DAMVS_WARP_PAIR");
-    return v && v[0] == '1';
+// Lanes per voxel the launcher uses for C-channel maps: the channel-split kernel for NHWC maps of 2 or 4 16-byte chunks
+// per pixel when the view pipeline takes the view count (odd N >= 3), else 1 (the one-lane kernel).
+// DAMVS_WARP_SPLIT=0 (one lane per voxel everywhere) and DAMVS_WARP_NO_PIPE=1 (no view pipeline) both give 1, so the
+// launcher's block geometry and launch_k's kernel choice follow one predicate.
+bool warp_no_pipe() {
+  static const bool v = [] {
+    const char* e = getenv("DAMVS_WARP_NO_PIPE");
+    return e && e[0] == '1';
   }();
-  constexpr int CH = C * (int)sizeof(T) / 16;
-  if (BLK || !on || C * (int)sizeof(T) % 16 || (CH != 1 && CH != 2 && CH != 4)) return 0;
-  const bool pipe_ok = a.N >= 3 && (a.N - 1) % 2 == 0;
-  return pipe_ok ? 2 * CH : 0;
+  return v;
 }
-
-// Lanes per voxel the launcher uses for C-channel maps: the corner-pair kernel when it takes the maps, else the
-// channel-split kernel for NHWC maps of 2 or 4 16-byte chunks per pixel (DAMVS_WARP_SPLIT=0: always one lane per
-// voxel), 1 otherwise.
 template <typename T, int C, bool BLK>
 int split_lanes(const WarpArgs& a) {
   static const bool off = [] {
     const char* v = getenv("DAMVS_WARP_SPLIT");
     return v && v[0] == '0';
   }();
-  if (const int pl = pair_lanes<T, C, BLK>(a)) return pl;
   constexpr int S = C * (int)sizeof(T) / 16;
-  if (BLK || off || (S != 2 && S != 4)) return 1;
+  if (BLK || off || warp_no_pipe() || (S != 2 && S != 4)) return 1;
   const bool pipe_ok = a.N >= 3 && (a.N - 1) % 2 == 0;
   return pipe_ok ? S : 1;
 }
 
 template <typename T, int C, int MODE, bool BLK>
 void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, int ndc) {
-  static const bool no_pipe = [] {
-    const char* v = getenv("DAMVS_WARP_NO_PIPE");
-    return v && v[0] == '1';
-  }();
+  const bool no_pipe = warp_no_pipe();
   static const bool runtime_views = [] {  // DAMVS_WARP_RUNTIME_VIEWS=1: the runtime view loop for N = 5 too
     const char* v = getenv("DAMVS_WARP_RUNTIME_VIEWS");
     return v && v[0] == '1';
   }();
-  if constexpr (!BLK && (C * sizeof(T) == 16 || C * sizeof(T) == 32 || C * sizeof(T) == 64)) {
-    if (pair_lanes<T, C, BLK>(a) > 0 && !no_pipe) {
-      if (a.N == 5 && !runtime_views)
-        hipLaunchKernelGGL((warp_pair_kernel<T, C, MODE, 4>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
-      else
-        hipLaunchKernelGGL((warp_pair_kernel<T, C, MODE, -1>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
-      return;
-    }
-  }
   if constexpr (!BLK && (C * sizeof(T) == 32 || C * sizeof(T) == 64)) {
-    if (split_lanes<T, C, BLK>(a) > 1 && !no_pipe) {
+    if (split_lanes<T, C, BLK>(a) > 1) {
       // DAMVS_WARP_LDS_PAD (A/B): unused dynamic LDS per block, capping the blocks per CU (fewer pixels in flight
       // per XCD, a smaller L2 working set)
       static const size_t pad = [] {

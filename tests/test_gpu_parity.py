@@ -125,6 +125,65 @@ def test_warp_aggregate_vs_oracle(mode, C, N):
     assert rel_max(np_(vol.permute(0, 4, 1, 2, 3)), ref.numpy()) < 5e-5
 
 
+@pytest.mark.parametrize("mode", ["adaptive", "variance"])
+@pytest.mark.parametrize("C", [16, 32])
+@pytest.mark.parametrize("N", [3, 5, 7, 11])
+def test_warp_split_bf16_vs_oracle(N, C, mode):
+    """The bf16 benchmark warp (warp_split_kernel: NHWC maps of 32 / 64 bytes per pixel, 2 / 4 lanes per voxel, the
+    view pipeline for odd N; stages 1-2 of cfgC/D/E) against the oracle's aggregation (models/cas_mvsnet.py:42-87)
+    on the same bf16-rounded features, at the bf16 homo_warping gate (5e-3 relative max, test_homo_warping_vs_oracle):
+    the kernel accumulates in fp32 and rounds each output voxel once to bf16 (2^-9)."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine
+    s = {32: 0, 16: 1}[C]
+    net = CascadeMVSNet(ndepths=[48, 32, 8], agg_mode=mode)
+    sd = model_state("depthnet_cfgA_" + mode)
+    net.load_state_dict(sd, strict=True)
+    B, H, W, D = 2, 32, 48, 8
+    feats, P, hyps = depthnet_inputs(B=B, N=N, H=H, W=W, D=D, stage_idx=s, C=C)
+    feats = [f.to(torch.bfloat16).float() for f in feats]
+    ref = O.aggregate(feats, P, hyps, sd, s, mode, warp_impl="gather")
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s] if mode == "adaptive" else None, mode,
+                      torch.bfloat16, torch.device(DEV))
+    vol = eng.warp_aggregate([cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats], cuda(P),
+                             cuda(hyps))
+    err = rel_max(np_(vol.permute(0, 4, 1, 2, 3)), ref.numpy())
+    print("warp split bf16 N=%d C=%d %s: rel_max %.3e" % (N, C, mode, err))
+    assert err < 5e-3
+
+
+@pytest.mark.parametrize("D,h,w", [(48, 24, 40), (32, 32, 72), (64, 16, 40), (8, 24, 104)])
+@pytest.mark.parametrize("with_init", [False, True])
+def test_prob_mfma_vs_oracle(D, h, w, with_init):
+    """prob_mfma_kernel (the bf16 default: the prob conv on MFMA, fp32 weights as two bf16 terms, fused softmax /
+    depth / confidence / exp-variance) on a given bf16 U-Net output against the oracle's prob conv + regression
+    (models/module.py:541, models/cas_mvsnet.py:105-124) in fp32 on the same voxels. w = 40 / 72 / 104 leave ragged
+    32-pixel tiles; with_init adds a prob_volume_init to the logits."""
+    import torch.nn.functional as F
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    cr = net.cost_regularization[1]
+    eng = StageEngine(cr, net.DepthNet.weight_net[1], "adaptive", torch.bfloat16, torch.device(DEV))
+    g = torch.Generator().manual_seed(D + w)
+    B = 2
+    c0 = (torch.rand(B, D, h, w, 8, generator=g) * 2).to(torch.bfloat16)
+    hyps = torch.sort(torch.rand(B, D, h, w, generator=g) * 300 + 450, dim=1).values
+    init = torch.randn(B, D, h, w, generator=g) if with_init else None
+    logits = F.conv3d(c0.float().permute(0, 4, 1, 2, 3), cr.prob.weight.detach().float(), padding=1)[:, 0]
+    ref = O.regression(logits, hyps, init)
+    depth, conf, var, prob = eng.regress_c0(cuda(c0), cuda(hyps), prob_init=None if init is None else cuda(init))
+    pr = pixel_rel(np_(depth), ref["depth"].numpy())
+    perr = float(np.abs(np_(prob) - ref["prob_volume"].numpy()).max())
+    verr = rel_max(np_(var), ref["variance"].numpy())
+    print("prob_mfma vs oracle D=%d w=%d: depth max %.2e, prob abs %.2e, var rel %.2e" % (D, w, pr.max(), perr, verr))
+    assert pr.max() < 1e-5 and perr < 1e-4 and verr < 1e-4
+    m = conf_mask_pair(np_(prob), ref["prob_volume"].numpy())
+    assert m.mean() > 0.99
+    assert np.abs(np_(conf) - ref["photometric_confidence"].numpy())[m].max() < 1e-4
+
+
 @pytest.mark.parametrize("C,dtype", [(32, torch.bfloat16), (16, torch.bfloat16), (16, torch.float32),
                                      (8, torch.float32)])
 def test_warp_aggregate_channel_blocked_layout(C, dtype):

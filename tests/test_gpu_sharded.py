@@ -60,6 +60,26 @@ def test_sharded_stage_bitwise(s, D, B, H, W, P, dtype, warp):
             assert torch.equal(o[k], ref[k]), (r, k, (o[k] - ref[k]).abs().max().item())
 
 
+@pytest.mark.parametrize("warp", ["depth", "gather"])
+@pytest.mark.parametrize("s,D,H,W", [(0, 64, 296, 400), (1, 32, 592, 800), (2, 8, 1184, 1600)])
+def test_sharded_stage_cfgD_8way_bitwise(s, D, H, W, warp):
+    """BASELINE.json configs[3] (cfgD: DTU 1600x1184, 7 views, 64/32/8, bf16) at every stage's real size over 8
+    emulated ranks, as bench.py --gpus 8 runs it: the H-slab mode ("depth": D-sharded warp -> all-to-all -> per-layer
+    haloed U-Net -> row all-gather) and north_star's literal volume all-gather ("gather"), bitwise the unsharded
+    stage on every rank."""
+    from damvsnet_amd.sharded import ThreadGroup, DepthShardedDepthNet
+    net, nhwc, proj, hyps = _stage_case(s, D, 1, H, W, torch.bfloat16, N=7)
+    cr = net.cost_regularization[s]
+    with torch.no_grad():
+        ref = net.DepthNet.forward_nhwc(s, nhwc, proj, hyps, cr)
+        outs = ThreadGroup(8).run(lambda comm: DepthShardedDepthNet(net, comm, warp=warp)(s, nhwc, proj, hyps, cr))
+    torch.cuda.synchronize()
+    assert len(outs) == 8
+    for r, o in enumerate(outs):
+        for k in ("depth", "photometric_confidence", "variance", "prob_volume"):
+            assert torch.equal(o[k], ref[k]), (r, k, (o[k] - ref[k]).abs().max().item())
+
+
 def test_sharded_cascade_bitwise():
     """The whole cascade (160x128, 5 views, 48/32/8, bf16) with every stage's DepthNet over 4 emulated ranks
     (stage-1 slabs of 8 rows) equals the single-GPU forward bitwise at every stage."""
