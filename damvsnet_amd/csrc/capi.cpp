@@ -60,6 +60,7 @@ struct LayerPlan {
   ConvPhase ph_pair[4];
   float* bias = nullptr;
   float wscale = 1.f;  // fp32: 2^-k of the split-f16 weights (split_weights)
+  void* wpack32 = nullptr;  // fp32: the z-streamed kernel's 32-K split packing (ConvArgs::wpack32)
 };
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -249,6 +250,21 @@ std::vector<uint16_t> split_weights(const std::vector<float>& pk, int k) {
     }
   return out;
 }
+// 32-K packing (8 values per lane and chunk, pack_2d at kchunk_k 32) -> per (chunk, cout tile): [hi: 64 lanes x 8 f16]
+// [lo: 64 lanes x 8 f16] of w * 2^k (conv2d_wide_kernel<float>, WideForm<float>)
+std::vector<uint16_t> split_weights_blocked(const std::vector<float>& pk, int k) {
+  std::vector<uint16_t> out(pk.size() * 2);
+  for (size_t blk = 0; blk < pk.size() / 512; ++blk)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int e = 0; e < 8; ++e) {
+        const float v = std::ldexp(pk[blk * 512 + lane * 8 + e], k);
+        const _Float16 hi = (_Float16)v;
+        const _Float16 lo = (_Float16)(v - (float)hi);
+        std::memcpy(&out[blk * 1024 + lane * 8 + e], &hi, 2);
+        std::memcpy(&out[blk * 1024 + 512 + lane * 8 + e], &lo, 2);
+      }
+  return out;
+}
 int upload_split(const std::vector<float>& pk, int k, void** dev) {
   const std::vector<uint16_t> h = split_weights(pk, k);
   return upload(h.data(), h.size() * 2, dev);
@@ -355,6 +371,7 @@ ConvArgs conv_args(const damvs_stage* st, int li, int B, const Shapes& S, int li
   a.resid = resid;
   a.wpack = P.wpack;
   a.wpack_pair = P.wpack_pair;
+  a.wpack32 = P.wpack32;
   a.bias = P.bias;
   a.B = B;
   a.Cin = P.cin;
@@ -527,6 +544,14 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
         std::vector<float> pk;
         pack_layer_xpair<float>(P, wf, E, pk, cvt_f32);
         rc = upload_split(pk, kexp, &P.wpack_pair);
+        if (rc == DAMVS_OK && P.cin == 16 && P.cout == 8) {  // conv11's z-streamed kernel (deconv_xpair_zslide<float>)
+          LayerPlan P32 = P;
+          build_phases_xpair(P32, 32);
+          std::vector<float> p32;
+          pack_layer_xpair<float>(P32, wf, 8, p32, cvt_f32);
+          const std::vector<uint16_t> h = split_weights_blocked(p32, kexp);
+          rc = upload(h.data(), h.size() * 2, &P.wpack32);
+        }
       }
     }
     if (rc == DAMVS_OK && P.kind == CONV_S1 && P.cout <= 8) {
@@ -601,6 +626,7 @@ int damvs_stage_destroy(damvs_stage* st) {
   for (auto& P : st->L) {
     if (P.wpack) (void)hipFree(P.wpack);
     if (P.wpack_pair) (void)hipFree(P.wpack_pair);
+    if (P.wpack32) (void)hipFree(P.wpack32);
     if (P.bias) (void)hipFree(P.bias);
   }
   if (st->prob_w) (void)hipFree(st->prob_w);
@@ -817,6 +843,8 @@ struct damvs_conv2d {
   float wscale = 1.f;  // fp32: 2^-k of the split-f16 weights (split_weights)
   Conv2dPhase ph[4];
   void* wpack = nullptr;
+  Conv2dPhase ph32[4];      // fp32 layers the wide kernel may take: phases and [hi8 | lo8] weights at 32 K per chunk
+  void* wpack32 = nullptr;
   float* wgeo = nullptr;
   float* bias = nullptr;
 };
@@ -973,6 +1001,11 @@ void pack_2d_xpair(const damvs_conv2d* L, const float* W, std::vector<S>& out, S
   }
 }
 
+bool conv2d_wide32_disabled() {  // DAMVS_CONV2D_WIDE32=0: fp32 wide layers on the 16-K generic kernels (A/B)
+  const char* v = getenv("DAMVS_CONV2D_WIDE32");
+  return v && v[0] == '0';
+}
+
 bool conv2d_xpair_disabled() {
   const char* v = getenv("DAMVS_CONV2D_XPAIR");
   return v && v[0] == '0';
@@ -1031,6 +1064,22 @@ int damvs_conv2d_create(const damvs_conv2d_desc* desc, const float* weight, cons
       const int kexp = split_exponent(pk);
       L->wscale = std::ldexp(1.f, -kexp);
       rc = upload_split(pk, kexp, &L->wpack);
+      // the wide kernel's form (conv2d_wide_kernel<float>): phases and weights at 32 K per chunk
+      const int ctot = d.c0 + d.c1;
+      if (rc == DAMVS_OK && !L->xpair && d.c0 % 32 == 0 && d.c1 % 32 == 0 && ctot >= 64 && d.cout % 32 == 0 &&
+          d.ngeo <= 1) {
+        damvs_conv2d T32 = *L;
+        T32.wpack = nullptr;
+        T32.kchunk_k = 32;
+        rc = build_phases_2d(&T32);
+        if (rc == DAMVS_OK) {
+          std::vector<float> p32;
+          pack_2d<float>(&T32, weight, p32, cvt_f32);
+          const std::vector<uint16_t> h = split_weights_blocked(p32, kexp);
+          rc = upload(h.data(), h.size() * 2, &L->wpack32);
+          std::memcpy(L->ph32, T32.ph, sizeof(L->ph32));
+        }
+      }
     }
   }
   if (rc == DAMVS_OK && d.ngeo > 0) {
@@ -1121,6 +1170,7 @@ int damvs_fusion_view(void* stream, int H, int W, int nsrc, const float* depth_r
 int damvs_conv2d_destroy(damvs_conv2d* L) {
   if (!L) return DAMVS_OK;
   if (L->wpack) (void)hipFree(L->wpack);
+  if (L->wpack32) (void)hipFree(L->wpack32);
   if (L->wgeo) (void)hipFree(L->wgeo);
   if (L->bias) (void)hipFree(L->bias);
   delete L;
@@ -1191,6 +1241,14 @@ int damvs_conv2d_forward(const damvs_conv2d* L, void* stream, int B, int Hi, int
   a.div_wq = make_fastdiv(a.Wq);
   a.div_hq = make_fastdiv(a.Hq);
   std::memcpy(a.ph, L->ph, sizeof(a.ph));
+  if (L->wpack32) {  // fp32: the wide kernel on the 32-K split packing when it takes the shape
+    Conv2dArgs a32 = a;
+    std::memcpy(a32.ph, L->ph32, sizeof(a32.ph));
+    a32.wpack = L->wpack32;
+    a32.wide32 = 1;
+    if (conv2d_wide_shape_ok(a32) && !conv2d_wide32_disabled())
+      return hip_check(launch_conv2d(reinterpret_cast<hipStream_t>(stream), L->dtype, a32), "conv2d launch");
+  }
   return hip_check(launch_conv2d(reinterpret_cast<hipStream_t>(stream), L->dtype, a), "conv2d launch");
 }
 

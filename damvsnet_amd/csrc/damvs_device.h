@@ -47,6 +47,32 @@ __device__ __forceinline__ void mma_split16(const float4& w, const float4& xs, f
   acc = __builtin_amdgcn_mfma_f32_16x16x16f16(wh, xh, acc, 0, 0, 0);
 }
 
+// The same split on the full-rate v_mfma_f32_16x16x32_f16 (8 channels per lane and K fragment, the bf16 kernels'
+// fragment shape): hi and lo halves of 8 values, 16 bytes each. Kernels that keep their fragments in LDS or
+// registers for many MFMAs (conv2d_wide_kernel<float>) use this form; the weights are packed as [hi8 | lo8].
+struct F16Pair {
+  uint4 h, l;
+};
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ F16Pair split8(const float* v) {
+  f16x8_t h, l;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    h[i] = (_Float16)v[i];
+    l[i] = (_Float16)(v[i] - (float)h[i]);
+  }
+  return F16Pair{__builtin_bit_cast(uint4, h), __builtin_bit_cast(uint4, l)};
+}
+__device__ __forceinline__ F16Pair split8(const float4& a, const float4& b) {
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  return split8(v);
+}
+__device__ __forceinline__ void mma_split32(const F16Pair& w, const F16Pair& x, f32x4_t& acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, w.l), __builtin_bit_cast(f16x8_t, x.h), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, w.h), __builtin_bit_cast(f16x8_t, x.l), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, w.h), __builtin_bit_cast(f16x8_t, x.h), acc, 0, 0, 0);
+}
+
 // MFMA K-fragment traits shared by the conv kernels. raw: one lane's 16-byte K fragment (A or B).
 //   mma(w, x, acc):     x as loaded from the activation tensor (fp32: split here, per use)
 //   stage(x):           the form an LDS tile keeps (fp32: split once when the tile is filled)

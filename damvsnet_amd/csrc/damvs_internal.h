@@ -76,6 +76,8 @@ struct ConvArgs {
   const void* resid;   // added after ReLU (may alias out); nullptr if none
   const void* wpack;   // packed A fragments, see pack_conv_weights()
   const void* wpack_pair;  // row-pair packing (stride-1, Cout <= 8), nullptr if none
+  const void* wpack32;     // fp32: the z-streamed kernel's packing of this layer, 32 K per chunk, split-f16
+                           // [chunk][hi: 64 lanes][lo: 64 lanes] (x-pair for conv11, row pairs for conv0), or nullptr
   const float* bias;   // [Cout] (folded BN shift)
   int B, Cin, Cout, MT;
   int Di, Hi, Wi;
@@ -120,6 +122,7 @@ struct Conv2dArgs {
   FastDiv div_wq, div_hq;   // output-grid decomposition q -> (b, qy, qx)
   int xpair;                // transposed stride 2, cout 8: both x parities in one phase's 16 MFMA rows
   float wscale;             // accumulator scale of the epilogue (see ConvArgs)
+  int wide32;               // fp32: ph / wpack are the 32-K split packing of conv2d_wide_kernel<float>
   Conv2dPhase ph[4];
 };
 
@@ -139,6 +142,7 @@ hipError_t launch_block_channels(hipStream_t s, int store, const FeatPtrs& src, 
                                  int hw, int C);
 hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a);
 hipError_t launch_conv2d(hipStream_t s, int store, const Conv2dArgs& a);
+bool conv2d_wide_shape_ok(const Conv2dArgs& a);  // the wide kernel takes the layer (given 32-K phase data)
 struct BorderArgs {
   float corr[9 * 16];  // [tap][channel] of a 3x3 conv, channels < 16
 };

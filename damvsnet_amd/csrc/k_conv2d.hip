@@ -766,28 +766,48 @@ struct WideHalo {
   }
 };
 
+// Storage forms of the wide kernel. bf16: a K fragment is 8 bf16 channels (one 16-byte slot), 4 slots per halo pixel
+// and slice, chunk slot s at s ^ ((p >> 2) & 3). fp32 (T = float): every product on split-f16 MFMAs (damvs_device.h,
+// mma_split32): a fragment is the hi and lo halves of 8 channels (two slots), 8 slots per halo pixel and slice (hi of
+// chunk s in slot s, lo in slot 4 + s), slot position q at q ^ ((p >> 1) & 7): the 16 lanes of an N-group (16
+// consecutive pixels, 128 bytes apart) then read 16 distinct 16-byte bank groups. The A chunk of a cout tile is
+// [hi: 64 lanes x 16 B][lo: 64 lanes x 16 B] (pack_2d at 32 K per chunk, split_weights_blocked).
+template <typename T> struct WideForm;
+template <> struct WideForm<bf16_t> {
+  static constexpr int PL = 1, SLOTS = 4;  // 16-byte pieces per 8-channel fragment; LDS slots per pixel
+  __device__ __forceinline__ static int slot(int p, int q) { return q ^ ((p >> 2) & 3); }
+};
+template <> struct WideForm<float> {
+  static constexpr int PL = 2, SLOTS = 8;
+  __device__ __forceinline__ static int slot(int p, int q) { return q ^ ((p >> 1) & 7); }
+};
+
 // WM = 2: a block owns 128 output channels x a 2 x 64 q-tile, its 4 waves a 2 x 2 grid (cout half, q-row); WM = 1:
 // 64 output channels (cout 64 layers) x a 4 x 64 q-tile, the 4 waves one q-row each; WM = 1 at input stride 2 (the
 // 4-row halo would not fit): a 2 x 64 q-tile, the 4 waves a 2 x 2 grid (q-row, 32-column half).
-template <bool TWO, int IS, int WM>
-__global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_kernel(const Conv2dArgs a, int tiles_x,
-                                                                                      int tiles_y, int nsl, int dmin, int span) {
+// T = float: the fp32 parity path's form (one halo buffer, rewritten between two barriers after a slice's last tap).
+template <typename T, bool TWO, int IS, int WM>
+__global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : IS == 1 ? 3 : 2) void conv2d_wide_kernel(
+    const Conv2dArgs a, int tiles_x, int tiles_y, int nsl, int dmin, int span) {
   typedef uint4 raw;
-  typedef BufIO<bf16_t> IO;
-  constexpr uint32_t ES = 2;
-  constexpr int WPER = IS == 1 ? 7 : 11;  // halo pieces per thread: up to 448 / 704 pixels
+  typedef WideForm<T> Fm;
+  constexpr bool SP = sizeof(T) == 4;
+  constexpr int PL = Fm::PL, SLOTS = Fm::SLOTS;
+  constexpr uint32_t ES = sizeof(T);
+  constexpr int WPER = IS == 1 ? 7 : 11;  // 8-channel halo pieces per thread: up to 448 / 704 pixels
   constexpr bool HALFW = WM == 1 && IS == 2;     // waves of 32 q-columns
   constexpr int NGW = HALFW ? 2 : 4;             // 16-column N-groups per wave
   constexpr int WRT = HALFW ? 2 : 4 / WM;        // q-tile rows
-  constexpr int AR = WM * 256;             // raws of one K chunk's A fragments (WM x 4 cout tiles)
+  constexpr int AR = WM * 256 * PL;        // 16-byte slots of one K chunk's A fragments (WM x 4 cout tiles)
+  constexpr int NA = WM * PL;              // A loads per thread and chunk
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  raw* abuf = reinterpret_cast<raw*>(smem);  // 2 x AR raws (WM x 4 KB per chunk)
+  raw* abuf = reinterpret_cast<raw*>(smem);  // 2 x AR slots
   const WideHalo<IS, WRT> hg(span);
   const int HP = hg.hp;
-  // stride 1: the next slice's halo goes to the other of two buffers; stride 2 (2.5x the pixels): one buffer,
-  // rewritten between two barriers after the slice's last tap
-  constexpr int NHB = IS == 1 ? 2 : 1;
-  raw* hbuf = abuf + 2 * AR;                 // NHB x HP * 4 raws
+  // bf16 stride 1: the next slice's halo goes to the other of two buffers; otherwise (stride 2: 2.5x the pixels;
+  // fp32: twice the bytes) one buffer, rewritten between two barriers after the slice's last tap
+  constexpr int NHB = IS == 1 && !SP ? 2 : 1;
+  raw* hbuf = abuf + 2 * AR;                 // NHB x HP * SLOTS slots
 
   // logical block = (tile, phase), phase fastest, XCD-contiguous
   const int ntile = tiles_x * tiles_y * a.B;
@@ -808,44 +828,62 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
   if (tid < 25) s_toff[tid] = tid < ph.ntaps ? hg.pix(ph.tap[tid][0] - dmin, ph.tap[tid][1] - dmin) : 0;
 
   const int nt = ph.ntaps;  // loop order (slice, tap); packed order chunk = tap * nsl + slice
-  const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack) + ((size_t)ph.w_off * a.MTtot + mt0) * 64;
-  const size_t cstride = (size_t)a.MTtot * 64;  // raws between consecutive packed chunks
+  const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack) + ((size_t)ph.w_off * a.MTtot + mt0) * 64 * PL;
+  const size_t cstride = (size_t)a.MTtot * 64 * PL;  // slots between consecutive packed chunks
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.wpack, 0x7fffffffLL);
-  const uint32_t wbase = (uint32_t)(((size_t)ph.w_off * a.MTtot + mt0) * 64 * 16);
-  const uint32_t cbytes = (uint32_t)a.MTtot * 64 * 16;  // bytes between consecutive packed chunks
+  const uint32_t wbase = (uint32_t)(((size_t)ph.w_off * a.MTtot + mt0) * 64 * 16 * PL);
+  const uint32_t cbytes = (uint32_t)a.MTtot * 64 * 16 * PL;  // bytes between consecutive packed chunks
   const int npix = a.B * a.Hi * a.Wi;
   const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.in0, (long long)npix * a.c0 * ES);
   const __amdgpu_buffer_rsrc_t r1 = make_rsrc(TWO ? a.in1 : a.in0, TWO ? (long long)npix * a.c1 * ES : 0);
   const int iy0 = IS * qy0 + dmin, ix0 = IS * qx0 + dmin, pb = b * a.Hi * a.Wi;
-  // this thread's halo pieces: input pixel index (-1: outside the image or past the halo) and the 16-byte
-  // chunk it fetches, the same for every slice
-  int hpix[WPER], hch[WPER];
+  // this thread's halo pieces (8 channels each): input pixel index (-1: outside the image or past the halo), the
+  // channel offset it fetches and the LDS slot(s) it fills, the same for every slice
+  int hpix[WPER], hch[WPER], hsl[WPER];
 #pragma unroll
   for (int k = 0; k < WPER; ++k) {
     const int i = tid + k * 256;
-    const int p = i >> 2, slot = i & 3;
+    const int p = i >> 2, q = i & 3;
     int row, col;
     hg.rc(p, row, col);
     const int iy = iy0 + row, ix = ix0 + col;
     const bool ok = p < HP && col >= 0 && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
     hpix[k] = ok ? pb + iy * a.Wi + ix : -1;
-    hch[k] = (slot ^ ((p >> 2) & 3)) * 8;
+    if (SP) {
+      hch[k] = q * 8;                                   // chunk q: hi to slot q, lo to slot 4 + q
+      hsl[k] = p < HP ? p * SLOTS : -1;
+    } else {
+      hch[k] = (q ^ ((p >> 2) & 3)) * 8;                // chunk q ^ sw to slot q (the thread's own)
+      hsl[k] = p < HP ? i : -1;
+    }
   }
-  raw hreg[WPER];
+  raw hreg[WPER][PL];
   auto hload = [&](int c) {
     const bool second = TWO && c * 32 >= a.c0;
     const int cs = second ? a.c1 : a.c0, cb = second ? c * 32 - a.c0 : c * 32;
 #pragma unroll
     for (int k = 0; k < WPER; ++k) {
       const uint32_t off = hpix[k] >= 0 ? (uint32_t)(hpix[k] * cs + cb + hch[k]) * ES : kOOB;
-      hreg[k] = (TWO && second) ? IO::frag(r1, off) : IO::frag(r0, off);
+#pragma unroll
+      for (int h = 0; h < PL; ++h) {
+        const uint32_t o = off == kOOB ? kOOB : off + 16u * h;
+        hreg[k][h] = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128((TWO && second) ? r1 : r0, o, 0, 0));
+      }
     }
   };
   auto hstore = [&](int bi) {
 #pragma unroll
     for (int k = 0; k < WPER; ++k) {
-      const int i = tid + k * 256;
-      if ((i >> 2) < HP) hbuf[bi * HP * 4 + i] = hreg[k];
+      if (hsl[k] < 0) continue;
+      if constexpr (SP) {
+        const int p = hsl[k] / SLOTS, q = hch[k] >> 3;
+        const F16Pair v = split8(__builtin_bit_cast(float4, hreg[k][0]), __builtin_bit_cast(float4, hreg[k][1]));
+        raw* hb = hbuf + bi * HP * SLOTS + hsl[k];
+        hb[Fm::slot(p, q)] = v.h;
+        hb[Fm::slot(p, q + 4)] = v.l;
+      } else {
+        hbuf[bi * HP * SLOTS + hsl[k]] = hreg[k][0];
+      }
     }
   };
 
@@ -856,7 +894,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
     for (int j = 0; j < NGW; ++j) acc[m][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   // the fp32 depth plane's halo (zero outside the image) for the trailing plane chunk, staged once
-  float* gbuf = reinterpret_cast<float*>(hbuf + NHB * HP * 4);  // HP floats
+  float* gbuf = reinterpret_cast<float*>(hbuf + NHB * HP * SLOTS);  // HP floats
   if (ph.gchunks > 0) {
     const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.geo[0], ((long long)(a.B - 1) * a.geo_bstride[0] + a.Hi * a.Wi) * 4);
     const int pg0 = b * (int)a.geo_bstride[0];
@@ -870,12 +908,12 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
   }
 
   // One K chunk per barrier, slices outer and taps inner. A: chunk k + 2 is loaded (scalar offset: no
-  // per-chunk VGPR address math) into one register pair while the other pair (chunk k + 1) goes to LDS
+  // per-chunk VGPR address math) into one register set while the other set (chunk k + 1) goes to LDS
   // after chunk k's MFMAs; loads past the last chunk re-read it (unconditional: exact vmcnt counting).
   // Halo of slice c + 1: loaded after tap 0's A store of slice c (hipcc counts the vmcnt in front of that
   // store as if no halo load were pending, so issuing them later keeps them out of it), stored after the
   // slice's last tap.
-  raw p0, p1, q0, q1;
+  raw pa[NA], qa[NA];
   int lc = 0, lt = 0;  // (slice, tap) of the next chunk to load, two ahead of the chunk computed
   auto next = [&](int& cc, int& tt) {
     if (++tt == nt) {
@@ -883,43 +921,60 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
       cc = cc + 1 < nsl ? cc + 1 : cc;  // past the end: stays on the last slice (clamped re-read)
     }
   };
-  auto wld = [&](raw& x0, raw& x1) {
+  auto wld = [&](raw (&x)[NA]) {
     const uint32_t so = wbase + (uint32_t)(lt * nsl + lc) * cbytes;
-    x0 = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)tid * 16u, so, 0));
-    if (WM == 2) x1 = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(tid + 256) * 16u, so, 0));
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      x[i] = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(tid + 256 * i) * 16u, so, 0));
     if (!(lc == nsl - 1 && lt == nt - 1)) next(lc, lt);
   };
-  wld(p0, p1);
-  wld(q0, q1);
+  wld(pa);
+  wld(qa);
   hload(0);
-  abuf[tid] = p0;
-  if (WM == 2) abuf[tid + 256] = p1;
+#pragma unroll
+  for (int i = 0; i < NA; ++i) abuf[tid + 256 * i] = pa[i];
   hstore(0);
   __syncthreads();
   const int lanepix = wn * IS * hg.pitch + wc + n;
   int k = 0;
-  auto step = [&](int c, int t, raw& ld0, raw& ld1, const raw& st0, const raw& st1) {
-    if (!(DAMVS_WIDE_DIAG & 8)) wld(ld0, ld1);
-    const raw* ab = abuf + (k & 1) * AR + wm * 256 + lane;
-    raw af[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) af[m] = ab[m * 64];
-    // 16 pixels apart keeps (p >> 2) & 3: one swizzled address, the 4 N-groups at immediate offsets
+  auto step = [&](int c, int t, raw (&ld)[NA], const raw (&st)[NA]) {
+    if (!(DAMVS_WIDE_DIAG & 8)) wld(ld);
     const int p0x = s_toff[t] + lanepix;
-    const raw* hb = hbuf + (NHB == 2 ? (c & 1) * HP * 4 : 0) + p0x * 4 + (g ^ ((p0x >> 2) & 3));
-    raw bf[NGW];
+    const raw* hb = hbuf + (NHB == 2 ? (c & 1) * HP * SLOTS : 0) + p0x * SLOTS;
+    if constexpr (SP) {
+      // A: tile m of the wave's cout half at m * 128 (hi) and m * 128 + 64 (lo); B: pixel + 16 j keeps the swizzle
+      const raw* ab = abuf + (k & 1) * AR + wm * 512 + lane;
+      F16Pair af[4], bf[NGW];
 #pragma unroll
-    for (int j = 0; j < NGW; ++j) bf[j] = hb[j * 64];
-    if (!(DAMVS_WIDE_DIAG & 1)) {
+      for (int m = 0; m < 4; ++m) af[m] = F16Pair{ab[m * 128], ab[m * 128 + 64]};
+      const int sh = Fm::slot(p0x, g), sl = Fm::slot(p0x, g + 4);
+#pragma unroll
+      for (int j = 0; j < NGW; ++j) bf[j] = F16Pair{hb[j * 16 * SLOTS + sh], hb[j * 16 * SLOTS + sl]};
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int j = 0; j < NGW; ++j) Frag2<bf16_t>::mma(af[m], bf[j], acc[m][j]);
+        for (int j = 0; j < NGW; ++j) mma_split32(af[m], bf[j], acc[m][j]);
     } else {
-      acc[0][0][0] += __uint_as_float(af[0].x ^ bf[0].y);
+      const raw* ab = abuf + (k & 1) * AR + wm * 256 + lane;
+      raw af[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) af[m] = ab[m * 64];
+      // 16 pixels apart keeps (p >> 2) & 3: one swizzled address, the 4 N-groups at immediate offsets
+      const raw* hbs = hb + Fm::slot(p0x, g);
+      raw bf[NGW];
+#pragma unroll
+      for (int j = 0; j < NGW; ++j) bf[j] = hbs[j * 64];
+      if (!(DAMVS_WIDE_DIAG & 1)) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int j = 0; j < NGW; ++j) Frag2<bf16_t>::mma(af[m], bf[j], acc[m][j]);
+      } else {
+        acc[0][0][0] += __uint_as_float(af[0].x ^ bf[0].y);
+      }
     }
-    abuf[((k + 1) & 1) * AR + tid] = st0;  // past the last chunk: a harmless copy
-    if (WM == 2) abuf[((k + 1) & 1) * AR + tid + 256] = st1;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) abuf[((k + 1) & 1) * AR + tid + 256 * i] = st[i];  // past the last chunk: a harmless copy
     if (!(DAMVS_WIDE_DIAG & 4)) {
       if (t == 0 && c + 1 < nsl) hload(c + 1);
       if (t == nt - 1 && c + 1 < nsl) {
@@ -932,23 +987,17 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
   };
   int c = 0, t = 0;
   const int nk = nt * nsl;
-  for (int kk = 0; kk < nk; kk += 2) {  // unrolled by two: the register pairs alternate statically
-    step(c, t, p0, p1, q0, q1);
+  for (int kk = 0; kk < nk; kk += 2) {  // unrolled by two: the register sets alternate statically
+    step(c, t, pa, qa);
     if (++t == nt) { t = 0; ++c; }
     if (kk + 1 < nk) {
-      step(c, t, q0, q1, p0, p1);
+      step(c, t, qa, pa);
       if (++t == nt) { t = 0; ++c; }
     }
   }
 
   // tail: the plane chunk (A fragments straight from global memory), then the epilogue
   const int qyw = qy0 + wn;  // the wave's q-row
-  raw ag[4];
-  if (ph.gchunks > 0) {
-    const raw* __restrict__ wg = wsrc + (size_t)ph.kchunks * cstride + wm * 256 + lane;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) ag[m] = wg[m * 64];
-  }
   const int up = a.post_up, us = a.post_up >> 1;
   const long long nout = (long long)a.B * a.Ho * a.Wo * a.cout;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout * ES);
@@ -965,11 +1014,28 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
 #pragma unroll
       for (int j = 0; j < NGW; ++j) v[j][e] = tv ? gbuf[po + j * 16] : 0.f;
     }
+    if constexpr (SP) {
+      const raw* wg = wsrc + (size_t)ph.kchunks * cstride + wm * 512 + lane;
+      F16Pair ag[4];
 #pragma unroll
-    for (int j = 0; j < NGW; ++j) {
-      const raw xf = pack_vals<bf16_t>(v[j]);
+      for (int m = 0; m < 4; ++m) ag[m] = F16Pair{wg[m * 128], wg[m * 128 + 64]};
 #pragma unroll
-      for (int m = 0; m < 4; ++m) Frag2<bf16_t>::mma(ag[m], xf, acc[m][j]);
+      for (int j = 0; j < NGW; ++j) {
+        const F16Pair xf = split8(v[j]);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) mma_split32(ag[m], xf, acc[m][j]);
+      }
+    } else {
+      const raw* wg = wsrc + (size_t)ph.kchunks * cstride + wm * 256 + lane;
+      raw ag[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) ag[m] = wg[m * 64];
+#pragma unroll
+      for (int j = 0; j < NGW; ++j) {
+        const raw xf = pack_vals<bf16_t>(v[j]);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) Frag2<bf16_t>::mma(ag[m], xf, acc[m][j]);
+      }
     }
   }
 
@@ -978,7 +1044,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
     // through LDS: the wave's 64 channels x 64 pixels go to a wave-private fp32 staging tile in two halves of 32
     // pixels (the K loop's A and halo buffers are free after its last barrier; 4 x 8.5 KB stay below the plane
     // halo, which other waves may still read), and each lane then finishes one pixel's
-    // 32-channel half: 64 contiguous bytes of residual loads and stores (16-byte accesses; the accumulator layout
+    // 32-channel half: contiguous residual loads and stores (16-byte accesses; the accumulator layout
     // stores 8 bytes per lane, 16 pixels apart). Row pitch 68 floats: the b128 writes of 16 lanes (16 pixels,
     // one column) and reads (16 pixels) hit distinct banks.
     constexpr int PITCH = 68;
@@ -988,12 +1054,20 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
     const int co0 = cb + hc * 32;
     const bool cvalid = co0 < a.cout;
     const float* bias = a.bias + (cvalid ? co0 : 0);  // a padded channel tile past cout reads channel 0's bias
-    auto add8 = [](const raw& q, float* v) {
-      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    auto add8 = [](const raw* q, float* v) {  // 8 channels of a residual record (bf16: one slot, fp32: two)
+      if constexpr (SP) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v[2 * i] += __uint_as_float(w[i] << 16);
-        v[2 * i + 1] += __uint_as_float(w[i] & 0xffff0000u);
+        for (int h = 0; h < 2; ++h) {
+          const float4 f = __builtin_bit_cast(float4, q[h]);
+          v[4 * h] += f.x; v[4 * h + 1] += f.y; v[4 * h + 2] += f.z; v[4 * h + 3] += f.w;
+        }
+      } else {
+        const uint32_t w[4] = {q[0].x, q[0].y, q[0].z, q[0].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[2 * i] += __uint_as_float(w[i] << 16);
+          v[2 * i + 1] += __uint_as_float(w[i] & 0xffff0000u);
+        }
       }
     };
 #pragma unroll
@@ -1014,52 +1088,67 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(IS == 1 ? 3 : 2) void conv2d_wide_
       const bool ok = qyw < a.Hq && qx < a.Wq && cvalid;
       const uint32_t ooff = ok ? (uint32_t)(pout * a.cout + co0) * ES : kOOB;
       const uint32_t poff = ok ? (uint32_t)(ppost * a.cout + co0) * ES : kOOB;
-      raw pre[4], post[4];  // all residual records requested before the first store
+      raw pre[4][PL], post[4][PL];  // all residual records requested before the first store
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (a.res_pre) pre[k] = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rpre, ooff + 16u * k, 0, 0));
-        if (a.res_post) post[k] = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rpost, poff + 16u * k, 0, 0));
-      }
+      for (int k2 = 0; k2 < 4; ++k2)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {  // 8 channels at a time
+        for (int h2 = 0; h2 < PL; ++h2) {
+          const uint32_t d = 16u * (k2 * PL + h2);
+          if (a.res_pre) pre[k2][h2] = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rpre, ooff + d, 0, 0));
+          if (a.res_post) post[k2][h2] = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rpost, poff + d, 0, 0));
+        }
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) {  // 8 channels at a time
         float r[8];
-        const float4 v0 = *reinterpret_cast<const float4*>(st + lp * PITCH + hc * 32 + 8 * k);
-        const float4 v1 = *reinterpret_cast<const float4*>(st + lp * PITCH + hc * 32 + 8 * k + 4);
-        const float4 b0 = *reinterpret_cast<const float4*>(bias + 8 * k);
-        const float4 b1 = *reinterpret_cast<const float4*>(bias + 8 * k + 4);
-        r[0] = v0.x + b0.x; r[1] = v0.y + b0.y; r[2] = v0.z + b0.z; r[3] = v0.w + b0.w;
-        r[4] = v1.x + b1.x; r[5] = v1.y + b1.y; r[6] = v1.z + b1.z; r[7] = v1.w + b1.w;
-        if (a.res_pre) add8(pre[k], r);
+        const float4 v0 = *reinterpret_cast<const float4*>(st + lp * PITCH + hc * 32 + 8 * k2);
+        const float4 v1 = *reinterpret_cast<const float4*>(st + lp * PITCH + hc * 32 + 8 * k2 + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(bias + 8 * k2);
+        const float4 b1 = *reinterpret_cast<const float4*>(bias + 8 * k2 + 4);
+        r[0] = fmaf(v0.x, a.wscale, b0.x); r[1] = fmaf(v0.y, a.wscale, b0.y);
+        r[2] = fmaf(v0.z, a.wscale, b0.z); r[3] = fmaf(v0.w, a.wscale, b0.w);
+        r[4] = fmaf(v1.x, a.wscale, b1.x); r[5] = fmaf(v1.y, a.wscale, b1.y);
+        r[6] = fmaf(v1.z, a.wscale, b1.z); r[7] = fmaf(v1.w, a.wscale, b1.w);
+        if (a.res_pre) add8(pre[k2], r);
         if (a.relu) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) r[e] = fmaxf(r[e], 0.f);
         }
-        if (a.res_post) add8(post[k], r);
-        uint32_t w[4];
+        if (a.res_post) add8(post[k2], r);
+        if constexpr (SP) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(r[2 * i]) | ((uint32_t)f2bf(r[2 * i + 1]) << 16);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, make_uint4(w[0], w[1], w[2], w[3])), ro,
-                                               ooff + 16u * k, 0, 0);
+          for (int h2 = 0; h2 < 2; ++h2)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(v4u32_t, make_float4(r[4 * h2], r[4 * h2 + 1], r[4 * h2 + 2], r[4 * h2 + 3])), ro,
+                ooff + 32u * k2 + 16u * h2, 0, 0);
+        } else {
+          uint32_t w[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(r[2 * i]) | ((uint32_t)f2bf(r[2 * i + 1]) << 16);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, make_uint4(w[0], w[1], w[2], w[3])), ro,
+                                                 ooff + 16u * k2, 0, 0);
+        }
       }
       asm volatile("" ::: "memory");  // the next half overwrites the staging tile
     }
   }
 }
 
-template <int IS, int WM>
+template <typename T, int IS, int WM>
 hipError_t launch_wide_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span) {
-  constexpr int WRT = WM == 1 && IS == 2 ? 2 : 4 / WM, AR = WM * 256;
+  constexpr bool SP = sizeof(T) == 4;
+  constexpr int WRT = WM == 1 && IS == 2 ? 2 : 4 / WM, AR = WM * 256 * WideForm<T>::PL, SLOTS = WideForm<T>::SLOTS;
   const WideHalo<IS, WRT> hg(span);
-  constexpr int NHB = IS == 1 ? 2 : 1, WPER = IS == 1 ? 7 : 11;
+  constexpr int NHB = IS == 1 && !SP ? 2 : 1, WPER = IS == 1 ? 7 : 11;
   if (hg.hp * 4 > WPER * 256) return hipErrorNotSupported;
-  const size_t below_plane = 2 * (size_t)AR * 16 + NHB * (size_t)hg.hp * 64;
+  const size_t below_plane = 2 * (size_t)AR * 16 + NHB * (size_t)hg.hp * SLOTS * 16;
   if (below_plane < 4 * 32 * 68 * 4) return hipErrorNotSupported;  // the epilogue's staging tiles stay below the plane halo
   const int tx = (a.Wq + WC - 1) / WC, ty = (a.Hq + WRT - 1) / WRT;
   const int nsl = (a.c0 + a.c1) / 32;
   const size_t smem = below_plane + (size_t)hg.hp * 4;  // A chunks, halo slices, plane halo
+  if (smem > 160 * 1024) return hipErrorNotSupported;
   const long long nblk = (long long)tx * ty * a.B * a.nphase;
   const dim3 grid((unsigned)nblk, (unsigned)(a.MTtot / (4 * WM)));
-  auto k = a.c1 > 0 ? conv2d_wide_kernel<true, IS, WM> : conv2d_wide_kernel<false, IS, WM>;
+  auto k = a.c1 > 0 ? conv2d_wide_kernel<T, true, IS, WM> : conv2d_wide_kernel<T, false, IS, WM>;
   if (smem > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)smem);
@@ -1069,14 +1158,9 @@ hipError_t launch_wide_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span)
   return hipGetLastError();
 }
 
-// Returns hipErrorNotSupported when the wide kernel does not take the layer (bf16 callers only). Input stride 2
-// (the stride-2 GeoBlock convs, one phase) unless DAMVS_CONV2D_WIDE_S2=0; cout 64 at input stride 1 on the 64-channel
-// block (WM = 1) unless DAMVS_CONV2D_WIDE64=0.
-hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
-  static const bool off = [] {
-    const char* v = getenv("DAMVS_CONV2D_WIDE");
-    return v && v[0] == '0';
-  }();
+// Shape checks of the wide kernel (K chunks of 32: bf16 packing, or the fp32 layer's 32-K split packing); returns
+// the tap offset range in dmin / span.
+bool wide_shape_ok(const Conv2dArgs& a, int& dmin, int& span) {
   static const bool s2 = [] {
     const char* v = getenv("DAMVS_CONV2D_WIDE_S2");
     return !(v && v[0] == '0');
@@ -1087,21 +1171,36 @@ hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
   }();
   const bool stride_ok = a.in_stride == 1 || (a.in_stride == 2 && s2 && a.nphase == 1 && a.out_stride == 1);
   const bool half = w64 && a.MTtot == 4;  // 64 output channels
-  if (off || !stride_ok || a.xpair || a.ngeo > 1 || (a.MTtot % 8 && !half) || a.c0 % 32 || a.c1 % 32 || a.c0 + a.c1 < 64 ||
+  if (!stride_ok || a.xpair || a.ngeo > 1 || (a.MTtot % 8 && !half) || a.c0 % 32 || a.c1 % 32 || a.c0 + a.c1 < 64 ||
       a.cout % 32)  // the epilogue finishes whole 32-channel halves per lane
-    return hipErrorNotSupported;
-  int dmin = 0, dmax = 0;
+    return false;
+  int lo = 0, hi = 0;
   for (int p = 0; p < a.nphase; ++p)
     for (int t = 0; t < a.ph[p].ntaps; ++t)
       for (int d = 0; d < 2; ++d) {
-        dmin = a.ph[p].tap[t][d] < dmin ? a.ph[p].tap[t][d] : dmin;
-        dmax = a.ph[p].tap[t][d] > dmax ? a.ph[p].tap[t][d] : dmax;
+        lo = a.ph[p].tap[t][d] < lo ? a.ph[p].tap[t][d] : lo;
+        hi = a.ph[p].tap[t][d] > hi ? a.ph[p].tap[t][d] : hi;
       }
-  const int span = dmax - dmin + 1;
   for (int p = 0; p < a.nphase; ++p)  // geo taps beyond one K chunk; fewer than 4 taps (halo schedule)
-    if (a.ph[p].gchunks > 1 || a.ph[p].ntaps < 4) return hipErrorNotSupported;
-  if (half) return a.in_stride == 1 ? launch_wide_t<1, 1>(s, a, dmin, span) : launch_wide_t<2, 1>(s, a, dmin, span);
-  return a.in_stride == 1 ? launch_wide_t<1, 2>(s, a, dmin, span) : launch_wide_t<2, 2>(s, a, dmin, span);
+    if (a.ph[p].gchunks > 1 || a.ph[p].ntaps < 4) return false;
+  dmin = lo;
+  span = hi - lo + 1;
+  return true;
+}
+
+// Returns hipErrorNotSupported when the wide kernel does not take the layer. Input stride 2 (the stride-2 GeoBlock
+// convs, one phase) unless DAMVS_CONV2D_WIDE_S2=0; cout 64 at input stride 1 on the 64-channel block (WM = 1) unless
+// DAMVS_CONV2D_WIDE64=0. T = float: `a` carries the layer's 32-K split packing (a.wide32, damvs_conv2d_forward).
+template <typename T>
+hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
+  static const bool off = [] {
+    const char* v = getenv("DAMVS_CONV2D_WIDE");
+    return v && v[0] == '0';
+  }();
+  int dmin = 0, span = 0;
+  if (off || !wide_shape_ok(a, dmin, span)) return hipErrorNotSupported;
+  if (a.MTtot % 8) return a.in_stride == 1 ? launch_wide_t<T, 1, 1>(s, a, dmin, span) : launch_wide_t<T, 2, 1>(s, a, dmin, span);
+  return a.in_stride == 1 ? launch_wide_t<T, 1, 2>(s, a, dmin, span) : launch_wide_t<T, 2, 2>(s, a, dmin, span);
 }
 
 // True when the layer is a plain 3x3 stride-1 padding-1 conv with dense row-major taps.
@@ -1412,6 +1511,10 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
     return hipGetLastError();
   }
   if (a.ngeo > 1) return hipErrorInvalidValue;  // the MFMA path takes at most one plane
+  if (a.wide32) {  // fp32 layer with its 32-K split packing (damvs_conv2d_forward checked conv2d_wide_shape_ok)
+    if constexpr (sizeof(T) == 4) return launch_wide<T>(s, a);
+    return hipErrorInvalidValue;
+  }
   if (a.xpair) {  // x-pair phases (built at layer creation): only the XP gather kernel runs them
     if (a.cout != 8 || a.MTtot != 1 || a.ngeo != 0 || a.nphase != 2) return hipErrorInvalidValue;
     const long long Qtot = (long long)a.B * a.Hq * a.Wq;
@@ -1429,7 +1532,7 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
     e = launch_halo<T>(s, a);
     if (e != hipErrorNotSupported) return e;
     if constexpr (T_is_bf16<T>::value) {
-      e = launch_wide(s, a);
+      e = launch_wide<T>(s, a);
       if (e != hipErrorNotSupported) return e;
     }
   }
@@ -1589,6 +1692,11 @@ hipError_t launch_border_bias(hipStream_t s, int store, const BorderArgs& a, int
   else
     hipLaunchKernelGGL(border_bias_kernel<float>, grid, dim3(256), 0, s, a, B, H, W, cstored, cout, static_cast<float*>(out));
   return hipGetLastError();
+}
+
+bool conv2d_wide_shape_ok(const Conv2dArgs& a) {
+  int dmin = 0, span = 0;
+  return wide_shape_ok(a, dmin, span);
 }
 
 hipError_t launch_conv2d(hipStream_t s, int store, const Conv2dArgs& a) {

@@ -1056,22 +1056,55 @@ hipError_t launch_lds(hipStream_t s, const ConvArgs& a) {
   return hipErrorNotSupported;
 }
 
-// conv11 (ConvTranspose3d k3 s2 p1 op1, 16 -> 8 channels, bf16, in-place skip) streamed along z:
+// Storage forms of the z-streamed kernels' LDS rings. bf16: a voxel of CH 8-channel chunks is CH 16-byte slots, chunk c
+// in slot c. fp32 (the split-f16 form, damvs_device.h mma_split32): 2 CH slots, the hi / lo halves of chunk c in slots
+// c and CH + c, XOR-swizzled by the voxel's column (zsw) so that 16 lanes reading one chunk of 16 consecutive voxels
+// (one MFMA B fragment) hit distinct bank groups; rows and planes shift by whole voxels and keep the swizzle.
+template <typename T> struct ZForm;
+template <> struct ZForm<bf16_t> {
+  typedef uint4 frag;
+  static constexpr int PL = 1;  // 16-byte slots (and HBM loads) per 8-channel chunk
+  template <int S> __device__ __forceinline__ static int zsw(int) { return 0; }
+  __device__ __forceinline__ static void mma(const frag& w, const frag& x, f32x4_t& acc) { Frag<bf16_t>::mma(w, x, acc); }
+  // A fragment s of a [chunk][lane] packing
+  __device__ __forceinline__ static frag wload(const uint4* __restrict__ w, int s, int lane) { return w[(size_t)s * 64 + lane]; }
+  // B fragment of chunk c of the voxel at ring slot base vs (column swizzle sw)
+  __device__ __forceinline__ static frag bread(const uint4* p, int c, int CH, int sw) { (void)CH; (void)sw; return p[c]; }
+};
+template <> struct ZForm<float> {
+  typedef F16Pair frag;
+  static constexpr int PL = 2;
+  template <int S> __device__ __forceinline__ static int zsw(int col) { return (col / (16 / S)) % S; }
+  __device__ __forceinline__ static void mma(const frag& w, const frag& x, f32x4_t& acc) { mma_split32(w, x, acc); }
+  // [chunk][hi: 64 lanes][lo: 64 lanes] (split_weights_blocked)
+  __device__ __forceinline__ static frag wload(const uint4* __restrict__ w, int s, int lane) {
+    return F16Pair{w[(size_t)s * 128 + lane], w[(size_t)s * 128 + 64 + lane]};
+  }
+  __device__ __forceinline__ static frag bread(const uint4* p, int c, int CH, int sw) {
+    return F16Pair{p[c ^ sw], p[(CH + c) ^ sw]};
+  }
+};
+
+// conv11 (ConvTranspose3d k3 s2 p1 op1, 16 -> 8 channels, in-place skip) streamed along z:
 // a block owns 8 x 16 input-grid columns (q) over DZ consecutive q-planes; input planes pass
 // through a 4-slot LDS ring ((8+1) x (16+1) x 16 channels: the deconv only reaches offsets 0 and
 // +1), loaded two planes ahead. Per q-plane each wave produces, for its 2 q-rows, the 4 (pz, py)
 // x-pair phases of build_phases_xpair (K chunk (a, b) = z offset a, y offset b, lane group g >> 1 =
 // x offset, g & 1 = channel half) with the 9 A fragments in registers, so the whole layer is the
 // skip read + output write + one pass over the input, with no per-lane tap decoding or bounds tests
-// in the K loop. Same K order and weights as the x-pair gather kernel: identical results.
-__global__ __launch_bounds__(256) DAMVS_WAVES(3) void deconv_xpair_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y,
+// in the K loop. bf16: same K order and weights as the x-pair gather kernel, identical results. fp32 (T = float):
+// the split-f16 form (ZForm<float>: fp32 loads split once into the ring, 3 MFMAs per product, fp32 skip and output).
+template <typename T>
+__global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 2 ? 3 : 2) void deconv_xpair_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y,
                                                                   int nzc, int zc, int ntiles) {
-  typedef uint4 raw;
-  constexpr int CH = 2, QX = 16, QY = 8, PW = QX + 1, PH = QY + 1;
-  constexpr int PLANE = PH * PW * CH;
-  constexpr int NLD = (PLANE + 255) / 256;
+  typedef ZForm<T> Z;
+  typedef typename Z::frag frag;
+  constexpr int PL = Z::PL, ES = sizeof(T);
+  constexpr int CH = 2, S = CH * PL, QX = 16, QY = 8, PW = QX + 1, PH = QY + 1;
+  constexpr int PLANE = PH * PW * S;           // 16-byte slots per ring plane
+  constexpr int NLD = (PH * PW * CH + 255) / 256;  // 8-channel chunks per thread per plane
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  raw* ring = reinterpret_cast<raw*>(smem);
+  uint4* ring = reinterpret_cast<uint4*>(smem);
 
   const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
   int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
@@ -1082,34 +1115,54 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void deconv_xpair_zslide_kernel
   const int qx0 = tx * QX, qy0 = ty * QY, zb = tz * zc;
   const int zend = min(zb + zc, a.Di);
 
-  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 16 * 2);
-  auto load_plane = [&](int iz, raw* v) {
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 16 * ES);
+  auto load_plane = [&](int iz, uint4 (*v)[PL]) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int c = threadIdx.x + i * 256;
       const int row = c / (PW * CH), col = c - row * (PW * CH);
       const int iy = qy0 + row, ix = qx0 + col / CH;
-      const bool ok = c < PLANE && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+      const bool ok = c < PH * PW * CH && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
                       (unsigned)ix < (unsigned)a.Wi;
-      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + qx0) * CH + col) * 16u;
-      v[i] = BufIO<bf16_t>::frag(rin, ok ? off : kOOB);
+      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + qx0) * CH + col) * (16u * PL);
+#pragma unroll
+      for (int h = 0; h < PL; ++h) v[i][h] = BufIO<bf16_t>::frag(rin, ok ? off + 16u * h : kOOB);
     }
   };
-  auto store_plane = [&](int iz, const raw* v) {
-    raw* dst = ring + (iz & 3) * PLANE;
+  auto store_plane = [&](int iz, const uint4 (*v)[PL]) {
+    uint4* dst = ring + (iz & 3) * PLANE;
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int c = threadIdx.x + i * 256;
-      if (c < PLANE) dst[c] = v[i];
+      if (c >= PH * PW * CH) continue;
+      if constexpr (PL == 1) {
+        dst[c] = v[i][0];
+      } else {
+        const int vox = c / CH, q = c - vox * CH, sw = Z::template zsw<S>(vox % PW);
+        const F16Pair p = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+        dst[vox * S + (q ^ sw)] = p.h;
+        dst[vox * S + ((CH + q) ^ sw)] = p.l;
+      }
     }
   };
-  raw wreg[9];
-  {
-    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack) + (threadIdx.x & 63);
+  // A fragments: bf16 in registers (9 x 4 VGPRs); fp32 (split, twice the registers) in LDS after the ring, read per
+  // use, so the kernel keeps two waves per SIMD
+  constexpr int NWR = PL == 1 ? 9 : 1;
+  frag wreg[NWR];
+  uint4* alds = ring + 4 * PLANE;  // fp32: 9 chunks x 128 slots
+  if constexpr (PL == 1) {
+    const uint4* __restrict__ wsrc = reinterpret_cast<const uint4*>(a.wpack) + (threadIdx.x & 63);
 #pragma unroll
-    for (int s = 0; s < 9; ++s) wreg[s] = wsrc[(size_t)s * 64];
+    for (int s = 0; s < 9; ++s) wreg[s] = Z::wload(wsrc, s, 0);
+  } else {
+    const uint4* __restrict__ wsrc = reinterpret_cast<const uint4*>(a.wpack);
+    for (int i = threadIdx.x; i < 9 * 128; i += 256) alds[i] = wsrc[i];
   }
-  raw pa[NLD], pb[NLD];
+  auto wfrag = [&](int s) -> frag {
+    if constexpr (PL == 1) return wreg[s];
+    else return Z::wload(alds, s, threadIdx.x & 63);
+  };
+  uint4 pa[NLD][PL], pb[NLD][PL];
   load_plane(zb, pa);
   store_plane(zb, pa);
   load_plane(zb + 1, pa);
@@ -1120,31 +1173,35 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void deconv_xpair_zslide_kernel
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
   const bool lead = (g & 1) == 0;
-  const int lbase = (2 * wave * PW + n + (g >> 1)) * CH + (g & 1);  // q-row 2w, column n, x offset g>>1
+  const int lcol = n + (g >> 1), lsw = Z::template zsw<S>(lcol);
+  const int lbase = (2 * wave * PW + lcol) * S + (PL == 1 ? (g & 1) : 0);  // q-row 2w, column n, x offset g>>1
+  const int lch = PL == 1 ? 0 : (g & 1);  // chunk (channel half) of this lane group, split form
   float b8[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) b8[i] = a.bias[i];
-  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * 8 * 2;
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * 8 * ES;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.resid ? a.resid : a.out, a.resid ? nout : 0);
   const int qx = qx0 + n;
 
-  auto step = [&](int qz, raw* cur, raw* nxt) {
+  auto step = [&](int qz, uint4 (*cur)[PL], uint4 (*nxt)[PL]) {
     if (qz + 2 < zend) load_plane(qz + 3, nxt);
     // output offsets and the skip records of this plane's 8 outputs, loaded before the MFMAs
     uint32_t off[8];
-    raw rq[8];
+    uint4 rq[8][PL];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int pd = k >> 2, py = (k >> 1) & 1, r = k & 1;
       const int qy = qy0 + 2 * wave + r;
       const bool ok = lead && qy < a.Hi && qx < a.Wi;
       const int oz = 2 * qz + pd, oy = 2 * qy + py, ox = 2 * qx + (g >> 1);
-      off[k] = ok ? (uint32_t)((((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * 8) * 2u : kOOB;
-      rq[k] = BufIO<bf16_t>::frag(rr, off[k]);  // zero when there is no skip tensor (empty range)
+      off[k] = ok ? (uint32_t)((((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * 8) * (uint32_t)ES : kOOB;
+#pragma unroll
+      for (int h = 0; h < PL; ++h)  // zero when there is no skip tensor (empty range)
+        rq[k][h] = BufIO<bf16_t>::frag(rr, off[k] == kOOB ? kOOB : off[k] + 16u * h);
     }
-    const raw* p0 = ring + (qz & 3) * PLANE + lbase;        // q-plane qz (z offset 0)
-    const raw* p1 = ring + ((qz + 1) & 3) * PLANE + lbase;  // q-plane qz + 1 (z offset +1)
+    const uint4* p0 = ring + (qz & 3) * PLANE + lbase;        // q-plane qz (z offset 0)
+    const uint4* p1 = ring + ((qz + 1) & 3) * PLANE + lbase;  // q-plane qz + 1 (z offset +1)
     f32x4_t acc[8];  // [pd][py][r]
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
@@ -1159,10 +1216,11 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void deconv_xpair_zslide_kernel
 #pragma unroll
           for (int cb = 0; cb < nb; ++cb) {
             const int zo = pd ? (ca == 0 ? 1 : 0) : 0, yo = py ? (cb == 0 ? 1 : 0) : 0;
-            const raw w = wreg[w0 + ca * nb + cb];
-            const raw* src = (zo ? p1 : p0) + yo * PW * CH;
+            const frag w = wfrag(w0 + ca * nb + cb);
+            const uint4* src = (zo ? p1 : p0) + yo * PW * S;
 #pragma unroll
-            for (int r = 0; r < 2; ++r) Frag<bf16_t>::mma(w, src[r * PW * CH], acc[(pd * 2 + py) * 2 + r]);
+            for (int r = 0; r < 2; ++r)
+              Z::mma(w, Z::bread(src + r * PW * S, lch, CH, lsw), acc[(pd * 2 + py) * 2 + r]);
           }
       }
     // epilogue per output: partner channels, bias, ReLU, skip (after the ReLU), 16-byte store
@@ -1174,14 +1232,24 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(3) void deconv_xpair_zslide_kernel
         v[i] = acc[k][i];
         v[4 + i] = __shfl_down(acc[k][i], 16);
       }
-      const uint32_t q4[4] = {rq[k].x, rq[k].y, rq[k].z, rq[k].w};
+      if constexpr (PL == 1) {
+        const uint32_t q4[4] = {rq[k][0].x, rq[k][0].y, rq[k][0].z, rq[k][0].w};
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        v[i] += b8[i];
-        if (a.relu) v[i] = fmaxf(v[i], 0.f);
-        v[i] += __uint_as_float((i & 1) ? (q4[i >> 1] & 0xffff0000u) : (q4[i >> 1] << 16));
+        for (int i = 0; i < 8; ++i) {
+          v[i] += b8[i];
+          if (a.relu) v[i] = fmaxf(v[i], 0.f);
+          v[i] += __uint_as_float((i & 1) ? (q4[i >> 1] & 0xffff0000u) : (q4[i >> 1] << 16));
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float4 f = __builtin_bit_cast(float4, rq[k][i >> 2]);
+          v[i] = v[i] * a.wscale + b8[i];  // 2^-k: exact
+          if (a.relu) v[i] = fmaxf(v[i], 0.f);
+          v[i] += (i & 3) == 0 ? f.x : (i & 3) == 1 ? f.y : (i & 3) == 2 ? f.z : f.w;
+        }
       }
-      if (lead) Vox8<bf16_t>::store(ro, off[k], v);
+      if (lead) Vox8<T>::store(ro, off[k], v);
     }
     if (qz + 1 < zend) store_plane(qz + 2, cur);  // slot of plane qz - 2, released by the last barrier
     __syncthreads();
@@ -1479,12 +1547,15 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
   long long per_block = 4LL * kGroups * 16;
   const int nq = (int)((Qtot + per_block - 1) / per_block);
   dim3 grid((unsigned)(nq * a.nphase));
-  if (sizeof(T) == 2 && a.xpair && a.Cin == 16 && a.Cout == 8 && a.nphase == 4 && !deconv_zslide_disabled()) {
+  if ((sizeof(T) == 2 || a.wpack32) && a.xpair && a.Cin == 16 && a.Cout == 8 && a.nphase == 4 &&
+      !deconv_zslide_disabled()) {
     constexpr int zc = 8;
     const int tx = (a.Wi + 15) / 16, ty = (a.Hi + 7) / 8, nzc = (a.Di + zc - 1) / zc;
     const long long nt = (long long)tx * ty * nzc * a.B;
-    const size_t smem = 4 * 9 * 17 * 2 * 16;
-    hipLaunchKernelGGL(deconv_xpair_zslide_kernel, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
+    const size_t smem = 4 * 9 * 17 * 2 * 16 * ZForm<T>::PL + (sizeof(T) == 4 ? 9 * 128 * 16 : 0);
+    ConvArgs az = a;
+    if (sizeof(T) == 4) az.wpack = a.wpack32;  // fp32: the blocked 32-K split packing of the x-pair phases
+    hipLaunchKernelGGL(deconv_xpair_zslide_kernel<T>, dim3((unsigned)nt), dim3(256), smem, s, az, tx, ty, nzc, zc, (int)nt);
     return hipGetLastError();
   }
   if (sizeof(T) == 2 && a.nphase == 1 && a.in_stride == 2 && a.Cin == 8 && a.Cout == 16 && a.MT == 1 && !a.resid &&
