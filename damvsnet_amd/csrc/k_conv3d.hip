@@ -570,26 +570,58 @@ __global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, 
   }
 }
 
-// z-sliding row-pair variant (bf16 conv0): a block owns an 8-row x TX-column output window over ZC
+// Storage forms of the z-streamed kernels' LDS rings. bf16: a voxel of CH 8-channel chunks is CH 16-byte slots, chunk c
+// in slot c. fp32 (the split-f16 form, damvs_device.h mma_split32): 2 CH slots, the hi / lo halves of chunk c in slots
+// c and CH + c, XOR-swizzled by the voxel's column (zsw) so that 16 lanes reading one chunk of 16 consecutive voxels
+// (one MFMA B fragment) hit distinct bank groups; rows and planes shift by whole voxels and keep the swizzle.
+template <typename T> struct ZForm;
+template <> struct ZForm<bf16_t> {
+  typedef uint4 frag;
+  static constexpr int PL = 1;  // 16-byte slots (and HBM loads) per 8-channel chunk
+  template <int S> __device__ __forceinline__ static int zsw(int) { return 0; }
+  __device__ __forceinline__ static void mma(const frag& w, const frag& x, f32x4_t& acc) { Frag<bf16_t>::mma(w, x, acc); }
+  // A fragment s of a [chunk][lane] packing
+  __device__ __forceinline__ static frag wload(const uint4* __restrict__ w, int s, int lane) { return w[(size_t)s * 64 + lane]; }
+  // B fragment of chunk c of the voxel at ring slot base vs (column swizzle sw)
+  __device__ __forceinline__ static frag bread(const uint4* p, int c, int CH, int sw) { (void)CH; (void)sw; return p[c]; }
+};
+template <> struct ZForm<float> {
+  typedef F16Pair frag;
+  static constexpr int PL = 2;
+  template <int S> __device__ __forceinline__ static int zsw(int col) { return (col / (16 / S)) % S; }
+  __device__ __forceinline__ static void mma(const frag& w, const frag& x, f32x4_t& acc) { mma_split32(w, x, acc); }
+  // [chunk][hi: 64 lanes][lo: 64 lanes] (split_weights_blocked)
+  __device__ __forceinline__ static frag wload(const uint4* __restrict__ w, int s, int lane) {
+    return F16Pair{w[(size_t)s * 128 + lane], w[(size_t)s * 128 + 64 + lane]};
+  }
+  __device__ __forceinline__ static frag bread(const uint4* p, int c, int CH, int sw) {
+    return F16Pair{p[c ^ sw], p[(CH + c) ^ sw]};
+  }
+};
+
+// z-sliding row-pair variant (conv0): a block owns an 8-row x TX-column output window over ZC
 // consecutive z-planes and streams the input through a 4-plane ring of (8+2) x (TX+2) x CIN halo
 // planes in LDS. Each output plane needs one new input plane, fetched into registers while the
 // current plane's MFMAs run and written to the ring slot freed by the plane before (one barrier
 // per plane): HBM/L2 re-reads drop from 2.1x (6x10x18 halo per 4x8x16 tile) to ~1.66x and the
-// fill latency is hidden behind compute instead of preceding it. Same K order, weights
-// (pack_layer_pair) and accumulation chain as conv3d_lds_pair_kernel: identical results.
+// fill latency is hidden behind compute instead of preceding it. bf16: same K order, weights
+// (pack_layer_pair) and accumulation chain as conv3d_lds_pair_kernel, identical results. fp32 (T = float, CIN 8 / 16):
+// the split-f16 form (ZForm<float>), the row-pair packing at 32 K per chunk (ConvArgs::wpack32).
 // Wave w owns row pair (y0 + 2w, y0 + 2w + 1); lane column n the output x = x0 + 16 xg + n.
-template <int CIN, int TXG>
-__global__ __launch_bounds__(256) void conv3d_zslide_pair_kernel(const ConvArgs a, int tiles_x, int tiles_y,
+template <typename T, int CIN, int TXG>
+__global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : 1) void conv3d_zslide_pair_kernel(const ConvArgs a, int tiles_x, int tiles_y,
                                                                  int nzc, int zc, int ntiles) {
-  typedef uint4 raw;
-  constexpr int E = 8, KC = 32, CH = CIN / E;
+  typedef ZForm<T> Z;
+  typedef typename Z::frag frag;
+  constexpr int PL = Z::PL, ES = sizeof(T);
+  constexpr int E = 8, KC = 32, CH = CIN / E, S = CH * PL;
   constexpr int TX = 16 * TXG, PW = TX + 2, PH = LTH + 2;
-  constexpr int PLANE = PH * PW * CH;  // 16-byte chunks per halo plane
-  constexpr int NLD = (PLANE + 255) / 256;
+  constexpr int PLANE = PH * PW * S;        // 16-byte slots per halo plane
+  constexpr int NLD = (PH * PW * CH + 255) / 256;  // 8-channel chunks per thread per plane
   constexpr int KCHUNKS = 36 * CIN / KC;
   static_assert(KC % CIN == 0 || CIN % KC == 0, "chunking");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  raw* ring = reinterpret_cast<raw*>(smem);
+  uint4* ring = reinterpret_cast<uint4*>(smem);
 
   const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
   int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
@@ -600,35 +632,44 @@ __global__ __launch_bounds__(256) void conv3d_zslide_pair_kernel(const ConvArgs 
   const int x0 = tx * TX, y0 = ty * LTH, zb = tz * zc;
   const int zend = min(zb + zc, a.Do);
 
-  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * 2);
-  auto load_plane = [&](int iz, raw* v) {
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * ES);
+  auto load_plane = [&](int iz, uint4 (*v)[PL]) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int c = threadIdx.x + i * 256;
       const int row = c / (PW * CH), col = c - row * (PW * CH);
       const int iy = y0 - 1 + row, ix = x0 - 1 + col / CH;
-      const bool ok = c < PLANE && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+      const bool ok = c < PH * PW * CH && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
                       (unsigned)ix < (unsigned)a.Wi;
-      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16u;
-      v[i] = BufIO<bf16_t>::frag(rin, ok ? off : kOOB);
+      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * (16u * PL);
+#pragma unroll
+      for (int h = 0; h < PL; ++h) v[i][h] = BufIO<bf16_t>::frag(rin, ok ? off + 16u * h : kOOB);
     }
   };
-  auto store_plane = [&](int iz, const raw* v) {
-    raw* dst = ring + ((iz + 4) & 3) * PLANE;
+  auto store_plane = [&](int iz, const uint4 (*v)[PL]) {
+    uint4* dst = ring + ((iz + 4) & 3) * PLANE;
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int c = threadIdx.x + i * 256;
-      if (c < PLANE) dst[c] = v[i];
+      if (c >= PH * PW * CH) continue;
+      if constexpr (PL == 1) {
+        dst[c] = v[i][0];
+      } else {
+        const int vox = c / CH, q = c - vox * CH, sw = Z::template zsw<S>(vox % PW);
+        const F16Pair p = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+        dst[vox * S + (q ^ sw)] = p.h;
+        dst[vox * S + ((CH + q) ^ sw)] = p.l;
+      }
     }
   };
-  // the layer's A fragments stay in registers for all ZC planes (18 / 36 VGPR quads for CIN 16 / 32)
-  raw wreg[KCHUNKS];
+  // the layer's A fragments stay in registers for all ZC planes (bf16: 18 / 36 VGPR quads for CIN 16 / 32)
+  frag wreg[KCHUNKS];
   {
-    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack_pair) + (threadIdx.x & 63);
+    const uint4* __restrict__ wsrc = reinterpret_cast<const uint4*>(PL == 1 ? a.wpack_pair : a.wpack32) + (threadIdx.x & 63);
 #pragma unroll
-    for (int s = 0; s < KCHUNKS; ++s) wreg[s] = wsrc[(size_t)s * 64];
+    for (int s = 0; s < KCHUNKS; ++s) wreg[s] = Z::wload(wsrc, s, 0);
   }
-  raw pa[NLD], pb[NLD];
+  uint4 pa[NLD][PL], pb[NLD][PL];
 #pragma unroll
   for (int p = -1; p <= 1; ++p) {
     load_plane(zb + p, pa);
@@ -640,8 +681,10 @@ __global__ __launch_bounds__(256) void conv3d_zslide_pair_kernel(const ConvArgs 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
   const int gi = (g * E) / CIN, gc = (g * E) % CIN / E;
-  const int lbase = (2 * wave * PW + n) * CH + gc;  // this lane's chunk at tap (dy' = 0, dx = 0)
-  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * 2;
+  // bf16: this lane's chunk at tap (dy' = 0, dx = 0); fp32: its voxel (the chunk and its column swizzle per tap)
+  const int lbase = PL == 1 ? (2 * wave * PW + n) * CH + gc : (2 * wave * PW + n) * S;
+  const int sw0 = Z::template zsw<S>(n), sw1 = Z::template zsw<S>(n + 1), sw2 = Z::template zsw<S>(n + 2);
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * ES;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
   const int co = (g & 1) * 4, r = g >> 1;
   float bias[4];
@@ -651,41 +694,49 @@ __global__ __launch_bounds__(256) void conv3d_zslide_pair_kernel(const ConvArgs 
 
   // one output plane: plane z + 2 (in `cur`, loaded one plane earlier) goes to the ring after the
   // MFMAs; plane z + 3 is fetched into `nxt` before them, so each load has two planes of cover
-  auto step = [&](int z, raw* cur, raw* nxt) {
+  auto step = [&](int z, uint4 (*cur)[PL], uint4 (*nxt)[PL]) {
     if (z + 2 < zend) load_plane(z + 3, nxt);
-    const raw* pl[3] = {ring + ((z + 3) & 3) * PLANE + lbase, ring + ((z + 4) & 3) * PLANE + lbase,
-                        ring + ((z + 5) & 3) * PLANE + lbase};
+    const uint4* pl[3] = {ring + ((z + 3) & 3) * PLANE + lbase, ring + ((z + 4) & 3) * PLANE + lbase,
+                          ring + ((z + 5) & 3) * PLANE + lbase};
     f32x4_t acc[TXG];
 #pragma unroll
     for (int xg = 0; xg < TXG; ++xg) acc[xg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KCHUNKS; ++s) {
-      const raw wf = wreg[s];
+      const frag wf = wreg[s];
       const int kt = (s * KC) / CIN, kc = ((s * KC) % CIN) / E;
       const int dz = kt / 12;  // uniform over the chunk's taps (12 taps per dz, 1/2/4 taps per chunk)
-      auto toff = [](int t) { return (((t / 3) % 4) * PW + t % 3) * CH; };
-      int off = toff(kt);
+      auto toff = [](int t) { return (((t / 3) % 4) * PW + t % 3) * (PL == 1 ? CH : S); };
+      int off = toff(kt), dx = kt % 3;
       if (KC > CIN) {
         off = gi == 1 ? toff(kt + 1) : off;
         off = gi == 2 ? toff(kt + 2) : off;
         off = gi == 3 ? toff(kt + 3) : off;
+        if (PL == 2) dx = (kt + gi) % 3;
       }
-      const raw* src = pl[dz] + off + kc;
+      if constexpr (PL == 1) {
+        const uint4* src = pl[dz] + off + kc;
 #pragma unroll
-      for (int xg = 0; xg < TXG; ++xg) Frag<bf16_t>::mma(wf, src[16 * xg * CH], acc[xg]);
+        for (int xg = 0; xg < TXG; ++xg) Z::mma(wf, src[16 * xg * CH], acc[xg]);
+      } else {
+        const uint4* src = pl[dz] + off;
+        const int sw = dx == 0 ? sw0 : dx == 1 ? sw1 : sw2;  // +16 columns keep the swizzle
+#pragma unroll
+        for (int xg = 0; xg < TXG; ++xg) Z::mma(wf, Z::bread(src + 16 * xg * S, kc + gc, CH, sw), acc[xg]);
+      }
     }
 #pragma unroll
     for (int xg = 0; xg < TXG; ++xg) {
       const int ox = x0 + 16 * xg + n;
       const bool vok = oy < a.Ho && ox < a.Wo && co < a.Cout;
-      const uint32_t off = (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * a.Cout + co) * 2u;
+      const uint32_t off = (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * a.Cout + co) * (uint32_t)ES;
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        v[i] = acc[xg][i] + bias[i];
+        v[i] = (PL == 1 ? acc[xg][i] : acc[xg][i] * a.wscale) + bias[i];  // 2^-k: exact
         if (a.relu) v[i] = fmaxf(v[i], 0.f);
       }
-      BufIO<bf16_t>::stq(ro, vok ? off : kOOB, v);
+      BufIO<T>::stq(ro, vok ? off : kOOB, v);
     }
     if (z + 1 < zend) store_plane(z + 2, cur);  // slot of plane z - 2, last read before the previous barrier
     __syncthreads();
@@ -836,9 +887,9 @@ bool zslide_disabled() {  // read per call: tests flip it between launches
   return v && v[0] == '1';
 }
 
-template <int CIN, int TXG>
+template <typename T, int CIN, int TXG>
 hipError_t launch_zslide_pair_t(hipStream_t s, const ConvArgs& a) {
-  constexpr int PLANE = (LTH + 2) * (16 * TXG + 2) * (CIN / 8);
+  constexpr int PLANE = (LTH + 2) * (16 * TXG + 2) * (CIN / 8) * ZForm<T>::PL;
   const size_t smem = 4 * PLANE * 16;
   static const int zc = [] {
     const char* v = getenv("DAMVS_ZSLIDE_ZC");
@@ -847,8 +898,13 @@ hipError_t launch_zslide_pair_t(hipStream_t s, const ConvArgs& a) {
   }();
   const int tx = (a.Wo + 16 * TXG - 1) / (16 * TXG), ty = (a.Ho + LTH - 1) / LTH, nzc = (a.Do + zc - 1) / zc;
   const long long nt = (long long)tx * ty * nzc * a.B;
-  hipLaunchKernelGGL((conv3d_zslide_pair_kernel<CIN, TXG>), dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc,
-                     (int)nt);
+  auto k = conv3d_zslide_pair_kernel<T, CIN, TXG>;
+  if (smem > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)smem);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
   return hipGetLastError();
 }
 
@@ -874,8 +930,14 @@ hipError_t launch_lds_pair_t(hipStream_t s, const ConvArgs& a) {
       const char* rv = getenv("DAMVS_CONV0_REUSE");
       const bool reuse = rv ? rv[0] == '1' : CIN == 32;
       if (reuse) return launch_zreuse_pair_t<CIN, 2>(s, a);
-      if constexpr (CIN == 32) return launch_zslide_pair_t<CIN, 1>(s, a);
-      else return launch_zslide_pair_t<CIN, 2>(s, a);
+      if constexpr (CIN == 32) return launch_zslide_pair_t<T, CIN, 1>(s, a);
+      else return launch_zslide_pair_t<T, CIN, 2>(s, a);
+    }
+  } else if constexpr (CIN <= 16) {
+    // fp32: the split-f16 z-streamed kernel on the 32-K row-pair packing (A fragments in registers at CIN 8 / 16)
+    if (!a.resid && a.wpack32 && !zslide_disabled()) {
+      if constexpr (CIN == 16) return launch_zslide_pair_t<T, CIN, 1>(s, a);  // 18 A pairs: 8 x 16 windows, no spill
+      else return launch_zslide_pair_t<T, CIN, 2>(s, a);
     }
   }
   const size_t smem = lds_tile_bytes<T, CIN>();
@@ -1034,7 +1096,7 @@ hipError_t launch_lds(hipStream_t s, const ConvArgs& a) {
   if (a.wpack_pair && a.Cout <= 8 && !no_pair) {
     if (a.Cin == 8) return launch_lds_pair_t<T, 8>(s, a);
     if (a.Cin == 16) return launch_lds_pair_t<T, 16>(s, a);
-    if (a.Cin == 32 && sizeof(T) == 2) return launch_lds_pair_t<T, 32>(s, a);
+    if (a.Cin == 32) return launch_lds_pair_t<T, 32>(s, a);  // fp32: the 138 KB tile (one block per CU)
   }
   if (sizeof(T) == 2 && a.Cin == 16 && a.Cout == 16 && MT == 1 && !a.resid && !zslide_disabled()) {
     constexpr int zc = 16;
@@ -1055,35 +1117,6 @@ hipError_t launch_lds(hipStream_t s, const ConvArgs& a) {
   if (a.Cin == 32 && MT == 2) return launch_lds_t<T, 32, 2>(s, a);
   return hipErrorNotSupported;
 }
-
-// Storage forms of the z-streamed kernels' LDS rings. bf16: a voxel of CH 8-channel chunks is CH 16-byte slots, chunk c
-// in slot c. fp32 (the split-f16 form, damvs_device.h mma_split32): 2 CH slots, the hi / lo halves of chunk c in slots
-// c and CH + c, XOR-swizzled by the voxel's column (zsw) so that 16 lanes reading one chunk of 16 consecutive voxels
-// (one MFMA B fragment) hit distinct bank groups; rows and planes shift by whole voxels and keep the swizzle.
-template <typename T> struct ZForm;
-template <> struct ZForm<bf16_t> {
-  typedef uint4 frag;
-  static constexpr int PL = 1;  // 16-byte slots (and HBM loads) per 8-channel chunk
-  template <int S> __device__ __forceinline__ static int zsw(int) { return 0; }
-  __device__ __forceinline__ static void mma(const frag& w, const frag& x, f32x4_t& acc) { Frag<bf16_t>::mma(w, x, acc); }
-  // A fragment s of a [chunk][lane] packing
-  __device__ __forceinline__ static frag wload(const uint4* __restrict__ w, int s, int lane) { return w[(size_t)s * 64 + lane]; }
-  // B fragment of chunk c of the voxel at ring slot base vs (column swizzle sw)
-  __device__ __forceinline__ static frag bread(const uint4* p, int c, int CH, int sw) { (void)CH; (void)sw; return p[c]; }
-};
-template <> struct ZForm<float> {
-  typedef F16Pair frag;
-  static constexpr int PL = 2;
-  template <int S> __device__ __forceinline__ static int zsw(int col) { return (col / (16 / S)) % S; }
-  __device__ __forceinline__ static void mma(const frag& w, const frag& x, f32x4_t& acc) { mma_split32(w, x, acc); }
-  // [chunk][hi: 64 lanes][lo: 64 lanes] (split_weights_blocked)
-  __device__ __forceinline__ static frag wload(const uint4* __restrict__ w, int s, int lane) {
-    return F16Pair{w[(size_t)s * 128 + lane], w[(size_t)s * 128 + 64 + lane]};
-  }
-  __device__ __forceinline__ static frag bread(const uint4* p, int c, int CH, int sw) {
-    return F16Pair{p[c ^ sw], p[(CH + c) ^ sw]};
-  }
-};
 
 // conv11 (ConvTranspose3d k3 s2 p1 op1, 16 -> 8 channels, in-place skip) streamed along z:
 // a block owns 8 x 16 input-grid columns (q) over DZ consecutive q-planes; input planes pass
