@@ -534,6 +534,15 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
       pack_layer<float>(P, wf, E, pk, cvt_f32);
       rc = upload_split(pk, kexp, &P.wpack);
     }
+    if (rc == DAMVS_OK && dtype != DAMVS_BF16 && P.kind == CONV_S1 && P.cin == 16 && P.cout == 16) {
+      // conv2's z-streamed kernel (conv_s1_c16_zslide<float>): the plain packing at 32 K per chunk
+      LayerPlan P32 = P;
+      build_phases(P32, 32);
+      std::vector<float> p32;
+      pack_layer<float>(P32, wf, 8, p32, cvt_f32);
+      const std::vector<uint16_t> h = split_weights_blocked(p32, kexp);
+      rc = upload(h.data(), h.size() * 2, &P.wpack32);
+    }
     if (rc == DAMVS_OK && P.kind == DECONV_S2 && P.cout <= 8) {
       build_phases_xpair(P, 4 * E);
       if (dtype == DAMVS_BF16) {

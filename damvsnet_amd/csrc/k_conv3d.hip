@@ -968,20 +968,25 @@ hipError_t launch_lds_t(hipStream_t s, const ConvArgs& a) {
   return hipGetLastError();
 }
 
-// conv2 (Conv3d k3 s1 p1, 16 -> 16 channels, bf16) streamed along z on conv0's plan (4-slot ring of
-// (8+2) x (32+2) x 16-channel planes, two planes ahead), with 16 output channels as the MFMA rows
+// conv2 (Conv3d k3 s1 p1, 16 -> 16 channels) streamed along z on conv0's plan (4-slot ring of
+// (8+2) x (TX+2) x 16-channel planes, two planes ahead), with 16 output channels as the MFMA rows
 // instead of conv0's row pairs: K = 27 taps x 16 channels in 14 chunks of 2 taps (lane group g:
 // tap 2s + (g >> 1), channel half g & 1; a chunk's two taps may sit in different planes), the 14 A
-// fragments in registers. Same K order and weights as conv3d_lds_kernel.
-__global__ __launch_bounds__(256) void conv_s1_c16_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y, int nzc,
+// fragments in registers. bf16 (TXG 2): same K order and weights as conv3d_lds_kernel. fp32 (T = float, TXG 1:
+// 8 x 16 windows, so the 14 split A pairs fit beside two waves per SIMD): the split-f16 form on the layer's 32-K
+// packing (ConvArgs::wpack32).
+template <typename T, int TXG>
+__global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : 1) void conv_s1_c16_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y, int nzc,
                                                                  int zc, int ntiles) {
-  typedef uint4 raw;
-  constexpr int CH = 2, TXG = 2, TX = 16 * TXG, PW = TX + 2, PH = LTH + 2;
-  constexpr int PLANE = PH * PW * CH;
-  constexpr int NLD = (PLANE + 255) / 256;
+  typedef ZForm<T> Z;
+  typedef typename Z::frag frag;
+  constexpr int PL = Z::PL, ES = sizeof(T);
+  constexpr int CH = 2, S = CH * PL, TX = 16 * TXG, PW = TX + 2, PH = LTH + 2;
+  constexpr int PLANE = PH * PW * S;
+  constexpr int NLD = (PH * PW * CH + 255) / 256;
   constexpr int KCH = 14;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  raw* ring = reinterpret_cast<raw*>(smem);
+  uint4* ring = reinterpret_cast<uint4*>(smem);
 
   const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
   int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
@@ -992,34 +997,43 @@ __global__ __launch_bounds__(256) void conv_s1_c16_zslide_kernel(const ConvArgs 
   const int x0 = tx * TX, y0 = ty * LTH, zb = tz * zc;
   const int zend = min(zb + zc, a.Do);
 
-  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 16 * 2);
-  auto load_plane = [&](int iz, raw* v) {
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 16 * ES);
+  auto load_plane = [&](int iz, uint4 (*v)[PL]) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int c = threadIdx.x + i * 256;
       const int row = c / (PW * CH), col = c - row * (PW * CH);
       const int iy = y0 - 1 + row, ix = x0 - 1 + col / CH;
-      const bool ok = c < PLANE && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+      const bool ok = c < PH * PW * CH && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
                       (unsigned)ix < (unsigned)a.Wi;
-      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16u;
-      v[i] = BufIO<bf16_t>::frag(rin, ok ? off : kOOB);
+      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * (16u * PL);
+#pragma unroll
+      for (int h = 0; h < PL; ++h) v[i][h] = BufIO<bf16_t>::frag(rin, ok ? off + 16u * h : kOOB);
     }
   };
-  auto store_plane = [&](int iz, const raw* v) {
-    raw* dst = ring + ((iz + 4) & 3) * PLANE;
+  auto store_plane = [&](int iz, const uint4 (*v)[PL]) {
+    uint4* dst = ring + ((iz + 4) & 3) * PLANE;
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int c = threadIdx.x + i * 256;
-      if (c < PLANE) dst[c] = v[i];
+      if (c >= PH * PW * CH) continue;
+      if constexpr (PL == 1) {
+        dst[c] = v[i][0];
+      } else {
+        const int vox = c / CH, q = c - vox * CH, sw = Z::template zsw<S>(vox % PW);
+        const F16Pair p = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+        dst[vox * S + (q ^ sw)] = p.h;
+        dst[vox * S + ((CH + q) ^ sw)] = p.l;
+      }
     }
   };
-  raw wreg[KCH];
+  frag wreg[KCH];
   {
-    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack) + (threadIdx.x & 63);
+    const uint4* __restrict__ wsrc = reinterpret_cast<const uint4*>(PL == 1 ? a.wpack : a.wpack32) + (threadIdx.x & 63);
 #pragma unroll
-    for (int s = 0; s < KCH; ++s) wreg[s] = wsrc[(size_t)s * 64];
+    for (int s = 0; s < KCH; ++s) wreg[s] = Z::wload(wsrc, s, 0);
   }
-  raw pa[NLD], pb[NLD];
+  uint4 pa[NLD][PL], pb[NLD][PL];
 #pragma unroll
   for (int p = -1; p <= 1; ++p) {
     load_plane(zb + p, pa);
@@ -1031,17 +1045,19 @@ __global__ __launch_bounds__(256) void conv_s1_c16_zslide_kernel(const ConvArgs 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
   const int gi = g >> 1, gc = g & 1;
-  const int lbase = (2 * wave * PW + n) * CH + gc;  // output row 2w (halo row 2w at dy = 0), column n
-  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * 16 * 2;
+  // output row 2w (halo row 2w at dy = 0), column n: bf16 the lane's chunk, fp32 its voxel
+  const int lbase = PL == 1 ? (2 * wave * PW + n) * CH + gc : (2 * wave * PW + n) * S;
+  const int sw0 = Z::template zsw<S>(n), sw1 = Z::template zsw<S>(n + 1), sw2 = Z::template zsw<S>(n + 2);
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * 16 * ES;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
   float bias[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) bias[i] = a.bias[g * 4 + i];
 
-  auto step = [&](int z, raw* cur, raw* nxt) {
+  auto step = [&](int z, uint4 (*cur)[PL], uint4 (*nxt)[PL]) {
     if (z + 2 < zend) load_plane(z + 3, nxt);
-    const raw* pl[3] = {ring + ((z + 3) & 3) * PLANE + lbase, ring + ((z + 4) & 3) * PLANE + lbase,
-                        ring + ((z + 5) & 3) * PLANE + lbase};
+    const uint4* pl[3] = {ring + ((z + 3) & 3) * PLANE + lbase, ring + ((z + 4) & 3) * PLANE + lbase,
+                          ring + ((z + 5) & 3) * PLANE + lbase};
     f32x4_t acc[2][TXG];
 #pragma unroll
     for (int r = 0; r < 2; ++r)
@@ -1049,17 +1065,20 @@ __global__ __launch_bounds__(256) void conv_s1_c16_zslide_kernel(const ConvArgs 
       for (int xg = 0; xg < TXG; ++xg) acc[r][xg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KCH; ++s) {
-      auto tap = [&](int t) {  // (plane, in-plane offset); tap 27 (K padding) reads tap 26 against zero weights
+      auto tap = [&](int t) {  // (plane, in-plane offset, dx); tap 27 (K padding) reads tap 26 against zero weights
         const int tc = t < 27 ? t : 26;
-        return (tc / 9) * 65536 + (((tc / 3) % 3) * PW + tc % 3) * CH;
+        return (tc / 9) * 65536 + (((tc / 3) % 3) * PW + tc % 3) * (PL == 1 ? CH : S) * 4 + tc % 3;
       };
       const int code = gi ? tap(2 * s + 1) : tap(2 * s);
-      const int dz = code >> 16, o = code & 0xffff;
-      const raw* src = (dz == 0 ? pl[0] : dz == 1 ? pl[1] : pl[2]) + o;
+      const int dz = code >> 16, o = (code & 0xffff) >> 2, dx = code & 3;
+      const uint4* src = (dz == 0 ? pl[0] : dz == 1 ? pl[1] : pl[2]) + o;
+      const int sw = dx == 0 ? sw0 : dx == 1 ? sw1 : sw2;  // fp32: the tap's column swizzle (+16 columns keep it)
 #pragma unroll
       for (int r = 0; r < 2; ++r)
 #pragma unroll
-        for (int xg = 0; xg < TXG; ++xg) Frag<bf16_t>::mma(wreg[s], src[r * PW * CH + 16 * xg * CH], acc[r][xg]);
+        for (int xg = 0; xg < TXG; ++xg)
+          Z::mma(wreg[s], Z::bread(src + r * PW * (PL == 1 ? CH : S) + 16 * xg * (PL == 1 ? CH : S), gc, CH, sw),
+                 acc[r][xg]);
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r)
@@ -1070,10 +1089,10 @@ __global__ __launch_bounds__(256) void conv_s1_c16_zslide_kernel(const ConvArgs 
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          v[i] = acc[r][xg][i] + bias[i];
+          v[i] = (PL == 1 ? acc[r][xg][i] : acc[r][xg][i] * a.wscale) + bias[i];  // 2^-k: exact
           if (a.relu) v[i] = fmaxf(v[i], 0.f);
         }
-        BufIO<bf16_t>::stq(ro, ok ? (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * 16 + g * 4) * 2u : kOOB, v);
+        BufIO<T>::stq(ro, ok ? (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * 16 + g * 4) * (uint32_t)ES : kOOB, v);
       }
     if (z + 1 < zend) store_plane(z + 2, cur);
     __syncthreads();
@@ -1098,12 +1117,13 @@ hipError_t launch_lds(hipStream_t s, const ConvArgs& a) {
     if (a.Cin == 16) return launch_lds_pair_t<T, 16>(s, a);
     if (a.Cin == 32) return launch_lds_pair_t<T, 32>(s, a);  // fp32: the 138 KB tile (one block per CU)
   }
-  if (sizeof(T) == 2 && a.Cin == 16 && a.Cout == 16 && MT == 1 && !a.resid && !zslide_disabled()) {
-    constexpr int zc = 16;
-    const int tx = (a.Wo + 31) / 32, ty = (a.Ho + LTH - 1) / LTH, nzc = (a.Do + zc - 1) / zc;
+  if ((sizeof(T) == 2 || a.wpack32) && a.Cin == 16 && a.Cout == 16 && MT == 1 && !a.resid && !zslide_disabled()) {
+    constexpr int zc = 16, TXG = sizeof(T) == 2 ? 2 : 1;
+    const int tx = (a.Wo + 16 * TXG - 1) / (16 * TXG), ty = (a.Ho + LTH - 1) / LTH, nzc = (a.Do + zc - 1) / zc;
     const long long nt = (long long)tx * ty * nzc * a.B;
-    const size_t smem = 4 * (LTH + 2) * 34 * 2 * 16;
-    hipLaunchKernelGGL(conv_s1_c16_zslide_kernel, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
+    const size_t smem = 4 * (LTH + 2) * (16 * TXG + 2) * 2 * 16 * ZForm<T>::PL;
+    hipLaunchKernelGGL((conv_s1_c16_zslide_kernel<T, TXG>), dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc,
+                       (int)nt);
     return hipGetLastError();
   }
   // The 4 x 8 x 16 tile stages a 6-plane halo: with fewer than 4 output planes (the deep levels at D = 8) most of
