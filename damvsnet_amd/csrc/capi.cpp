@@ -534,8 +534,10 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
       pack_layer<float>(P, wf, E, pk, cvt_f32);
       rc = upload_split(pk, kexp, &P.wpack);
     }
-    if (rc == DAMVS_OK && dtype != DAMVS_BF16 && P.kind == CONV_S1 && P.cin == 16 && P.cout == 16) {
-      // conv2's z-streamed kernel (conv_s1_c16_zslide<float>): the plain packing at 32 K per chunk
+    if (rc == DAMVS_OK && dtype != DAMVS_BF16 &&
+        ((P.kind == CONV_S1 && P.cin == 16 && P.cout == 16) || (P.kind == DECONV_S2 && P.cin == 32 && P.cout == 16) ||
+         (P.kind == CONV_S2 && P.cin == 8 && P.cout == 16))) {
+      // the z-streamed kernels of conv2, conv9 and conv1 (fp32 split-f16 forms): the plain packing at 32 K per chunk
       LayerPlan P32 = P;
       build_phases(P32, 32);
       std::vector<float> p32;

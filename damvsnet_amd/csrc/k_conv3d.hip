@@ -1313,21 +1313,26 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 2 ? 3 : 2) void decon
   }
 }
 
-// conv9 (ConvTranspose3d k3 s2 p1 op1, 32 -> 16 channels, bf16, in-place skip) streamed along z like
+// conv9 (ConvTranspose3d k3 s2 p1 op1, 32 -> 16 channels, in-place skip) streamed along z like
 // deconv_xpair_zslide_kernel: 4-slot LDS ring of (8+1) x (16+1) x 32-channel input q-planes loaded
 // two ahead, the 27 A fragments (8 single-parity phases of build_phases, 1 tap per K chunk, lane
-// group g = channel block g) in registers; per q-plane and half (pd) each wave issues its 8 skip
-// records first, then the 4 (py, px) phases x 2 q-rows, then the 16-byte epilogue (lane group g + 1
-// hands its 4 channels to group g). Same K order and weights as the gather kernel.
-template <bool AHEAD, bool ALDS>
+// group g = channel block g); per q-plane and half (pd) each wave issues its 8 skip records, then the
+// 4 (py, px) phases x 2 q-rows, then the 16-byte epilogue (lane group g + 1 hands its 4 channels to group g).
+// bf16 (ALDS): the A fragments in LDS after the ring (27 KB) instead of 108 VGPRs, two waves per SIMD; same K order
+// and weights as the gather kernel. fp32 (T = float, split-f16 form, the 32-K packing ConvArgs::wpack32): the 78 KB
+// ring leaves one block per CU, so the 27 A pairs sit in registers (one wave per SIMD, no LDS reads for A).
+template <typename T, bool ALDS>
 __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y, int nzc,
                                                                 int zc, int ntiles) {
-  typedef uint4 raw;
-  constexpr int CH = 4, QX = 16, QY = 8, PW = QX + 1, PH = QY + 1;
-  constexpr int PLANE = PH * PW * CH;
-  constexpr int NLD = (PLANE + 255) / 256;
+  typedef ZForm<T> Z;
+  typedef typename Z::frag frag;
+  constexpr int PL = Z::PL, ES = sizeof(T);
+  constexpr int CH = 4, S = CH * PL, QX = 16, QY = 8, PW = QX + 1, PH = QY + 1;
+  constexpr int PLANE = PH * PW * S;
+  constexpr int NLD = (PH * PW * CH + 255) / 256;
+  static_assert(!ALDS || PL == 1, "A fragments in LDS: bf16 form");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  raw* ring = reinterpret_cast<raw*>(smem);
+  uint4* ring = reinterpret_cast<uint4*>(smem);
 
   const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
   int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
@@ -1338,39 +1343,47 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
   const int qx0 = tx * QX, qy0 = ty * QY, zb = tz * zc;
   const int zend = min(zb + zc, a.Di);
 
-  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 32 * 2);
-  auto load_plane = [&](int iz, raw* v) {
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 32 * ES);
+  auto load_plane = [&](int iz, uint4 (*v)[PL]) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int c = threadIdx.x + i * 256;
       const int row = c / (PW * CH), col = c - row * (PW * CH);
       const int iy = qy0 + row, ix = qx0 + col / CH;
-      const bool ok = c < PLANE && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+      const bool ok = c < PH * PW * CH && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
                       (unsigned)ix < (unsigned)a.Wi;
-      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + qx0) * CH + col) * 16u;
-      v[i] = BufIO<bf16_t>::frag(rin, ok ? off : kOOB);
+      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + qx0) * CH + col) * (16u * PL);
+#pragma unroll
+      for (int h = 0; h < PL; ++h) v[i][h] = BufIO<bf16_t>::frag(rin, ok ? off + 16u * h : kOOB);
     }
   };
-  auto store_plane = [&](int iz, const raw* v) {
-    raw* dst = ring + (iz & 3) * PLANE;
+  auto store_plane = [&](int iz, const uint4 (*v)[PL]) {
+    uint4* dst = ring + (iz & 3) * PLANE;
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int c = threadIdx.x + i * 256;
-      if (c < PLANE) dst[c] = v[i];
+      if (c >= PH * PW * CH) continue;
+      if constexpr (PL == 1) {
+        dst[c] = v[i][0];
+      } else {
+        const int vox = c / CH, q = c - vox * CH, sw = Z::template zsw<S>(vox % PW);
+        const F16Pair p = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+        dst[vox * S + (q ^ sw)] = p.h;
+        dst[vox * S + ((CH + q) ^ sw)] = p.l;
+      }
     }
   };
-  // ALDS: the 27 A fragments in LDS after the ring (27 KB) instead of 108 VGPRs, for two waves per SIMD
-  raw wreg[ALDS ? 1 : 27];
-  raw* aw = ring + 4 * PLANE;
+  frag wreg[ALDS ? 1 : 27];
+  uint4* aw = ring + 4 * PLANE;
   if constexpr (ALDS) {
-    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack);
+    const uint4* __restrict__ wsrc = reinterpret_cast<const uint4*>(a.wpack);
     for (int i = threadIdx.x; i < 27 * 64; i += 256) aw[i] = wsrc[i];
   } else {
-    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack) + (threadIdx.x & 63);
+    const uint4* __restrict__ wsrc = reinterpret_cast<const uint4*>(PL == 1 ? a.wpack : a.wpack32) + (threadIdx.x & 63);
 #pragma unroll
-    for (int s = 0; s < 27; ++s) wreg[s] = wsrc[(size_t)s * 64];
+    for (int s = 0; s < 27; ++s) wreg[s] = Z::wload(wsrc, s, 0);
   }
-  raw pa[NLD], pb[NLD];
+  uint4 pa[NLD][PL], pb[NLD][PL];
   load_plane(zb, pa);
   store_plane(zb, pa);
   load_plane(zb + 1, pa);
@@ -1382,43 +1395,41 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
   const int n = lane & 15, g = lane >> 4;
   const bool lead = (g & 1) == 0;
   const int co = g * 4;                             // lead lanes own channels co .. co + 7
-  const int lbase = (2 * wave * PW + n) * CH + g;  // q-row 2w, column n, channel block g
+  // q-row 2w, column n: bf16 the lane's channel block g, fp32 its voxel (chunk g at the column's swizzle)
+  const int lbase = PL == 1 ? (2 * wave * PW + n) * CH + g : (2 * wave * PW + n) * S;
+  const int sw0 = Z::template zsw<S>(n), sw1 = Z::template zsw<S>(n + 1);
   float b8[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) b8[i] = a.bias[(co & 8) + i];
-  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * 16 * 2;
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * 16 * ES;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.resid ? a.resid : a.out, a.resid ? nout : 0);
   const int qx = qx0 + n;
   constexpr int WOFF[8] = {0, 1, 3, 5, 9, 11, 15, 19};  // build_phases chunk offsets (Cin 32)
 
-  // the 8 skip records of output half (qz, pd): requested one half ahead of their use (the next half's while this
-  // half's MFMAs run); half (qz, pd) writes plane 2 qz + pd, the prefetched half reads plane 2 qz + pd + 1
-  auto skip_load = [&](int qz, int pd, uint32_t* off, raw* rq) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {  // k = (py, px, r)
-      const int py = k >> 2, px = (k >> 1) & 1, r = k & 1;
-      const int qy = qy0 + 2 * wave + r;
-      const bool ok = lead && qy < a.Hi && qx < a.Wi;
-      const int oz = 2 * qz + pd, oy = 2 * qy + py, ox = 2 * qx + px;
-      off[k] = ok ? (uint32_t)((((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * 16 + (co & 8)) * 2u : kOOB;
-      rq[k] = BufIO<bf16_t>::frag(rr, off[k]);
-    }
-  };
-  uint32_t offA[8], offB[8];
-  raw rqA[8], rqB[8];
-  if (AHEAD) skip_load(zb, 0, offA, rqA);
-  auto step = [&](int qz, raw* cur, raw* nxt) {
+  auto step = [&](int qz, uint4 (*cur)[PL], uint4 (*nxt)[PL]) {
     if (qz + 2 < zend) load_plane(qz + 3, nxt);
-    const raw* p0 = ring + (qz & 3) * PLANE + lbase;
-    const raw* p1 = ring + ((qz + 1) & 3) * PLANE + lbase;
+    const uint4* p0 = ring + (qz & 3) * PLANE + lbase;
+    const uint4* p1 = ring + ((qz + 1) & 3) * PLANE + lbase;
 #pragma unroll
     for (int pd = 0; pd < 2; ++pd) {
-      const uint32_t* off = AHEAD ? (pd ? offB : offA) : offA;
-      const raw* rq = AHEAD ? (pd ? rqB : rqA) : rqA;
-      if (!AHEAD) skip_load(qz, pd, offA, rqA);  // (DAMVS_DECONV_SKIP_AHEAD=0) this half's records, right before use
-      else if (pd == 0) skip_load(qz, 1, offB, rqB);
-      else if (qz + 1 < zend) skip_load(qz + 1, 0, offA, rqA);
+      // this half's 8 skip records (k = (py, px, r)): bf16 requested before its MFMAs; fp32 (twice the registers, beside
+      // 27 A pairs) after them
+      uint32_t off[8];
+      uint4 rq[8][PL];
+      auto skip_load = [&]() {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int py = k >> 2, px = (k >> 1) & 1, r = k & 1;
+          const int qy = qy0 + 2 * wave + r;
+          const bool ok = lead && qy < a.Hi && qx < a.Wi;
+          const int oz = 2 * qz + pd, oy = 2 * qy + py, ox = 2 * qx + px;
+          off[k] = ok ? (uint32_t)((((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * 16 + (co & 8)) * (uint32_t)ES : kOOB;
+#pragma unroll
+          for (int h = 0; h < PL; ++h) rq[k][h] = BufIO<bf16_t>::frag(rr, off[k] == kOOB ? kOOB : off[k] + 16u * h);
+        }
+      };
+      if constexpr (PL == 1) skip_load();
       f32x4_t acc[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
@@ -1436,14 +1447,18 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
               for (int ic = 0; ic < nc; ++ic) {
                 const int zo = pd ? (ia == 0 ? 1 : 0) : 0, yo = py ? (ib == 0 ? 1 : 0) : 0;
                 const int xo = px ? (ic == 0 ? 1 : 0) : 0;
-                const raw w = ALDS ? aw[(WOFF[ph] + (ia * nb + ib) * nc + ic) * 64 + (threadIdx.x & 63)]
-                                   : wreg[ALDS ? 0 : WOFF[ph] + (ia * nb + ib) * nc + ic];
-                const raw* src = (zo ? p1 : p0) + (yo * PW + xo) * CH;
+                const int s = WOFF[ph] + (ia * nb + ib) * nc + ic;
+                frag w;
+                if constexpr (ALDS) w = aw[s * 64 + (threadIdx.x & 63)];
+                else w = wreg[s];
+                const uint4* src = (zo ? p1 : p0) + (yo * PW + xo) * (PL == 1 ? CH : S);
 #pragma unroll
                 for (int r = 0; r < 2; ++r)
-                  Frag<bf16_t>::mma(w, src[r * PW * CH], acc[(py * 2 + px) * 2 + r]);
+                  Z::mma(w, Z::bread(src + r * PW * (PL == 1 ? CH : S), PL == 1 ? 0 : g, CH, xo ? sw1 : sw0),
+                         acc[(py * 2 + px) * 2 + r]);
               }
         }
+      if constexpr (PL == 2) skip_load();
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float v[8];
@@ -1452,14 +1467,24 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
           v[i] = acc[k][i];
           v[4 + i] = __shfl_down(acc[k][i], 16);
         }
-        const uint32_t q4[4] = {rq[k].x, rq[k].y, rq[k].z, rq[k].w};
+        if constexpr (PL == 1) {
+          const uint32_t q4[4] = {rq[k][0].x, rq[k][0].y, rq[k][0].z, rq[k][0].w};
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          v[i] += b8[i];
-          if (a.relu) v[i] = fmaxf(v[i], 0.f);
-          v[i] += __uint_as_float((i & 1) ? (q4[i >> 1] & 0xffff0000u) : (q4[i >> 1] << 16));
+          for (int i = 0; i < 8; ++i) {
+            v[i] += b8[i];
+            if (a.relu) v[i] = fmaxf(v[i], 0.f);
+            v[i] += __uint_as_float((i & 1) ? (q4[i >> 1] & 0xffff0000u) : (q4[i >> 1] << 16));
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float4 f = __builtin_bit_cast(float4, rq[k][i >> 2]);
+            v[i] = v[i] * a.wscale + b8[i];  // 2^-k: exact
+            if (a.relu) v[i] = fmaxf(v[i], 0.f);
+            v[i] += (i & 3) == 0 ? f.x : (i & 3) == 1 ? f.y : (i & 3) == 2 ? f.z : f.w;
+          }
         }
-        if (lead) Vox8<bf16_t>::store(ro, off[k], v);
+        if (lead) Vox8<T>::store(ro, off[k], v);
       }
     }
     if (qz + 1 < zend) store_plane(qz + 2, cur);
@@ -1471,20 +1496,27 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
   }
 }
 
-// conv1 (Conv3d k3 s2 p1, 8 -> 16 channels, bf16) streamed along z: output plane z reads input planes
+// conv1 (Conv3d k3 s2 p1, 8 -> 16 channels) streamed along z: output plane z reads input planes
 // 2z-1 .. 2z+1, so a block keeps a 5-slot LDS ring of (2*8+1) x (2*16+1) x 8-channel input planes
 // and fetches the next two planes while it computes the current output plane. K = 27 taps x 8
 // channels in 7 chunks of 4 taps (lane group g = tap 4s + g; past tap 26 the weights are zero), the
-// 7 A fragments in registers. Same K order and weights as the gather kernel.
+// 7 A fragments in registers. bf16: same K order and weights as the gather kernel. fp32 (T = float): the split-f16
+// form on the 32-K packing (ConvArgs::wpack32), each ring row stored as its even then its odd columns (a lane's
+// stride-2 taps then read consecutive pixels: conflict-free with the hi / lo slot swizzle).
+template <typename T>
 __global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a, int tiles_x, int tiles_y, int nzc,
                                                                 int zc, int ntiles) {
-  typedef uint4 raw;
+  typedef ZForm<T> Z;
+  typedef typename Z::frag frag;
+  constexpr int PL = Z::PL, ES = sizeof(T);
   constexpr int QX = 16, QY = 8, PW = 2 * QX + 1, PH = 2 * QY + 1;
-  constexpr int PLANE = PH * PW;  // 16-byte (8-channel) pixels per halo plane
-  constexpr int NLD = (PLANE + 255) / 256;
+  constexpr int HCE = (PW + 1) / 2, PWE = PL == 1 ? PW : 2 * HCE;  // fp32: even / odd column halves of a row
+  constexpr int NPIX = PH * PW;         // 8-channel pixels per halo plane
+  constexpr int PLANE = PH * PWE * PL;  // 16-byte slots per ring plane
+  constexpr int NLD = (NPIX + 255) / 256;
   constexpr int NS = 5;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  raw* ring = reinterpret_cast<raw*>(smem);
+  uint4* ring = reinterpret_cast<uint4*>(smem);
 
   const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
   int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
@@ -1496,35 +1528,45 @@ __global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a
   const int zend = min(zb + zc, a.Do);
   const int ix0 = 2 * ox0 - 1, iy0 = 2 * oy0 - 1;
 
-  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 8 * 2);
-  auto load_plane = [&](int iz, raw* v) {
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 8 * ES);
+  auto load_plane = [&](int iz, uint4 (*v)[PL]) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int c = threadIdx.x + i * 256;
       const int row = c / PW, col = c - row * PW;
       const int iy = iy0 + row, ix = ix0 + col;
-      const bool ok = c < PLANE && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+      const bool ok = c < NPIX && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
                       (unsigned)ix < (unsigned)a.Wi;
-      const uint32_t off = (uint32_t)(((b * a.Di + iz) * a.Hi + iy) * a.Wi + ix) * 16u;
-      v[i] = BufIO<bf16_t>::frag(rin, ok ? off : kOOB);
+      const uint32_t off = (uint32_t)(((b * a.Di + iz) * a.Hi + iy) * a.Wi + ix) * (16u * PL);
+#pragma unroll
+      for (int h = 0; h < PL; ++h) v[i][h] = BufIO<bf16_t>::frag(rin, ok ? off + 16u * h : kOOB);
     }
   };
-  auto store_plane = [&](int iz, const raw* v) {
-    raw* dst = ring + ((iz + NS) % NS) * PLANE;
+  auto store_plane = [&](int iz, const uint4 (*v)[PL]) {
+    uint4* dst = ring + ((iz + NS) % NS) * PLANE;
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int c = threadIdx.x + i * 256;
-      if (c < PLANE) dst[c] = v[i];
+      if (c >= NPIX) continue;
+      if constexpr (PL == 1) {
+        dst[c] = v[i][0];
+      } else {
+        const int row = c / PW, col = c - row * PW, hp = col >> 1;
+        const int p = row * PWE + (col & 1) * HCE + hp, sw = Z::template zsw<2>(hp);
+        const F16Pair q = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+        dst[p * 2 + sw] = q.h;
+        dst[p * 2 + (1 ^ sw)] = q.l;
+      }
     }
   };
-  raw wreg[7];
+  frag wreg[7];
   {
-    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack) + (threadIdx.x & 63);
+    const uint4* __restrict__ wsrc = reinterpret_cast<const uint4*>(PL == 1 ? a.wpack : a.wpack32) + (threadIdx.x & 63);
 #pragma unroll
-    for (int s = 0; s < 7; ++s) wreg[s] = wsrc[(size_t)s * 64];
+    for (int s = 0; s < 7; ++s) wreg[s] = Z::wload(wsrc, s, 0);
   }
   {
-    raw v[NLD];
+    uint4 v[NLD][PL];
 #pragma unroll
     for (int p = -1; p <= 1; ++p) {
       load_plane(2 * zb + p, v);
@@ -1535,39 +1577,49 @@ __global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
-  const int lbase = (2 * (2 * wave) * PW + 2 * n);  // output row 2w (halo row 2*2w), column n
+  // output row 2w (halo row 2*2w), column n: bf16 the pixel slot of tap (0, 0); fp32 the row's pixel base
+  const int lbase = PL == 1 ? (2 * (2 * wave) * PW + 2 * n) : 2 * (2 * wave) * PWE;
   float bias[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) bias[i] = a.bias[g * 4 + i];
-  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * 16 * 2;
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * 16 * ES;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
   const int ox = ox0 + n;
 
   for (int z = zb; z < zend; ++z) {
     const bool more = z + 1 < zend;
-    raw na[NLD], nb[NLD];
+    uint4 na[NLD][PL], nb[NLD][PL];
     if (more) {
       load_plane(2 * z + 2, na);
       load_plane(2 * z + 3, nb);
     }
-    const raw* pl[3] = {ring + ((2 * z - 1 + NS) % NS) * PLANE, ring + ((2 * z) % NS) * PLANE,
-                        ring + ((2 * z + 1) % NS) * PLANE};
+    const uint4* pl[3] = {ring + ((2 * z - 1 + NS) % NS) * PLANE, ring + ((2 * z) % NS) * PLANE,
+                          ring + ((2 * z + 1) % NS) * PLANE};
     f32x4_t acc[2] = {(f32x4_t){0.f, 0.f, 0.f, 0.f}, (f32x4_t){0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int s = 0; s < 7; ++s) {
       const int t0 = 4 * s;
-      auto tap = [&](int t) {  // (plane, in-plane offset) of tap t (past 26: a valid pixel, zero weight)
+      // (plane, in-plane pixel offset, dx) of tap t (past 26: a valid pixel, zero weight)
+      auto tap = [&](int t) {
         const int tc = t < 27 ? t : 26;
-        return (tc / 9) * 65536 + (((tc / 3) % 3) * PW + tc % 3);
+        return (tc / 9) * 65536 + (((tc / 3) % 3) * (PL == 1 ? PW : PWE) + (PL == 1 ? tc % 3 : 0)) * 4 + tc % 3;
       };
       int code = tap(t0);
       code = g == 1 ? tap(t0 + 1) : code;
       code = g == 2 ? tap(t0 + 2) : code;
       code = g == 3 ? tap(t0 + 3) : code;
-      const int dz = code >> 16, o = code & 0xffff;
-      const raw* src = (dz == 0 ? pl[0] : dz == 1 ? pl[1] : pl[2]) + lbase + o;
+      const int dz = code >> 16, o = (code & 0xffff) >> 2, dx = code & 3;
+      const uint4* pz = dz == 0 ? pl[0] : dz == 1 ? pl[1] : pl[2];
+      if constexpr (PL == 1) {
+        const uint4* src = pz + lbase + o;
 #pragma unroll
-      for (int r = 0; r < 2; ++r) Frag<bf16_t>::mma(wreg[s], src[r * 2 * PW], acc[r]);
+        for (int r = 0; r < 2; ++r) Z::mma(wreg[s], src[r * 2 * PW], acc[r]);
+      } else {
+        // column 2n + dx: half (dx & 1), index n + (dx >> 1)
+        const int hp = n + (dx >> 1), p = lbase + o + (dx & 1) * HCE + hp, sw = Z::template zsw<2>(hp);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) Z::mma(wreg[s], Z::bread(pz + (p + r * 2 * PWE) * 2, 0, 1, sw), acc[r]);
+      }
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
@@ -1576,10 +1628,10 @@ __global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        v[i] = acc[r][i] + bias[i];
+        v[i] = (PL == 1 ? acc[r][i] : acc[r][i] * a.wscale) + bias[i];  // 2^-k: exact
         if (a.relu) v[i] = fmaxf(v[i], 0.f);
       }
-      BufIO<bf16_t>::stq(ro, ok ? (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * 16 + g * 4) * 2u : kOOB, v);
+      BufIO<T>::stq(ro, ok ? (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * 16 + g * 4) * (uint32_t)ES : kOOB, v);
     }
     if (more) {  // slots of planes 2z - 3 and 2z - 2, last read before the previous barrier
       store_plane(2 * z + 2, na);
@@ -1611,39 +1663,38 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
     hipLaunchKernelGGL(deconv_xpair_zslide_kernel<T>, dim3((unsigned)nt), dim3(256), smem, s, az, tx, ty, nzc, zc, (int)nt);
     return hipGetLastError();
   }
-  if (sizeof(T) == 2 && a.nphase == 1 && a.in_stride == 2 && a.Cin == 8 && a.Cout == 16 && a.MT == 1 && !a.resid &&
-      a.ph[0].ntaps == 27 && !deconv_zslide_disabled()) {
+  if ((sizeof(T) == 2 || a.wpack32) && a.nphase == 1 && a.in_stride == 2 && a.Cin == 8 && a.Cout == 16 && a.MT == 1 &&
+      !a.resid && a.ph[0].ntaps == 27 && !deconv_zslide_disabled()) {
     constexpr int zc = 8;
     const int tx = (a.Wo + 15) / 16, ty = (a.Ho + 7) / 8, nzc = (a.Do + zc - 1) / zc;
     const long long nt = (long long)tx * ty * nzc * a.B;
-    const size_t smem = 5 * 17 * 33 * 16;
-    hipLaunchKernelGGL(conv_s2_c8_zslide_kernel, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
+    const size_t smem = sizeof(T) == 2 ? 5 * 17 * 33 * 16 : 5 * 17 * 34 * 32;
+    auto k = conv_s2_c8_zslide_kernel<T>;
+    if (smem > 64 * 1024) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc, (int)nt);
     return hipGetLastError();
   }
-  if (sizeof(T) == 2 && !a.xpair && a.nphase == 8 && a.Cin == 32 && a.Cout == 16 && a.MT == 1 &&
+  if ((sizeof(T) == 2 || a.wpack32) && !a.xpair && a.nphase == 8 && a.Cin == 32 && a.Cout == 16 && a.MT == 1 &&
       !deconv_zslide_disabled()) {
     constexpr int zc = 8;
     const int tx = (a.Wi + 15) / 16, ty = (a.Hi + 7) / 8, nzc = (a.Di + zc - 1) / zc;
     const long long nt = (long long)tx * ty * nzc * a.B;
-    const size_t smem = 4 * 9 * 17 * 4 * 16;
-    // read per call (A/B): DAMVS_DECONV_SKIP_AHEAD=1 requests each half's skip records one half earlier (measured
-    // flat: U-Net 1.154-1.159 / 2.060-2.079 / 1.870-1.892 against 1.144-1.151 / 2.061-2.076 / 1.886-1.893 ms,
-    // profiles/r03/ab_conv9.jsonl); the A fragments sit in LDS (27 KB) instead of 108 VGPRs, two waves per SIMD
-    // instead of one: U-Net 1.136-1.149 / 2.071-2.102 / 1.879-1.884 -> 1.128-1.129 / 2.020-2.024 / 1.826-1.837 ms
-    // (same file; DAMVS_DECONV_A_LDS=0 restores the register form)
-    const char* ah = getenv("DAMVS_DECONV_SKIP_AHEAD");
-    const char* al = getenv("DAMVS_DECONV_A_LDS");
-    const bool ahead = ah && ah[0] == '1', alds = !(al && al[0] == '0');
-    const size_t sm = alds ? smem + 27 * 64 * 16 : smem;
-    if (alds) {
-      if (ahead)
-        hipLaunchKernelGGL((deconv_c16_zslide_kernel<true, true>), dim3((unsigned)nt), dim3(256), sm, s, a, tx, ty, nzc, zc, (int)nt);
-      else
-        hipLaunchKernelGGL((deconv_c16_zslide_kernel<false, true>), dim3((unsigned)nt), dim3(256), sm, s, a, tx, ty, nzc, zc, (int)nt);
-    } else if (ahead) {
-      hipLaunchKernelGGL((deconv_c16_zslide_kernel<true, false>), dim3((unsigned)nt), dim3(256), sm, s, a, tx, ty, nzc, zc, (int)nt);
+    const size_t ring = 4 * 9 * 17 * 4 * 16 * ZForm<T>::PL;
+    if constexpr (sizeof(T) == 2) {
+      // the A fragments in LDS (27 KB) instead of 108 VGPRs: two waves per SIMD instead of one, U-Net 1.136-1.149 /
+      // 2.071-2.102 / 1.879-1.884 -> 1.128-1.129 / 2.020-2.024 / 1.826-1.837 ms (profiles/r03/ab_conv9.jsonl)
+      hipLaunchKernelGGL((deconv_c16_zslide_kernel<T, true>), dim3((unsigned)nt), dim3(256), ring + 27 * 64 * 16, s, a,
+                         tx, ty, nzc, zc, (int)nt);
     } else {
-      hipLaunchKernelGGL((deconv_c16_zslide_kernel<false, false>), dim3((unsigned)nt), dim3(256), sm, s, a, tx, ty, nzc, zc, (int)nt);
+      auto k = deconv_c16_zslide_kernel<T, false>;
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)ring);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(256), ring, s, a, tx, ty, nzc, zc, (int)nt);
     }
     return hipGetLastError();
   }

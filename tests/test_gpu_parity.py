@@ -582,9 +582,8 @@ def test_costreg_bf16_deterministic(s, D, B, H, W):
 def test_conv0_zslide_matches_tile_kernel(s, D, H, W, monkeypatch):
     """The z-streaming kernels (bf16) against the kernels they replace, each on the same U-Net:
     conv0's ring-buffer row-pair kernel vs the 4x8x16-tile row-pair kernel, conv0's input-plane walk (each plane's
-    fragments read once for three output planes) vs the output-plane walk, conv9 with its skip records requested one
-    half ahead vs right before use and with its A fragments in LDS vs registers, and conv11's z-streamed
-    x-pair deconv vs the x-pair gather kernel. Same K order and accumulation chains, so the logits
+    fragments read once for three output planes) vs the output-plane walk, conv1 / conv2 / conv9 and conv11's
+    z-streamed kernels vs the gather / tile kernels. Same K order and accumulation chains, so the logits
     agree bitwise (partial tiles included)."""
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import StageEngine
@@ -596,17 +595,38 @@ def test_conv0_zslide_matches_tile_kernel(s, D, H, W, monkeypatch):
                       torch.device(DEV))
     nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats]
     vol = eng.warp_aggregate(nhwc, cuda(P), cuda(hyps))
-    for knob in ("DAMVS_CONV_NO_ZSLIDE", "DAMVS_DECONV_NO_ZSLIDE", "DAMVS_CONV0_REUSE", "DAMVS_DECONV_SKIP_AHEAD",
-                 "DAMVS_DECONV_A_LDS"):
-        on, off = ("1", "0") if knob.startswith(("DAMVS_CONV0", "DAMVS_DECONV_SKIP", "DAMVS_DECONV_A")) else ("0", "1")
-        if knob == "DAMVS_DECONV_SKIP_AHEAD":
-            on, off = off, on  # default off: compare the opt-in form against it
+    for knob in ("DAMVS_CONV_NO_ZSLIDE", "DAMVS_DECONV_NO_ZSLIDE", "DAMVS_CONV0_REUSE"):
+        on, off = ("1", "0") if knob.startswith("DAMVS_CONV0") else ("0", "1")
         monkeypatch.setenv(knob, on)
         a = eng.costreg_logits(vol).clone()
         monkeypatch.setenv(knob, off)
         b = eng.costreg_logits(vol).clone()
         monkeypatch.setenv(knob, on)
         assert torch.equal(a, b), knob
+
+
+@pytest.mark.parametrize("s,D,H,W", [(1, 24, 40, 72), (2, 8, 48, 96), (1, 32, 32, 80), (0, 48, 40, 72)])
+def test_zslide_split_kernels_vs_tile_kernels_fp32(s, D, H, W, monkeypatch):
+    """fp32 U-Net: the split-f16 z-streamed kernels (conv0 at CIN 8 / 16, conv1, conv2, conv9, conv11: 16x16x32 f16
+    MFMAs on 32-K packings) against the 16-K split-f16 tile / gather kernels (DAMVS_CONV_NO_ZSLIDE /
+    DAMVS_DECONV_NO_ZSLIDE) on the same volume, partial tiles included. Different MFMA shapes and K order: equal to
+    fp32 rounding (the U-Net golden gate is 2e-5)."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine
+    C = (32, 16, 8)[s]
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    feats, P, hyps = depthnet_inputs(B=2, N=3, H=H, W=W, D=D, stage_idx=s, C=C)
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.float32,
+                      torch.device(DEV))
+    vol = eng.warp_aggregate([cuda(f.permute(0, 2, 3, 1).contiguous()) for f in feats], cuda(P), cuda(hyps))
+    a = eng.costreg_logits(vol).clone()
+    monkeypatch.setenv("DAMVS_CONV_NO_ZSLIDE", "1")
+    monkeypatch.setenv("DAMVS_DECONV_NO_ZSLIDE", "1")
+    b = eng.costreg_logits(vol).clone()
+    err = rel_max(np_(a), np_(b))
+    print("split z-streamed vs tile kernels stage %d: rel_max %.3e" % (s, err))
+    assert err < 2e-5
 
 
 def test_forward_batch2_matches_batch1():
