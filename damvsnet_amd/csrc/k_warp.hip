@@ -24,7 +24,11 @@
 // Diagnostic variants (DIAGNOSTIC builds only, tools/diag_streams.py; the product is always 0 / 0):
 // DAMVS_DIAG_WARP_LDS_CAMS = 1 stages the cameras in LDS as round 2 first did and, with -DDAMVS_DIAG, records every
 // camera word whose LDS copy differs from the global cameras right after the barrier and again after the depth walk;
-// DAMVS_DIAG_WARP_NT = 1 writes the volume with nontemporal stores.
+// DAMVS_DIAG_WARP_NT = 1 writes the volume with nontemporal stores; DAMVS_DIAG_WARP_NT_RELEASE = 1 adds an agent-scope
+// release (buffer_wbl2 sc1: the XCD L2's dirty lines written back) at the end of every wave of the warp kernels.
+#ifndef DAMVS_DIAG_WARP_NT_RELEASE
+#define DAMVS_DIAG_WARP_NT_RELEASE 0
+#endif
 #ifndef DAMVS_DIAG_WARP_LDS_CAMS
 #define DAMVS_DIAG_WARP_LDS_CAMS 0
 #endif
@@ -409,6 +413,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
 #if DAMVS_DIAG_WARP_LDS_CAMS && defined(DAMVS_DIAG)
   diag_check_cams(s_cam, gcam, (a.N - 1) * 12, 2);
 #endif
+#if DAMVS_DIAG_WARP_NT_RELEASE
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
 }
 
 // Channel-split form (NHWC maps whose pixel is S = C * sizeof(T) / 16 chunks of 16 bytes, S = 2 or 4): S
@@ -518,7 +525,7 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
         o[e] = acc[e];
       }
     }
-    Stor<T>::store16(reinterpret_cast<T*>(a.out) + vox_of(d) * C + q * E, o);
+    store_vol<T, E>(reinterpret_cast<T*>(a.out) + vox_of(d) * C + q * E, o);
   };
   auto init = [&](float* acc, float* sq) {
 #pragma unroll
@@ -600,6 +607,9 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
     hyp_n = hyp_nn;
     finish(d, acc, sq);
   }
+#if DAMVS_DIAG_WARP_NT_RELEASE
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
 }
 
 // Lanes per voxel the launcher uses for C-channel maps: the channel-split kernel for NHWC maps of 2 or 4 16-byte chunks
