@@ -322,9 +322,10 @@ bool feat_blocked(int dtype, int C) {
     return v && v[0] == '0';
   }();
   const int bytes = C * (dtype == DAMVS_BF16 ? 2 : 4);
-  // 32- and 64-byte pixels go to the channel-split warp, which gathers the NHWC maps in place (a lane quad reads a
-  // 64-byte pixel in one instruction, where the blocked layout needs one line per 16-byte chunk)
-  if (!split_off && limit == 32 && (bytes == 32 || bytes == 64)) return false;
+  // 32-, 64- and 128-byte pixels go to the channel-split warp, which gathers the NHWC maps in place (a lane quad reads a
+  // 64-byte pixel in one instruction, where the blocked layout needs one line per 16-byte chunk); with an even view
+  // count (no view pipeline) the one-lane kernel gathers them unblocked
+  if (!split_off && limit == 32 && (bytes == 32 || bytes == 64 || bytes == 128)) return false;
   return bytes > limit;
 }
 bool feat_needs_blocking(const damvs_stage* st) { return feat_blocked(st->dtype, st->C); }

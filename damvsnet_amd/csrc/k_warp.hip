@@ -418,7 +418,8 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
 #endif
 }
 
-// Channel-split form (NHWC maps whose pixel is S = C * sizeof(T) / 16 chunks of 16 bytes, S = 2 or 4): S
+// Channel-split form (NHWC maps whose pixel is S = C * sizeof(T) / 16 chunks of 16 bytes, S = 2, 4 or 8 -- 8: the
+// fp32 path's 32-channel stage-1 maps, 128-byte pixels): S
 // consecutive lanes share one voxel, lane q owning channel chunk q. Per (voxel, view) sample each lane issues 4
 // loads (its chunk of the 4 bilinear corners) instead of 4 S, and the S lanes of a voxel read one contiguous
 // 16 S-byte pixel record per corner in the SAME instruction: one L1 tag lookup per corner per voxel where the
@@ -432,6 +433,9 @@ __device__ __forceinline__ float dpp_xor1(float v) {
 __device__ __forceinline__ float dpp_xor2(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
 }
+__device__ __forceinline__ float swz_xor4(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x101F));  // and 0x1F, xor 4 (no LDS memory)
+}
 
 template <typename T, int C, int MODE, int NVC>
 __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const float* __restrict__ cams,
@@ -439,7 +443,7 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
   constexpr int E = Stor<T>::E;  // channels per 16-byte chunk
   constexpr int S = C / E;       // lanes per voxel
   constexpr int PPB = 256 / S;   // pixels per block
-  static_assert(S == 2 || S == 4, "channel-split form: 2 or 4 chunks per pixel");
+  static_assert(S == 2 || S == 4 || S == 8, "channel-split form: 2, 4 or 8 chunks per pixel");
   static_assert(NVC % 2 == 0 || NVC < 0, "the view pipeline alternates two register sets");
   const int hw = a.h * a.w;
   const int bid = blockIdx.x;
@@ -505,7 +509,8 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
         dot += kq[e] * sq[e];
       }
       dot += dpp_xor1(dot);
-      if (S == 4) dot += dpp_xor2(dot);
+      if (S >= 4) dot += dpp_xor2(dot);
+      if (S == 8) dot += swz_xor4(dot);
       const float a1 = fmaxf(dot * a.s1 + a.t1, 0.f);
       const float wv = fmaxf(a1 * a.s2 + a.t2, 0.f) + 1.f;
 #pragma unroll
@@ -630,7 +635,7 @@ int split_lanes(const WarpArgs& a) {
     return v && v[0] == '0';
   }();
   constexpr int S = C * (int)sizeof(T) / 16;
-  if (BLK || off || warp_no_pipe() || (S != 2 && S != 4)) return 1;
+  if (BLK || off || warp_no_pipe() || (S != 2 && S != 4 && S != 8)) return 1;
   const bool pipe_ok = a.N >= 3 && (a.N - 1) % 2 == 0;
   return pipe_ok ? S : 1;
 }
@@ -642,7 +647,7 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
     const char* v = getenv("DAMVS_WARP_RUNTIME_VIEWS");
     return v && v[0] == '1';
   }();
-  if constexpr (!BLK && (C * sizeof(T) == 32 || C * sizeof(T) == 64)) {
+  if constexpr (!BLK && (C * sizeof(T) == 32 || C * sizeof(T) == 64 || C * sizeof(T) == 128)) {
     if (split_lanes<T, C, BLK>(a) > 1) {
       // DAMVS_WARP_LDS_PAD (A/B): unused dynamic LDS per block, capping the blocks per CU (fewer pixels in flight
       // per XCD, a smaller L2 working set)

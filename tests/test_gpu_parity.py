@@ -184,8 +184,8 @@ def test_prob_mfma_vs_oracle(D, h, w, with_init):
     assert np.abs(np_(conf) - ref["photometric_confidence"].numpy())[m].max() < 1e-4
 
 
-@pytest.mark.parametrize("C,dtype", [(32, torch.bfloat16), (16, torch.bfloat16), (16, torch.float32),
-                                     (8, torch.float32)])
+@pytest.mark.parametrize("C,dtype", [(32, torch.bfloat16), (16, torch.bfloat16), (32, torch.float32),
+                                     (16, torch.float32), (8, torch.float32)])
 def test_warp_aggregate_channel_blocked_layout(C, dtype):
     """The channel-blocked feature layout (used inside the stage forward) gives the NHWC result."""
     from damvsnet_amd import _capi
@@ -199,8 +199,8 @@ def test_warp_aggregate_channel_blocked_layout(C, dtype):
     nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(dtype)) for f in feats]
     a = eng.warp_aggregate(nhwc, cuda(P), cuda(hyps))
     b = eng.warp_aggregate(block_channels(nhwc), cuda(P), cuda(hyps), layout=_capi.DAMVS_LAYOUT_CBLOCK)
-    if C * nhwc[0].element_size() in (32, 64):
-        # NHWC maps of 2 / 4 chunks go to the channel-split kernel (the weight net's channel dot product summed per
+    if C * nhwc[0].element_size() in (32, 64, 128):
+        # NHWC maps of 2 / 4 / 8 chunks go to the channel-split kernel (the weight net's channel dot product summed per
         # lane chunk, then across lanes): the same voxels within the rounding of that sum -- one storage ulp
         a, b = a.float(), b.float()
         ulp = 2.0 ** -7 if dtype == torch.bfloat16 else 5e-5
