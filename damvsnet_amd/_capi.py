@@ -133,11 +133,15 @@ def load_library(path: str = LIB_PATH):
         raise RuntimeError("libdamvs ABI mismatch")
     if os.path.abspath(path) == os.path.abspath(os.path.join(_HERE, "libdamvs.so")):
         # the in-tree library must be the build of the sources beside it (A/B builds through DAMVS_LIB are exempt)
-        from .build import source_hash
+        from .build import source_hash, ARCH
         got, want = lib.damvs_build_id().decode(), source_hash()
         if got != want:
-            raise RuntimeError("libdamvs.so is stale: built from sources %s, the tree holds %s — rebuild with "
-                               "`python -m damvsnet_amd.build`" % (got, want))
+            other = [a for a in ("gfx950",) if a != ARCH and source_hash(a) == got]
+            if other:
+                raise RuntimeError("libdamvs.so was built from these sources for --offload-arch=%s, but DAMVS_ARCH=%s "
+                                   "in this environment: unset it or rebuild" % (other[0], ARCH))
+            raise RuntimeError("libdamvs.so is stale: built from sources %s, the tree holds %s (arch %s) — rebuild "
+                               "with `python -m damvsnet_amd.build`" % (got, want, ARCH))
     _lib = lib
     return lib
 

@@ -39,16 +39,20 @@ def _inputs():
     return sources() + sorted(glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h")))
 
 
-def source_hash() -> str:
+def source_hash(arch: str | None = None) -> str:
     """First 16 hex digits of sha256 over (path relative to the repo, contents) of every source and header, plus
-    the compiler flags that do not depend on where the repo lives."""
+    the compiler flags that do not depend on where the repo lives (``arch``: the offload arch to hash the flags for,
+    default DAMVS_ARCH / gfx950)."""
     h = hashlib.sha256()
     for p in _inputs():
         h.update(os.path.relpath(p, REPO).encode() + b"\0")
         with open(p, "rb") as f:
             h.update(f.read())
         h.update(b"\0")
-    h.update(" ".join(f for f in CFLAGS if not f.startswith("-I")).encode())
+    flags = [f for f in CFLAGS if not f.startswith("-I")]
+    if arch is not None:
+        flags = ["--offload-arch=" + arch if f.startswith("--offload-arch=") else f for f in flags]
+    h.update(" ".join(flags).encode())
     return h.hexdigest()[:16]
 
 
