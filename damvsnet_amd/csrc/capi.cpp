@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
@@ -72,6 +73,8 @@ struct damvs_stage {
   LayerPlan L[10];
   float* prob_w = nullptr;  // device [kd][kh][kw][c]
   void* prob_pack = nullptr;  // bf16, base 8: banded MFMA form of the prob conv (pack_prob_banded)
+  void* prob_split = nullptr;  // fp32, base 8: the same rows as split-f16 pairs (the fused head, k_head.hip)
+  float prob_scale = 1.f;      // 2^-k of prob_split
   float k1[32] = {0};
   float s1 = 0, t1 = 0, s2 = 0, t2 = 0;
 };
@@ -405,7 +408,7 @@ ConvArgs conv_args(const damvs_stage* st, int li, int B, const Shapes& S, int li
 
 // U-Net through conv11 (+conv0 skip): the prob conv input ends in c[0].
 int run_unet(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, const void* vol, char* ws,
-             const Workspace& W) {
+             const Workspace& W, int nlayers = 10) {
   const Shapes S = level_shapes(D, h, w);
   void* c[7];
   for (int i = 0; i < 7; ++i) c[i] = ws + W.c[i];
@@ -416,7 +419,8 @@ int run_unet(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, c
       {3, 1, 2, c[2], c[3], nullptr}, {4, 2, 2, c[3], c[4], nullptr}, {5, 2, 3, c[4], c[5], nullptr},
       {6, 3, 3, c[5], c[6], nullptr}, {7, 3, 2, c[6], c[4], c[4]},    {8, 2, 1, c[4], c[2], c[2]},
       {9, 1, 0, c[2], c[0], c[0]}};
-  for (const Step& k : steps) {
+  for (int i = 0; i < nlayers; ++i) {
+    const Step& k = steps[i];
     ConvArgs a = conv_args(st, k.li, B, S, k.lin, k.lout, k.in, k.out, k.res);
     DAMVS_TRY(hip_check(launch_conv3d(s, st->dtype, a), "conv3d launch"));
   }
@@ -459,6 +463,41 @@ int regress_tail(const damvs_stage* st, hipStream_t s, int B, int D, int h, int 
   DAMVS_TRY(hip_check(launch_prob_conv(s, st->dtype, B, st->base, D, h, w, feat, st->prob_w, prob_init, logits),
                       "prob conv launch"));
   return hip_check(launch_regress(s, B, D, h, w, logits, hyps, depth, conf, var, prob), "regress launch");
+}
+
+// The fused head (k_head.hip: conv11 + skip + prob conv + regression, the full-resolution U-Net output never in
+// HBM) for base 8 stages whose logit column fits LDS; DAMVS_HEAD_FUSE=0 (read per call: tests flip it) keeps the
+// separate conv11 and regress_tail launches.
+bool head_fusable(const damvs_stage* st, int D, int h, int w) {
+  const char* v = getenv("DAMVS_HEAD_FUSE");
+  if (v && v[0] == '0') return false;
+  const void* pk = st->dtype == DAMVS_BF16 ? st->prob_pack : st->prob_split;
+  if (!pk || st->base != 8 || prob_mfma_disabled()) return false;
+  if (D % 2 || h % 2 || w % 2) return false;
+  return head_smem(st->dtype, D) <= 160 * 1024;
+}
+
+// conv11 + regression: x = conv9 output (level 1), c0 = conv0 output (level 0), the skip
+int run_head(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, const void* x, const void* c0,
+             const float* hyps, const float* prob_init, float* depth, float* conf, float* var, float* prob) {
+  const Shapes S = level_shapes(D, h, w);
+  const LayerPlan& P = st->L[9];
+  HeadArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.x = x;
+  a.skip = c0;
+  a.wdec = st->dtype == DAMVS_BF16 ? P.wpack_pair : P.wpack32;
+  a.bdec = P.bias;
+  a.wscale = P.wscale;
+  a.wprob = st->dtype == DAMVS_BF16 ? st->prob_pack : st->prob_split;
+  a.pscale = st->dtype == DAMVS_BF16 ? 1.f : st->prob_scale;
+  a.prob_init = prob_init;
+  a.hyps = hyps;
+  a.depth = depth; a.conf = conf; a.var = var; a.prob = prob;
+  a.B = B; a.D = S.D[0]; a.h = S.H[0]; a.w = S.W[0];
+  a.Di = S.D[1]; a.Hi = S.H[1]; a.Wi = S.W[1];
+  if (!a.wdec) return fail(DAMVS_E_ARG, "conv11 has no x-pair packing");
+  return hip_check(launch_head(s, st->dtype, a), "head launch");
 }
 
 // U-Net layer i (conv0..conv6, conv7, conv9, conv11): (input level, output level)
@@ -615,6 +654,22 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
         }
     rc = upload(pk.data(), pk.size() * 2, &st->prob_pack);
   }
+  if (rc == DAMVS_OK && dtype == DAMVS_F32 && b == 8) {
+    // the rows of pack_prob_rows (above) with fp32 weights, split-f16 at 32 K per chunk: the fused head's fp32 form
+    std::vector<float> pf((size_t)kProbRowChunks * 64 * 8, 0.f), all(cr->prob_weight, cr->prob_weight + 27 * 8);
+    for (int k = 0; k < kProbRowChunks; ++k)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int e = 0; e < 8; ++e) {
+          const int m = lane & 15, j = m >> 2, dz = m & 3, sl = 4 * k + (lane >> 4), r = sl / 3, kx = sl % 3;
+          const int ky = r - j;
+          if (dz < 3 && sl < 18 && ky >= 0 && ky <= 2)
+            pf[((size_t)k * 64 + lane) * 8 + e] = cr->prob_weight[(size_t)e * 27 + dz * 9 + ky * 3 + kx];
+        }
+    const int kp = split_exponent(all);
+    st->prob_scale = std::ldexp(1.f, -kp);
+    const std::vector<uint16_t> hsp = split_weights_blocked(pf, kp);
+    rc = upload(hsp.data(), hsp.size() * 2, &st->prob_split);
+  }
   if (rc == DAMVS_OK && agg_mode == DAMVS_AGG_ADAPTIVE) {
     std::vector<float> sc1, sh1, sc2, sh2;
     rc = fold_bn(aw->bn1, 1, sc1, sh1);
@@ -649,6 +704,7 @@ int damvs_stage_destroy(damvs_stage* st) {
   }
   if (st->prob_w) (void)hipFree(st->prob_w);
   if (st->prob_pack) (void)hipFree(st->prob_pack);
+  if (st->prob_split) (void)hipFree(st->prob_split);
   delete st;
   return DAMVS_OK;
 }
@@ -703,6 +759,12 @@ int damvs_stage_forward_probed(const damvs_stage* st, void* stream, int B, int N
   DAMVS_TRY(mark(0));
   DAMVS_TRY(hip_check(launch_warp_aggregate(s, st->dtype, st->mode, wa, blk), "warp_aggregate launch"));
   DAMVS_TRY(mark(1));
+  if (head_fusable(st, D, h, w)) {  // conv11 inside the head kernel (mark 2 then sits before the head)
+    DAMVS_TRY(run_unet(st, s, B, D, h, w, ws + W.vol, ws, W, 9));
+    DAMVS_TRY(mark(2));
+    DAMVS_TRY(run_head(st, s, B, D, h, w, ws + W.c[2], ws + W.c[0], hyps, prob_init, depth, conf, var, prob));
+    return mark(3);
+  }
   DAMVS_TRY(run_unet(st, s, B, D, h, w, ws + W.vol, ws, W));
   DAMVS_TRY(mark(2));
   DAMVS_TRY(regress_tail(st, s, B, D, h, w, ws + W.c[0], hyps, prob_init, reinterpret_cast<float*>(ws + W.logits), depth,

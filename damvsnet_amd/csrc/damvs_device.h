@@ -96,6 +96,35 @@ template <> struct MmaFrag<bf16_t> {
   __device__ __forceinline__ static raw zero() { return make_uint4(0u, 0u, 0u, 0u); }
 };
 
+// Storage forms of the z-streamed kernels' LDS rings. bf16: a voxel of CH 8-channel chunks is CH 16-byte slots, chunk c
+// in slot c. fp32 (the split-f16 form, damvs_device.h mma_split32): 2 CH slots, the hi / lo halves of chunk c in slots
+// c and CH + c, XOR-swizzled by the voxel's column (zsw) so that 16 lanes reading one chunk of 16 consecutive voxels
+// (one MFMA B fragment) hit distinct bank groups; rows and planes shift by whole voxels and keep the swizzle.
+template <typename T> struct ZForm;
+template <> struct ZForm<bf16_t> {
+  typedef uint4 frag;
+  static constexpr int PL = 1;  // 16-byte slots (and HBM loads) per 8-channel chunk
+  template <int S> __device__ __forceinline__ static int zsw(int) { return 0; }
+  __device__ __forceinline__ static void mma(const frag& w, const frag& x, f32x4_t& acc) { MmaFrag<bf16_t>::mma(w, x, acc); }
+  // A fragment s of a [chunk][lane] packing
+  __device__ __forceinline__ static frag wload(const uint4* __restrict__ w, int s, int lane) { return w[(size_t)s * 64 + lane]; }
+  // B fragment of chunk c of the voxel at ring slot base vs (column swizzle sw)
+  __device__ __forceinline__ static frag bread(const uint4* p, int c, int CH, int sw) { (void)CH; (void)sw; return p[c]; }
+};
+template <> struct ZForm<float> {
+  typedef F16Pair frag;
+  static constexpr int PL = 2;
+  template <int S> __device__ __forceinline__ static int zsw(int col) { return (col / (16 / S)) % S; }
+  __device__ __forceinline__ static void mma(const frag& w, const frag& x, f32x4_t& acc) { mma_split32(w, x, acc); }
+  // [chunk][hi: 64 lanes][lo: 64 lanes] (split_weights_blocked)
+  __device__ __forceinline__ static frag wload(const uint4* __restrict__ w, int s, int lane) {
+    return F16Pair{w[(size_t)s * 128 + lane], w[(size_t)s * 128 + 64 + lane]};
+  }
+  __device__ __forceinline__ static frag bread(const uint4* p, int c, int CH, int sw) {
+    return F16Pair{p[c ^ sw], p[(CH + c) ^ sw]};
+  }
+};
+
 // Storage traits: E = elements per 16-byte chunk.
 template <typename T> struct Stor;
 template <> struct Stor<float> {
