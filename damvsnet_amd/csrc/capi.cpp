@@ -614,7 +614,7 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
         std::vector<float> pk;
         pack_layer_pair<float>(P, wf, E, pk, cvt_f32);
         rc = upload_split(pk, kexp, &P.wpack_pair);
-        if (rc == DAMVS_OK && P.cin <= 16) {  // conv0's z-streamed kernel (conv3d_zslide_pair<float>)
+        if (rc == DAMVS_OK) {  // conv0's z-streamed kernel (conv3d_zslide_pair<float>, CIN 8 / 16 / 32)
           std::vector<float> p32;
           pack_layer_pair<float>(P, wf, 8, p32, cvt_f32);
           const std::vector<uint16_t> h = split_weights_blocked(p32, kexp);

@@ -580,7 +580,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, 
 // the split-f16 form (ZForm<float>), the row-pair packing at 32 K per chunk (ConvArgs::wpack32).
 // Wave w owns row pair (y0 + 2w, y0 + 2w + 1); lane column n the output x = x0 + 16 xg + n.
 template <typename T, int CIN, int TXG>
-__global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : 1) void conv3d_zslide_pair_kernel(const ConvArgs a, int tiles_x, int tiles_y,
+__global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 && CIN <= 16 ? 2 : 1) void conv3d_zslide_pair_kernel(const ConvArgs a, int tiles_x, int tiles_y,
                                                                  int nzc, int zc, int ntiles) {
   typedef ZForm<T> Z;
   typedef typename Z::frag frag;
@@ -904,10 +904,11 @@ hipError_t launch_lds_pair_t(hipStream_t s, const ConvArgs& a) {
       if constexpr (CIN == 32) return launch_zslide_pair_t<T, CIN, 1>(s, a);
       else return launch_zslide_pair_t<T, CIN, 2>(s, a);
     }
-  } else if constexpr (CIN <= 16) {
-    // fp32: the split-f16 z-streamed kernel on the 32-K row-pair packing (A fragments in registers at CIN 8 / 16)
+  } else {
+    // fp32: the split-f16 z-streamed kernel on the 32-K row-pair packing, A fragments in registers (CIN 32: 36 pairs,
+    // 288 VGPRs, with the 92 KB ring one block and one wave per SIMD)
     if (!a.resid && a.wpack32 && !zslide_disabled()) {
-      if constexpr (CIN == 16) return launch_zslide_pair_t<T, CIN, 1>(s, a);  // 18 A pairs: 8 x 16 windows, no spill
+      if constexpr (CIN >= 16) return launch_zslide_pair_t<T, CIN, 1>(s, a);  // 8 x 16 windows, no spill
       else return launch_zslide_pair_t<T, CIN, 2>(s, a);
     }
   }
