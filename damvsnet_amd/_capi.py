@@ -92,6 +92,8 @@ SIGNATURES = (
                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p)),
     ("damvs_fpn_top_forward", c_int, (c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p)),
+    ("damvs_fpn_top_forward_f32", c_int, (c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                          ctypes.c_float, c_void_p, c_void_p)),
     ("damvs_conv2d_create", c_int, (ctypes.POINTER(DamvsConv2dDesc), c_void_p, c_void_p, c_int,
                                     ctypes.POINTER(c_void_p))),
     ("damvs_conv2d_destroy", c_int, (c_void_p,)),

@@ -1190,7 +1190,18 @@ int damvs_fpn_top_forward(void* stream, int B, int H, int W, const void* c0, con
   if (!c0 || !f || !apack || !bias || !out) return fail(DAMVS_E_ARG, "null argument");
   if (B < 1 || H < 2 || W < 2 || H % 2 || W % 2) return fail(DAMVS_E_SHAPE, "B %d H %d W %d (H, W even)", B, H, W);
   if ((long long)B * H * W * 16 >= (1ll << 31)) return fail(DAMVS_E_SHAPE, "operands must be smaller than 2 GiB");
-  return hip_check(launch_fpn_top(static_cast<hipStream_t>(stream), B, H, W, c0, f, apack, bias, out), "fpn_top launch");
+  return hip_check(launch_fpn_top(static_cast<hipStream_t>(stream), ST_BF16, B, H, W, c0, f, apack, 1.f, bias, out),
+                   "fpn_top launch");
+}
+
+int damvs_fpn_top_forward_f32(void* stream, int B, int H, int W, const void* c0, const void* f, const void* apack,
+                              float wscale, const float* bias, void* out) {
+  if (!c0 || !f || !apack || !bias || !out) return fail(DAMVS_E_ARG, "null argument");
+  if (B < 1 || H < 2 || W < 2 || H % 2 || W % 2) return fail(DAMVS_E_SHAPE, "B %d H %d W %d (H, W even)", B, H, W);
+  if ((long long)B * H * W * 32 >= (1ll << 31)) return fail(DAMVS_E_SHAPE, "operands must be smaller than 2 GiB");
+  if (!(wscale > 0.f)) return fail(DAMVS_E_ARG, "wscale %g", (double)wscale);
+  return hip_check(launch_fpn_top(static_cast<hipStream_t>(stream), ST_F32, B, H, W, c0, f, apack, wscale, bias, out),
+                   "fpn_top launch");
 }
 
 int damvs_conv2d_border_bias(void* stream, int dtype, int B, int H, int W, int cout_stored, int cout, const float* corr,

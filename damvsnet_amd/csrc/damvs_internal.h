@@ -146,8 +146,8 @@ bool conv2d_wide_shape_ok(const Conv2dArgs& a);  // the wide kernel takes the la
 struct BorderArgs {
   float corr[9 * 16];  // [tap][channel] of a 3x3 conv, channels < 16
 };
-hipError_t launch_fpn_top(hipStream_t s, int B, int H, int W, const void* c0, const void* f, const void* apack,
-                          const float* bias, void* out);
+hipError_t launch_fpn_top(hipStream_t s, int store, int B, int H, int W, const void* c0, const void* f,
+                          const void* apack, float wscale, const float* bias, void* out);
 hipError_t launch_border_bias(hipStream_t s, int store, const BorderArgs& a, int B, int H, int W, int cstored, int cout,
                               void* out);
 // ---------------------------------------------------------------- depth fusion (filter/dypcd.py)

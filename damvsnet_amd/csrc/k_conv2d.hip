@@ -1589,19 +1589,37 @@ __global__ __launch_bounds__(256) void border_bias_kernel(BorderArgs a, int B, i
 // and f's 6 x 66-pixel x 32-channel halo with its 16-byte chunks XOR-swizzled by (pixel >> 2) & 3; both are
 // filled by stage_chunks (8 loads in flight per lane). Per output row 3 + 6 MFMAs, the 15 A chunks in
 // registers for the whole block. Row parity py of output row y0 + j is j & 1 (y0 is a multiple of 8).
-constexpr int FT_R = 8, FT_Q = 64;
+constexpr int FT_Q = 64;
+// T = float (the fp32 parity path): the same plan on split-f16 MFMAs (damvs_device.h mma_split32). c0's halo keeps each
+// 8-channel record as its f16 hi / lo halves in two planes; f's 128-byte pixels keep chunk q's halves in slots q and
+// 4 + q, slot position s at s ^ ((pixel >> 1) & 7) (WideForm<float>); A chunks [hi: 64 lanes][lo: 64 lanes] of
+// A * 2^k, the epilogue scales by wscale = 2^-k. 4 output rows per block (59 KB of LDS: two blocks per CU).
+template <typename T> struct FpnTopForm;
+template <> struct FpnTopForm<bf16_t> {
+  static constexpr int R = 8, PL = 1, FS = 4;  // output rows per block; 16-byte pieces per chunk; slots per f pixel
+  __device__ __forceinline__ static int fslot(int fc, int q) { return q ^ ((fc >> 2) & 3); }
+};
+template <> struct FpnTopForm<float> {
+  static constexpr int R = 4, PL = 2, FS = 8;
+  __device__ __forceinline__ static int fslot(int fc, int q) { return q ^ ((fc >> 1) & 7); }
+};
 
-__global__ __launch_bounds__(256) void fpn_top_kernel(const bf16_t* __restrict__ c0, const bf16_t* __restrict__ f,
-                                                      const uint4* __restrict__ apack, const float* __restrict__ bias,
-                                                      bf16_t* __restrict__ out, int B, int H, int W, int tiles_x,
-                                                      int tiles_y, int ntiles) {
-  typedef BufIO<bf16_t> IO;
+template <typename T>
+__global__ __launch_bounds__(256) void fpn_top_kernel(const T* __restrict__ c0, const T* __restrict__ f,
+                                                      const uint4* __restrict__ apack, float wscale,
+                                                      const float* __restrict__ bias, T* __restrict__ out, int B, int H,
+                                                      int W, int tiles_x, int tiles_y, int ntiles) {
+  typedef FpnTopForm<T> Fm;
+  typedef ZForm<T> Z;
+  typedef typename Z::frag frag;
+  constexpr int FT_R = Fm::R, PL = Fm::PL, FS = Fm::FS;
+  constexpr uint32_t ES = sizeof(T);
   constexpr int CW = FT_Q + 2;                       // c0 records per (row, parity): q0-1 .. q0+64
   constexpr int C0_CHUNKS = (FT_R + 2) * 2 * CW;
   constexpr int FR = FT_R / 2 + 2, FC = FT_Q + 2;    // f halo rows x columns
-  constexpr int F_CHUNKS = FR * FC * 4;
-  __shared__ uint4 sc0[C0_CHUNKS];
-  __shared__ uint4 sf[F_CHUNKS];
+  constexpr int F_CHUNKS = FR * FC * 4;              // 8-channel chunks of the f halo
+  __shared__ uint4 sc0[C0_CHUNKS * PL];              // fp32: hi plane, then lo plane
+  __shared__ uint4 sf[FR * FC * FS];
 
   const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
   int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
@@ -1610,28 +1628,65 @@ __global__ __launch_bounds__(256) void fpn_top_kernel(const bf16_t* __restrict__
   const int b = tt / tiles_y;
   const int y0 = ty * FT_R, q0 = tx * FT_Q;
   const int Hh = H >> 1, Wh = W >> 1;
-  const __amdgpu_buffer_rsrc_t rc0 = make_rsrc(c0, (long long)B * H * W * 16);
-  const __amdgpu_buffer_rsrc_t rf = make_rsrc(f, (long long)B * Hh * Wh * 64);
+  const __amdgpu_buffer_rsrc_t rc0 = make_rsrc(c0, (long long)B * H * W * 8 * ES);
+  const __amdgpu_buffer_rsrc_t rf = make_rsrc(f, (long long)B * Hh * Wh * 32 * ES);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
 
-  uint4 af[15];
+  frag af[15];
 #pragma unroll
-  for (int c = 0; c < 15; ++c) af[c] = apack[c * 64 + lane];
+  for (int c = 0; c < 15; ++c) af[c] = Z::wload(apack, c, lane);
 
-  stage_chunks<C0_CHUNKS, 8>(sc0, [&](int c) {
+  auto c0_off = [&](int c) -> uint32_t {  // byte offset of c0 halo record c (row, x parity, q)
     const int hr = c / (2 * CW), rem = c - hr * (2 * CW), par = rem / CW, jj = rem - par * CW;
     const int y = y0 - 1 + hr, x = 2 * (q0 - 1 + jj) + par;
     const bool ok = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-    return IO::frag(rc0, ok ? (uint32_t)(((b * H + y) * W + x) * 16) : kOOB);
-  });
-  stage_chunks<F_CHUNKS, 8>(sf, [&](int c) {
-    const int p = c >> 2, fr = p / FC, fc = p - fr * FC;
-    const int chunk = (c & 3) ^ ((fc >> 2) & 3);
+    return ok ? (uint32_t)((b * H + y) * W + x) * 8u * ES : kOOB;
+  };
+  auto f_off = [&](int p, int chunk) -> uint32_t {  // byte offset of chunk `chunk` of f halo pixel p
+    const int fr = p / FC, fc = p - fr * FC;
     const int y = (y0 >> 1) - 1 + fr, x = q0 - 1 + fc;
     const bool ok = (unsigned)y < (unsigned)Hh && (unsigned)x < (unsigned)Wh;
-    return IO::frag(rf, ok ? (uint32_t)((((b * Hh + y) * Wh + x) * 4 + chunk) * 16) : kOOB);
-  });
+    return ok ? (uint32_t)(((b * Hh + y) * Wh + x) * 4 + chunk) * 8u * ES : kOOB;
+  };
+  if constexpr (PL == 1) {
+    stage_chunks<C0_CHUNKS, 8>(sc0, [&](int c) { return BufIO<bf16_t>::frag(rc0, c0_off(c)); });
+    stage_chunks<F_CHUNKS, 8>(sf, [&](int c) {
+      const int p = c >> 2, fc = p % FC;
+      return BufIO<bf16_t>::frag(rf, f_off(p, (c & 3) ^ ((fc >> 2) & 3)));
+    });
+  } else {
+    // 8-channel chunks as two 16-byte loads each, split at the LDS write; 4 chunks (8 loads) in flight per lane
+    constexpr int NC = (C0_CHUNKS + 255) / 256, NF = (F_CHUNKS + 255) / 256;
+#pragma unroll
+    for (int i0 = 0; i0 < NC + NF; i0 += 4) {
+      uint4 r[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = i0 + i, c = threadIdx.x + (k < NC ? k : k - NC) * 256;
+        const bool isc = k < NC, ok = isc ? c < C0_CHUNKS : (k < NC + NF && c < F_CHUNKS);
+        const uint32_t o = !ok ? kOOB : isc ? c0_off(c) : f_off(c >> 2, c & 3);
+        const __amdgpu_buffer_rsrc_t rr = isc ? rc0 : rf;
+        r[i][0] = BufIO<bf16_t>::frag(rr, o);
+        r[i][1] = BufIO<bf16_t>::frag(rr, o == kOOB ? kOOB : o + 16u);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = i0 + i, c = threadIdx.x + (k < NC ? k : k - NC) * 256;
+        const F16Pair v = split8(__builtin_bit_cast(float4, r[i][0]), __builtin_bit_cast(float4, r[i][1]));
+        if (k < NC) {
+          if (c < C0_CHUNKS) {
+            sc0[c] = v.h;
+            sc0[C0_CHUNKS + c] = v.l;
+          }
+        } else if (k < NC + NF && c < F_CHUNKS) {
+          const int p = c >> 2, q = c & 3, fc = p % FC;
+          sf[p * FS + Fm::fslot(fc, q)] = v.h;
+          sf[p * FS + Fm::fslot(fc, q + 4)] = v.l;
+        }
+      }
+    }
+  }
   __syncthreads();
 
   f32x4_t acc[FT_R];
@@ -1640,21 +1695,27 @@ __global__ __launch_bounds__(256) void fpn_top_kernel(const bf16_t* __restrict__
   const int qn = wave * 16 + n;
   // c0 record of lane group g (x = 2q - 1 + g): parity plane (g + 1) & 1, index q - q0 + 1 + ((g - 1) >> 1)
   const uint4* c0b = sc0 + ((g + 1) & 1) * CW + qn + 1 + ((g - 1) >> 1);
+  auto c0frag = [&](int i) -> frag {
+    if constexpr (PL == 1) return c0b[i];
+    else return F16Pair{c0b[i], c0b[C0_CHUNKS + i]};
+  };
+  auto ffrag = [&](int fr, int fc) -> frag {
+    const uint4* px = sf + (fr * FC + fc) * FS;
+    if constexpr (PL == 1) return px[Fm::fslot(fc, g)];
+    else return F16Pair{px[Fm::fslot(fc, g)], px[Fm::fslot(fc, g + 4)]};
+  };
 #pragma unroll
   for (int j = 0; j < FT_R; ++j) {
 #pragma unroll
-    for (int dy = 0; dy < 3; ++dy) Frag2<bf16_t>::mma(af[dy], c0b[(j + dy) * 2 * CW], acc[j]);
+    for (int dy = 0; dy < 3; ++dy) Z::mma(af[dy], c0frag((j + dy) * 2 * CW), acc[j]);
     const int py = j & 1;
 #pragma unroll
     for (int r2 = 0; r2 < 2; ++r2)
 #pragma unroll
-      for (int xx = 0; xx < 3; ++xx) {
-        const int fr = j / 2 + r2 + py, fc = qn + xx;
-        Frag2<bf16_t>::mma(af[3 + py * 6 + r2 * 3 + xx], sf[(fr * FC + fc) * 4 + (g ^ ((fc >> 2) & 3))], acc[j]);
-      }
+      for (int xx = 0; xx < 3; ++xx) Z::mma(af[3 + py * 6 + r2 * 3 + xx], ffrag(j / 2 + r2 + py, qn + xx), acc[j]);
   }
 
-  const __amdgpu_buffer_rsrc_t ro = make_rsrc(out, (long long)B * H * W * 16);
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(out, (long long)B * H * W * 8 * ES);
   const int px = g >> 1, cb = (g & 1) * 4;
   float bs[4];
 #pragma unroll
@@ -1665,21 +1726,27 @@ __global__ __launch_bounds__(256) void fpn_top_kernel(const bf16_t* __restrict__
     const int y = y0 + j;
     float r[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = acc[j][i] + bs[i];
+    for (int i = 0; i < 4; ++i) r[i] = (PL == 1 ? acc[j][i] : acc[j][i] * wscale) + bs[i];  // 2^-k: exact
     const bool ok = y < H && x < W;
-    IO::stq(ro, ok ? (uint32_t)((((b * H + y) * W + x) * 8 + cb) * 2) : kOOB, r);
+    BufIO<T>::stq(ro, ok ? (uint32_t)(((b * H + y) * W + x) * 8 + cb) * ES : kOOB, r);
   }
 }
 
 }  // namespace
 
-hipError_t launch_fpn_top(hipStream_t s, int B, int H, int W, const void* c0, const void* f, const void* apack,
-                          const float* bias, void* out) {
-  const int tx = (W / 2 + FT_Q - 1) / FT_Q, ty = (H + FT_R - 1) / FT_R;
+hipError_t launch_fpn_top(hipStream_t s, int store, int B, int H, int W, const void* c0, const void* f,
+                          const void* apack, float wscale, const float* bias, void* out) {
+  const int R = store == ST_BF16 ? FpnTopForm<bf16_t>::R : FpnTopForm<float>::R;
+  const int tx = (W / 2 + FT_Q - 1) / FT_Q, ty = (H + R - 1) / R;
   const long long nt = (long long)tx * ty * B;
-  hipLaunchKernelGGL(fpn_top_kernel, dim3((unsigned)nt), dim3(256), 0, s, static_cast<const bf16_t*>(c0),
-                     static_cast<const bf16_t*>(f), static_cast<const uint4*>(apack), bias, static_cast<bf16_t*>(out),
-                     B, H, W, tx, ty, (int)nt);
+  if (store == ST_BF16)
+    hipLaunchKernelGGL(fpn_top_kernel<bf16_t>, dim3((unsigned)nt), dim3(256), 0, s, static_cast<const bf16_t*>(c0),
+                       static_cast<const bf16_t*>(f), static_cast<const uint4*>(apack), 1.f, bias,
+                       static_cast<bf16_t*>(out), B, H, W, tx, ty, (int)nt);
+  else
+    hipLaunchKernelGGL(fpn_top_kernel<float>, dim3((unsigned)nt), dim3(256), 0, s, static_cast<const float*>(c0),
+                       static_cast<const float*>(f), static_cast<const uint4*>(apack), wscale, bias,
+                       static_cast<float*>(out), B, H, W, tx, ty, (int)nt);
   return hipGetLastError();
 }
 

@@ -13,6 +13,7 @@ SparseDownSampleClose geometry.py:443-455.
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 
 import torch
@@ -144,13 +145,20 @@ def fpn_top_layers(inner2, out3, dtype):
             (up.weight.data.clone(), c0.weight.data.clone(), c0.bias.data.clone()))
 
 
-def pack_fpn_top(wt, wc):
-    """MFMA A chunks of damvs_fpn_top_forward (15 x 64 lanes x 8 bf16): lane (g = lane >> 4, row = lane & 15)
-    holds A[row][8g .. 8g+7], row = (output x parity px = row >> 3, channel co = row & 7).
-      chunks 0-2  (3x3 conv, kernel row dy): k = (x-pair tap g: c0 column 2q-1+g, channel) -> Wc[co][ci][dy][g-px];
-      chunks 3-14 (ConvTranspose k4 s2 p1, row parity py, input row m-1+rr with rr = r2+py, column q-1+xx):
-                  k = channel 8g+e -> Wt[ci][co][ky][kx], ky = py+3-2rr, kx = px+3-2xx (zero outside 0..3).
-    wt: (32, 8, 4, 4), wc: (8, 8, 3, 3) fp32."""
+def pack_fpn_top_split(wt, wc):
+    """damvs_fpn_top_forward_f32's A chunks: pack_fpn_top's 15 x 64 x 8 values in fp32, scaled by 2^k (largest |A| in
+    (2^13, 2^14]) and split into f16 halves hi = f16(v), lo = f16(v - hi); laid out [chunk][hi / lo][64 lanes][8].
+    Returns (int16 view of the halves, wscale = 2^-k)."""
+    A = _fpn_top_A(wt, wc)
+    mx = float(A.abs().max())
+    k = 0 if mx == 0.0 else 14 - math.frexp(mx)[1]
+    v = A * (2.0 ** k)
+    hi = v.half()
+    lo = (v - hi.float()).half()
+    return torch.stack([hi, lo], 1).contiguous().view(torch.int16), 2.0 ** -k
+
+
+def _fpn_top_A(wt, wc):
     A = torch.zeros(15, 64, 8, dtype=torch.float32)
     for lane in range(64):
         g, row = lane >> 4, lane & 15
@@ -166,7 +174,17 @@ def pack_fpn_top(wt, wc):
                     kx = px + 3 - 2 * xx
                     if 0 <= kx <= 3:
                         A[3 + py * 6 + r2 * 3 + xx, lane] = wt[8 * g:8 * g + 8, co, ky, kx]
-    return A.to(torch.bfloat16)
+    return A
+
+
+def pack_fpn_top(wt, wc):
+    """MFMA A chunks of damvs_fpn_top_forward (15 x 64 lanes x 8 bf16): lane (g = lane >> 4, row = lane & 15)
+    holds A[row][8g .. 8g+7], row = (output x parity px = row >> 3, channel co = row & 7).
+      chunks 0-2  (3x3 conv, kernel row dy): k = (x-pair tap g: c0 column 2q-1+g, channel) -> Wc[co][ci][dy][g-px];
+      chunks 3-14 (ConvTranspose k4 s2 p1, row parity py, input row m-1+rr with rr = r2+py, column q-1+xx):
+                  k = channel 8g+e -> Wt[ci][co][ky][kx], ky = py+3-2rr, kx = px+3-2xx (zero outside 0..3).
+    wt: (32, 8, 4, 4), wc: (8, 8, 3, 3) fp32."""
+    return _fpn_top_A(wt, wc).to(torch.bfloat16)
 
 
 class HipFeatureNet:
@@ -185,11 +203,16 @@ class HipFeatureNet:
             self.out2 = L(fnet.out2, False, c0=fnet.out2.in_channels)
             if self.num_stage == 3:
                 self.top_up, self.top_c0, self.top_corr, (wt, wc, bc) = fpn_top_layers(fnet.inner2, fnet.out3, dtype)
-                # one fused launch (damvs_fpn_top_forward) for bf16; DAMVS_FPN_TOP_FUSED=0 keeps the two layers
+                # one fused launch (damvs_fpn_top_forward, fp32: _f32 on split-f16 MFMAs); DAMVS_FPN_TOP_FUSED=0
+                # keeps the two layers
                 self.top_fused = None
-                if dtype == torch.bfloat16 and wt.shape[0] == 32 and wt.shape[1] == 8 and wc.shape[1] == 8 and \
+                if wt.shape[0] == 32 and wt.shape[1] == 8 and wc.shape[1] == 8 and \
                         os.environ.get("DAMVS_FPN_TOP_FUSED", "1") != "0":
-                    self.top_fused = (pack_fpn_top(wt, wc), bc.float())
+                    if dtype == torch.bfloat16:
+                        self.top_fused = (pack_fpn_top(wt, wc), bc.float(), None)
+                    elif dtype == torch.float32:
+                        ap, ws = pack_fpn_top_split(wt, wc)
+                        self.top_fused = (ap, bc.float(), ws)
         else:
             self.up = []
             for fu in [fnet.deconv1] + ([fnet.deconv2] if self.num_stage == 3 else []):
@@ -230,12 +253,16 @@ class HipFeatureNet:
                 # out3(up2(f) + inner2(c0)) without the 32-channel full-resolution sum (fpn_top_layers)
                 lib = self.top_c0._lib
                 if self.top_fused is not None and h == 2 * f.shape[1] and w == 2 * f.shape[2]:
-                    ap, bc = self.top_fused
+                    ap, bc, ws = self.top_fused
                     if ap.device != c0.device:
-                        self.top_fused = ap, bc = ap.to(c0.device), bc.to(c0.device)
+                        self.top_fused = ap, bc, ws = ap.to(c0.device), bc.to(c0.device), ws
                     o3 = torch.empty(B, h, w, 8, device=c0.device, dtype=c0.dtype)
-                    check(lib.damvs_fpn_top_forward(_capi.stream_ptr(c0.device), B, h, w, ptr(c0), ptr(f), ptr(ap),
-                                                    ptr(bc), ptr(o3)))
+                    if ws is None:
+                        check(lib.damvs_fpn_top_forward(_capi.stream_ptr(c0.device), B, h, w, ptr(c0), ptr(f), ptr(ap),
+                                                        ptr(bc), ptr(o3)))
+                    else:
+                        check(lib.damvs_fpn_top_forward_f32(_capi.stream_ptr(c0.device), B, h, w, ptr(c0), ptr(f),
+                                                            ptr(ap), ws, ptr(bc), ptr(o3)))
                 else:
                     t = self.top_up(B, f.shape[1], f.shape[2], f)
                     o3 = self.top_c0(B, h, w, c0, res_pre=t)

@@ -242,6 +242,12 @@ int damvs_conv2d_border_bias(void* stream, int dtype, int B, int H, int W, int c
 int damvs_fpn_top_forward(void* stream, int B, int H, int W, const void* c0, const void* f, const void* apack,
                           const float* bias, void* out);
 
+/* The same in fp32 storage (the fp32 parity path): c0, f, out fp32; the products as split-f16 MFMAs. apack: the
+ * 15 A chunks scaled by 2^k (max |A| in (2^13, 2^14]) as f16 halves, [chunk][hi: 64 lanes x 8][lo: 64 lanes x 8]
+ * (frontend_hip.pack_fpn_top_split); wscale = 2^-k. */
+int damvs_fpn_top_forward_f32(void* stream, int B, int H, int W, const void* c0, const void* f, const void* apack,
+                              float wscale, const float* bias, void* out);
+
 /* ------------------------------------------------------------------ depth fusion (f4)
  * One reference view of the reference's dynamic-consistency fusion (filter/dypcd.py:98-297,
  * filter_depth per ref view): all maps [H][W] fp32 device buffers of one resolution. Camera
