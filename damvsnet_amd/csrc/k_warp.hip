@@ -100,6 +100,18 @@ template <> struct Rec16<bf16_t> {
 // batch element's map (rec bytes per record) and their weights. A corner outside the map gets the offset
 // kOOB, so its buffer load returns 0: grid_sample's zero padding without a weight select. Samples far
 // outside (or NaN) are moved to (-4, -4), where all four corners are outside.
+// Spelled-out multiply-adds shared by the warp kernels: with contraction left to the compiler, a*b + c*d + e may
+// fuse as fma(a, b, c*d) in one kernel and fma(c, d, a*b) in another, and the kernels that must agree bit for bit
+// (warp_split / warp_sweep) differed in the last bit of a coordinate. Every product-sum on the sampling path goes
+// through these.
+__device__ __forceinline__ float ray3(float m0, float m1, float m2, float fx, float fy) {
+  return fmaf(m0, fx, fmaf(m1, fy, m2));
+}
+__device__ __forceinline__ float src_coord(float q, float iz, float k) { return fmaf(q * iz, k, -0.5f); }
+__device__ __forceinline__ float bilerp(float v0, float v1, float v2, float v3, const float* wt) {
+  return fmaf(v3, wt[3], fmaf(v2, wt[2], fmaf(v1, wt[1], v0 * wt[0])));
+}
+
 struct Taps {
   uint32_t off[4];
   float wt[4];
@@ -234,13 +246,13 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
       for (int k = 0; k < 4; ++k) Rec16<T>::unpack(rv[q * 4 + k], v[k]);
       float s[E];
 #pragma unroll
-      for (int e = 0; e < E; ++e) s[e] = ((v[0][e] * wt[0] + v[1][e] * wt[1]) + v[2][e] * wt[2]) + v[3][e] * wt[3];
+      for (int e = 0; e < E; ++e) s[e] = bilerp(v[0][e], v[1][e], v[2][e], v[3][e], wt);
       if (MODE == AGG_WARP_ONLY) {
 #pragma unroll
         for (int e = 0; e < E; ++e) acc[q * E + e] = s[e];
       } else if (MODE == AGG_VARIANCE) {
 #pragma unroll
-        for (int e = 0; e < E; ++e) { acc[q * E + e] += s[e]; sq[q * E + e] += s[e] * s[e]; }
+        for (int e = 0; e < E; ++e) { acc[q * E + e] += s[e]; sq[q * E + e] = fmaf(s[e], s[e], sq[q * E + e]); }
       } else {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
@@ -252,11 +264,11 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
     if (MODE == AGG_ADAPTIVE) {
       float dot = 0.f;
 #pragma unroll
-      for (int c = 0; c < C; ++c) dot += a.k1[c] * sq[c];
-      const float a1 = fmaxf(dot * a.s1 + a.t1, 0.f);
-      const float wv = fmaxf(a1 * a.s2 + a.t2, 0.f) + 1.f;
+      for (int c = 0; c < C; ++c) dot = fmaf(a.k1[c], sq[c], dot);
+      const float a1 = fmaxf(fmaf(dot, a.s1, a.t1), 0.f);
+      const float wv = fmaxf(fmaf(a1, a.s2, a.t2), 0.f) + 1.f;
 #pragma unroll
-      for (int c = 0; c < C; ++c) acc[c] += wv * sq[c];
+      for (int c = 0; c < C; ++c) acc[c] = fmaf(wv, sq[c], acc[c]);
     }
   };
   auto finish = [&](int d, float* acc, float* sq) {
@@ -297,9 +309,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
 #pragma unroll
       for (int v = 0; v < NVC; ++v) {
         const float* m = cam + v * 12;
-        rx[v] = m[0] * fx + m[1] * fy + m[2];
-        ry[v] = m[3] * fx + m[4] * fy + m[5];
-        rz[v] = m[6] * fx + m[7] * fy + m[8];
+        rx[v] = ray3(m[0], m[1], m[2], fx, fy);
+        ry[v] = ray3(m[3], m[4], m[5], fx, fy);
+        rz[v] = ray3(m[6], m[7], m[8], fx, fy);
         tx[v] = m[9];
         ty[v] = m[10];
         tz[v] = m[11];
@@ -311,7 +323,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
 #pragma unroll
       for (int v = 0; v < NVC; ++v) {
         const float* g = gcam + v * 12;
-        const float e[6] = {g[0] * fx + g[1] * fy + g[2], g[3] * fx + g[4] * fy + g[5], g[6] * fx + g[7] * fy + g[8],
+        const float e[6] = {ray3(g[0], g[1], g[2], fx, fy), ray3(g[3], g[4], g[5], fx, fy), ray3(g[6], g[7], g[8], fx, fy),
                             g[9], g[10], g[11]};
         const float h[6] = {rx[v], ry[v], rz[v], tx[v], ty[v], tz[v]};
 #pragma unroll
@@ -324,18 +336,18 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
     auto taps = [&](int v, float hyp) {
       float qx, qy, qz;
       if constexpr (NVC > 0) {
-        qx = rx[v] * hyp + tx[v], qy = ry[v] * hyp + ty[v], qz = rz[v] * hyp + tz[v];
+        qx = fmaf(rx[v], hyp, tx[v]), qy = fmaf(ry[v], hyp, ty[v]), qz = fmaf(rz[v], hyp, tz[v]);
       } else {
         const float* m = cam + v * 12;
-        const float vx = m[0] * fx + m[1] * fy + m[2];
-        const float vy = m[3] * fx + m[4] * fy + m[5];
-        const float vz = m[6] * fx + m[7] * fy + m[8];
-        qx = vx * hyp + m[9], qy = vy * hyp + m[10], qz = vz * hyp + m[11];
+        const float vx = ray3(m[0], m[1], m[2], fx, fy);
+        const float vy = ray3(m[3], m[4], m[5], fx, fy);
+        const float vz = ray3(m[6], m[7], m[8], fx, fy);
+        qx = fmaf(vx, hyp, m[9]), qy = fmaf(vy, hyp, m[10]), qz = fmaf(vz, hyp, m[11]);
       }
       // g = (q/qz) / ((W-1)/2) - 1 and ix = ((g + 1) W - 1) / 2 fold to ix = (q/qz) W/(W-1) - 1/2:
       // one reciprocal instead of four IEEE divisions (coordinates agree to ~1 ulp)
       const float iz = __builtin_amdgcn_rcpf(qz);
-      return bilinear_taps(a.h, a.w, rec, qx * iz * kx - 0.5f, qy * iz * ky - 0.5f);
+      return bilinear_taps(a.h, a.w, rec, src_coord(qx, iz, kx), src_coord(qy, iz, ky));
     };
     auto issue = [&](int v, const Taps& t, uint4* rv, float* wt) {
       __amdgpu_buffer_rsrc_t r;
@@ -392,12 +404,12 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
       init(acc, sq);
       for (int j = 1; j < nviews; ++j) {
         const float* m = cam + (j - 1) * 12;
-        const float rx = m[0] * fx + m[1] * fy + m[2];
-        const float ry = m[3] * fx + m[4] * fy + m[5];
-        const float rz = m[6] * fx + m[7] * fy + m[8];
-        const float qx = rx * hyp + m[9], qy = ry * hyp + m[10], qz = rz * hyp + m[11];
+        const float rx = ray3(m[0], m[1], m[2], fx, fy);
+        const float ry = ray3(m[3], m[4], m[5], fx, fy);
+        const float rz = ray3(m[6], m[7], m[8], fx, fy);
+        const float qx = fmaf(rx, hyp, m[9]), qy = fmaf(ry, hyp, m[10]), qz = fmaf(rz, hyp, m[11]);
         const float iz = __builtin_amdgcn_rcpf(qz);
-        const Taps t = bilinear_taps(a.h, a.w, rec, qx * iz * kx - 0.5f, qy * iz * ky - 0.5f);
+        const Taps t = bilinear_taps(a.h, a.w, rec, src_coord(qx, iz, kx), src_coord(qy, iz, ky));
         const __amdgpu_buffer_rsrc_t r = make_rsrc(a.feats[j], fbytes);
         uint4 rv[4 * NQ];
 #pragma unroll
@@ -493,28 +505,28 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
     for (int k = 0; k < 4; ++k) Rec16<T>::unpack(rv[k], v[k]);
     float s[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) s[e] = ((v[0][e] * wt[0] + v[1][e] * wt[1]) + v[2][e] * wt[2]) + v[3][e] * wt[3];
+    for (int e = 0; e < E; ++e) s[e] = bilerp(v[0][e], v[1][e], v[2][e], v[3][e], wt);
     if (MODE == AGG_WARP_ONLY) {
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[e] = s[e];
     } else if (MODE == AGG_VARIANCE) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) { acc[e] += s[e]; sq[e] += s[e] * s[e]; }
+      for (int e = 0; e < E; ++e) { acc[e] += s[e]; sq[e] = fmaf(s[e], s[e], sq[e]); }
     } else {
       float dot = 0.f;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const float df = ref[e] - s[e];
         sq[e] = df * df;
-        dot += kq[e] * sq[e];
+        dot = fmaf(kq[e], sq[e], dot);
       }
       dot += dpp_xor1(dot);
       if (S >= 4) dot += dpp_xor2(dot);
       if (S == 8) dot += swz_xor4(dot);
-      const float a1 = fmaxf(dot * a.s1 + a.t1, 0.f);
-      const float wv = fmaxf(a1 * a.s2 + a.t2, 0.f) + 1.f;
+      const float a1 = fmaxf(fmaf(dot, a.s1, a.t1), 0.f);
+      const float wv = fmaxf(fmaf(a1, a.s2, a.t2), 0.f) + 1.f;
 #pragma unroll
-      for (int e = 0; e < E; ++e) acc[e] += wv * sq[e];
+      for (int e = 0; e < E; ++e) acc[e] = fmaf(wv, sq[e], acc[e]);
     }
   };
   auto finish = [&](int d, float* acc, float* sq) {
@@ -548,9 +560,9 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
 #pragma unroll
     for (int v = 0; v < NVC; ++v) {
       const float* m = cam + v * 12;
-      rx[v] = m[0] * fx + m[1] * fy + m[2];
-      ry[v] = m[3] * fx + m[4] * fy + m[5];
-      rz[v] = m[6] * fx + m[7] * fy + m[8];
+      rx[v] = ray3(m[0], m[1], m[2], fx, fy);
+      ry[v] = ray3(m[3], m[4], m[5], fx, fy);
+      rz[v] = ray3(m[6], m[7], m[8], fx, fy);
       tx[v] = m[9];
       ty[v] = m[10];
       tz[v] = m[11];
@@ -560,16 +572,16 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
   auto taps = [&](int v, float hyp) {
     float qx, qy, qz;
     if constexpr (NVC > 0) {
-      qx = rx[v] * hyp + tx[v], qy = ry[v] * hyp + ty[v], qz = rz[v] * hyp + tz[v];
+      qx = fmaf(rx[v], hyp, tx[v]), qy = fmaf(ry[v], hyp, ty[v]), qz = fmaf(rz[v], hyp, tz[v]);
     } else {
       const float* m = cam + v * 12;
-      const float vx = m[0] * fx + m[1] * fy + m[2];
-      const float vy = m[3] * fx + m[4] * fy + m[5];
-      const float vz = m[6] * fx + m[7] * fy + m[8];
-      qx = vx * hyp + m[9], qy = vy * hyp + m[10], qz = vz * hyp + m[11];
+      const float vx = ray3(m[0], m[1], m[2], fx, fy);
+      const float vy = ray3(m[3], m[4], m[5], fx, fy);
+      const float vz = ray3(m[6], m[7], m[8], fx, fy);
+      qx = fmaf(vx, hyp, m[9]), qy = fmaf(vy, hyp, m[10]), qz = fmaf(vz, hyp, m[11]);
     }
     const float iz = __builtin_amdgcn_rcpf(qz);
-    return bilinear_taps(a.h, a.w, rec, qx * iz * kx - 0.5f, qy * iz * ky - 0.5f);
+    return bilinear_taps(a.h, a.w, rec, src_coord(qx, iz, kx), src_coord(qy, iz, ky));
   };
   auto issue = [&](int v, const Taps& t, uint4* rv, float* wt) {
     __amdgpu_buffer_rsrc_t r;
@@ -768,28 +780,28 @@ __global__ __launch_bounds__(256) void warp_sweep_kernel(const WarpArgs a, const
     for (int c4 = 0; c4 < 4; ++c4) Rec16<T>::unpack(rv[c4], v4[c4]);
     float s[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) s[e] = ((v4[0][e] * wt[0] + v4[1][e] * wt[1]) + v4[2][e] * wt[2]) + v4[3][e] * wt[3];
+    for (int e = 0; e < E; ++e) s[e] = bilerp(v4[0][e], v4[1][e], v4[2][e], v4[3][e], wt);
     if (MODE == AGG_WARP_ONLY) {
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[k][e] = s[e];
     } else if (MODE == AGG_VARIANCE) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) { acc[k][e] += s[e]; sq[k][e] += s[e] * s[e]; }
+      for (int e = 0; e < E; ++e) { acc[k][e] += s[e]; sq[k][e] = fmaf(s[e], s[e], sq[k][e]); }
     } else {
       float dot = 0.f, t[E];
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const float df = ref[e] - s[e];
         t[e] = df * df;
-        dot += kq[e] * t[e];
+        dot = fmaf(kq[e], t[e], dot);
       }
       dot += dpp_xor1(dot);
       if (S >= 4) dot += dpp_xor2(dot);
       if (S == 8) dot += swz_xor4(dot);
-      const float a1 = fmaxf(dot * a.s1 + a.t1, 0.f);
-      const float wv = fmaxf(a1 * a.s2 + a.t2, 0.f) + 1.f;
+      const float a1 = fmaxf(fmaf(dot, a.s1, a.t1), 0.f);
+      const float wv = fmaxf(fmaf(a1, a.s2, a.t2), 0.f) + 1.f;
 #pragma unroll
-      for (int e = 0; e < E; ++e) acc[k][e] += wv * t[e];
+      for (int e = 0; e < E; ++e) acc[k][e] = fmaf(wv, t[e], acc[k][e]);
     }
   };
 
@@ -819,15 +831,15 @@ __global__ __launch_bounds__(256) void warp_sweep_kernel(const WarpArgs a, const
       fload(nxt, (j + 1) - c1 * nv);
     }
     const float* m = cam + v * 12;
-    const float rxv = m[0] * fx + m[1] * fy + m[2], ryv = m[3] * fx + m[4] * fy + m[5], rzv = m[6] * fx + m[7] * fy + m[8];
+    const float rxv = ray3(m[0], m[1], m[2], fx, fy), ryv = ray3(m[3], m[4], m[5], fx, fy), rzv = ray3(m[6], m[7], m[8], fx, fy);
     if (cur.fits) {
       const uint4* fb = fbuf + (j & 1) * FPX * S + q;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const float hyp = hk[k];
-        const float qx = rxv * hyp + m[9], qy = ryv * hyp + m[10], qz = rzv * hyp + m[11];
+        const float qx = fmaf(rxv, hyp, m[9]), qy = fmaf(ryv, hyp, m[10]), qz = fmaf(rzv, hyp, m[11]);
         const float iz = __builtin_amdgcn_rcpf(qz);
-        const float ix = qx * iz * kx - 0.5f, iy = qy * iz * ky - 0.5f;
+        const float ix = src_coord(qx, iz, kx), iy = src_coord(qy, iz, ky);
         // bilinear_taps' arithmetic, corners read from the footprint (outside the image: 0)
         const bool inside = ix > -2.f && ix < (float)a.w + 1.f && iy > -2.f && iy < (float)a.h + 1.f;
         const float cx = inside ? ix : -4.f, cy = inside ? iy : -4.f;
@@ -854,9 +866,9 @@ __global__ __launch_bounds__(256) void warp_sweep_kernel(const WarpArgs a, const
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const float hyp = hk[k];
-        const float qx = rxv * hyp + m[9], qy = ryv * hyp + m[10], qz = rzv * hyp + m[11];
+        const float qx = fmaf(rxv, hyp, m[9]), qy = fmaf(ryv, hyp, m[10]), qz = fmaf(rzv, hyp, m[11]);
         const float iz = __builtin_amdgcn_rcpf(qz);
-        const Taps tp = bilinear_taps(a.h, a.w, rec, qx * iz * kx - 0.5f, qy * iz * ky - 0.5f);
+        const Taps tp = bilinear_taps(a.h, a.w, rec, src_coord(qx, iz, kx), src_coord(qy, iz, ky));
         uint4 rv[4];
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4)
