@@ -22,6 +22,7 @@
 // fp32 (T = float): the split-f16 form of both convs (damvs_device.h mma_split32): the feature tile keeps each fp32
 // voxel as its f16 hi / lo halves, the prob weights are split on the host (2^k scaled, pscale = 2^-k).
 #include <cstdlib>
+#include <type_traits>
 
 #include "damvs_device.h"
 
@@ -34,6 +35,7 @@ constexpr int kHFY = kHTY + 2, kHFX = 34;  // feature tile: rows y0-1 .. y0+8, c
 constexpr int kHFV = kHFY * kHFX;          // 340 voxels
 constexpr int kHQY = 6, kHQX = 17;         // conv9-output tile per q-plane: q-rows qy0 .. qy0+5, q-cols qx0 .. qx0+16
 constexpr int kHPix = 256;                 // logit column stride (8 rows x 32 columns; columns 30, 31 unused)
+template <int V> using IC = std::integral_constant<int, V>;
 
 template <typename T> struct HeadForm;
 template <> struct HeadForm<bf16_t> {
@@ -150,8 +152,8 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(2) void head_kernel(const HeadArgs
   const long long nskip = (long long)a.B * D * h * w * 8 * ES;
   const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.skip, nskip);
   // the five outputs of this lane (unit u: q-row, phase), their feature-tile slot (or -1) and skip offset
-  auto out_geom = [&](int p, int u, uint32_t& off) -> int {
-    const int r = u < 4 ? wave : 4, ph = u < 4 ? u : wave, pd = ph >> 1, py = ph & 1;
+  auto out_geom = [&](int p, int r, int ph, uint32_t& off) -> int {
+    const int pd = ph >> 1, py = ph & 1;
     const int oz = 2 * p + pd, oy = 2 * (qy0 + r) + py, ox = 2 * (qx0 + n) + (g >> 1);
     const bool in = lead && oz < D && (unsigned)oy < (unsigned)h && (unsigned)ox < (unsigned)w;
     off = in ? (uint32_t)((((b * D + oz) * h + oy) * w + ox) * 8) * (uint32_t)ES : kOOB;
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(2) void head_kernel(const HeadArgs
 #pragma unroll
     for (int u = 0; u < 5; ++u) {
       uint32_t off;
-      (void)out_geom(p, u, off);
+      (void)out_geom(p, u < 4 ? wave : 4, u < 4 ? u : wave, off);
 #pragma unroll
       for (int hh = 0; hh < PL; ++hh) rq[u][hh] = BufIO<bf16_t>::frag(rs, off == kOOB ? kOOB : off + 16u * hh);
     }
@@ -229,10 +231,12 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(2) void head_kernel(const HeadArgs
     const uint4* r0 = ring + (p % 3) * RPLANE + lofs;        // q-plane p (z offset 0)
     const uint4* r1 = ring + ((p + 1) % 3) * RPLANE + lofs;  // q-plane p + 1 (z offset +1)
     // conv11: 5 units of one (q-row, phase) each, the epilogue straight into the feature tile
-    auto unit = [&](int u, int r, int ph) __attribute__((always_inline)) {
-      const int pd = ph >> 1, py = ph & 1;
-      const int na = pd ? 2 : 1, nb = py ? 2 : 1;
-      const int w0 = ph == 0 ? 0 : ph == 1 ? 1 : ph == 2 ? 3 : 5;
+    // unit u (compile-time: the skip record slot) = q-row r, phase PH (compile-time: the A fragment indices)
+    auto unit = [&](auto phc, auto uc, int r) {
+      constexpr int ph = decltype(phc)::value, u = decltype(uc)::value;
+      constexpr int pd = ph >> 1, py = ph & 1;
+      constexpr int na = pd ? 2 : 1, nb = py ? 2 : 1;
+      constexpr int w0 = ph == 0 ? 0 : ph == 1 ? 1 : ph == 2 ? 3 : 5;
       f32x4_t acc = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ca = 0; ca < na; ++ca)
@@ -249,7 +253,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(2) void head_kernel(const HeadArgs
         v[4 + i] = __shfl_down(acc[i], 16);
       }
       uint32_t off;
-      const int slot = out_geom(p, u, off);
+      const int slot = out_geom(p, r, ph, off);
       if constexpr (PL == 1) {
         const uint32_t q4[4] = {rq[u][0].x, rq[u][0].y, rq[u][0].z, rq[u][0].w};
 #pragma unroll
@@ -284,13 +288,15 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(2) void head_kernel(const HeadArgs
         }
       }
     };
-#pragma unroll
-    for (int u = 0; u < 4; ++u) unit(u, wave, u);
+    unit(IC<0>{}, IC<0>{}, wave);
+    unit(IC<1>{}, IC<1>{}, wave);
+    unit(IC<2>{}, IC<2>{}, wave);
+    unit(IC<3>{}, IC<3>{}, wave);
     switch (wave) {  // q-row 4: phase = wave (a wave-uniform branch, each case with a constant phase)
-      case 0: unit(4, 4, 0); break;
-      case 1: unit(4, 4, 1); break;
-      case 2: unit(4, 4, 2); break;
-      default: unit(4, 4, 3); break;
+      case 0: unit(IC<0>{}, IC<4>{}, 4); break;
+      case 1: unit(IC<1>{}, IC<4>{}, 4); break;
+      case 2: unit(IC<2>{}, IC<4>{}, 4); break;
+      default: unit(IC<3>{}, IC<4>{}, 4); break;
     }
     if (p + 1 < Di) load_skip(p + 1);
     // ring: q-plane p + 2 into the slot of p - 1 (last read before the previous barrier), fetch p + 3

@@ -1061,8 +1061,16 @@ __global__ __launch_bounds__(256) void block_channels_kernel(const FeatPtrs src,
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= hw) return;
   const int v = blockIdx.y / B, b = blockIdx.y - v * B;
-  const uint4* sp = reinterpret_cast<const uint4*>(src.p[v]) + ((size_t)b * hw + p) * NQ;
-  uint4* dp = const_cast<uint4*>(reinterpret_cast<const uint4*>(dst.p[v])) + (size_t)b * NQ * hw + p;
+  // the view's pointers by a select chain (indexing the by-value pointer arrays with v would copy them to scratch)
+  const void* sv = src.p[0];
+  const void* dv = dst.p[0];
+#pragma unroll
+  for (int i = 1; i < kMaxViews; ++i) {
+    sv = v == i ? src.p[i] : sv;
+    dv = v == i ? dst.p[i] : dv;
+  }
+  const uint4* sp = reinterpret_cast<const uint4*>(sv) + ((size_t)b * hw + p) * NQ;
+  uint4* dp = const_cast<uint4*>(reinterpret_cast<const uint4*>(dv)) + (size_t)b * NQ * hw + p;
   uint4 r[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) r[q] = sp[q];
