@@ -38,8 +38,11 @@ constexpr int kHPix = 256;                 // logit column stride (8 rows x 32 c
 template <int V> using IC = std::integral_constant<int, V>;
 
 template <typename T> struct HeadForm;
+#ifndef DAMVS_HEAD_NFB
+#define DAMVS_HEAD_NFB 2  // (A/B builds: 1 = one feature tile and two barriers per q-plane for bf16 too)
+#endif
 template <> struct HeadForm<bf16_t> {
-  static constexpr int NFB = 2;    // feature tile buffers (double: one barrier per q-plane)
+  static constexpr int NFB = DAMVS_HEAD_NFB;  // feature tile buffers (double: one barrier per q-plane)
   static constexpr bool ALDS = false;  // conv11 A fragments in registers
   static constexpr int PCH = kProbRowChunks * kProbRowTerms;  // prob A fragments (uint4) per lane
 };
@@ -51,7 +54,7 @@ template <> struct HeadForm<float> {
 
 size_t head_smem_t(int store, int D) {
   const bool bf = store == ST_BF16;
-  const int PL = bf ? 1 : 2, NFB = bf ? 2 : 1;
+  const int PL = bf ? 1 : 2, NFB = bf ? DAMVS_HEAD_NFB : 1;
   size_t b = 3 * (size_t)kHQY * kHQX * 2 * PL * 16;  // input ring
   b += (size_t)NFB * 2 * kHFV * PL * 16;              // feature tiles (2 planes each)
   if (!bf) b += 9 * 128 * 16;                         // conv11 A fragments (fp32)
