@@ -477,6 +477,10 @@ bool head_fusable(const damvs_stage* st, int D, int h, int w) {
   return head_smem(st->dtype, D) <= 160 * 1024;
 }
 
+#ifdef DAMVS_DIAG
+float* g_head_diag = nullptr;  // diagnostic builds: damvs_head_diag_set
+#endif
+
 // conv11 + regression: x = conv9 output (level 1), c0 = conv0 output (level 0), the skip
 int run_head(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, const void* x, const void* c0,
              const float* hyps, const float* prob_init, float* depth, float* conf, float* var, float* prob) {
@@ -496,6 +500,9 @@ int run_head(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, c
   a.depth = depth; a.conf = conf; a.var = var; a.prob = prob;
   a.B = B; a.D = S.D[0]; a.h = S.H[0]; a.w = S.W[0];
   a.Di = S.D[1]; a.Hi = S.H[1]; a.Wi = S.W[1];
+#ifdef DAMVS_DIAG
+  a.diag = g_head_diag;
+#endif
   if (!a.wdec) return fail(DAMVS_E_ARG, "conv11 has no x-pair packing");
   return hip_check(launch_head(s, st->dtype, a), "head launch");
 }
@@ -508,6 +515,11 @@ constexpr int kLayerLevels[10][2] = {{0, 0}, {0, 1}, {1, 1}, {1, 2}, {2, 2}, {2,
 extern "C" {
 
 int damvs_abi_version(void) { return DAMVS_ABI_VERSION; }
+
+#ifdef DAMVS_DIAG
+// diagnostic builds only: the fused head also writes its conv11 + skip outputs (fp32) to p ([B][D][h][w][8])
+void damvs_head_diag_set(float* p) { g_head_diag = p; }
+#endif
 
 #ifndef DAMVS_BUILD_ID
 #define DAMVS_BUILD_ID "unstamped"

@@ -207,6 +207,7 @@ struct HeadArgs {
   const float* hyps;
   float *depth, *conf, *var, *prob;
   int B, D, h, w, Di, Hi, Wi;
+  float* diag;  // diagnostic builds: conv11 + skip outputs (fp32, [B][D][h][w][8], tile interiors), else nullptr
 };
 size_t head_smem(int store, int D);
 hipError_t launch_head(hipStream_t s, int store, const HeadArgs& a);

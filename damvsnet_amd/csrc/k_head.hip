@@ -274,6 +274,14 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(2) void head_kernel(const HeadArgs
           v[i] += (i & 3) == 0 ? f.x : (i & 3) == 1 ? f.y : (i & 3) == 2 ? f.z : f.w;
         }
       }
+      if (a.diag && slot >= 0 && off != kOOB) {
+        const int tr = 2 * r + py, tc = 2 * n + (g >> 1);
+        if (tr >= 1 && tr <= kHTY && tc >= 1 && tc <= kHTX) {
+          float* dd = a.diag + (size_t)off / ES;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) dd[i] = v[i];
+        }
+      }
       if (slot >= 0) {
         if (off == kOOB) {  // outside the image: the prob conv's zero padding
 #pragma unroll

@@ -1,0 +1,59 @@
+"""Fused head: its conv11 + skip feature (diagnostic build, -DDAMVS_DIAG, damvs_head_diag_set) against the unfused
+conv11 output (layer by layer through damvs_costreg_layer), twice, on a failing shape. GPU diagnostic, not a test.
+  DAMVS_LIB=damvsnet_amd/ab/libdamvs_diag.so python tools/diag_head_feat.py"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from common import model_state, depthnet_inputs  # noqa: E402
+
+
+def main(s=2, D=8, B=1, H=48, W=96):
+    from damvsnet_amd import _capi
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine
+    lib = _capi.load_library()
+    lib.damvs_head_diag_set.argtypes = [ctypes.c_void_p]
+    C = (32, 16, 8)[s]
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    feats, P, hyps = depthnet_inputs(B=B, N=3, H=H, W=W, D=D, stage_idx=s, C=C)
+    dt = torch.bfloat16
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", dt, torch.device("cuda"))
+    nhwc = [f.permute(0, 2, 3, 1).contiguous().to(dt).cuda() for f in feats]
+    P, hyps = P.cuda(), hyps.cuda()
+    vol = eng.warp_aggregate(nhwc, P, hyps)
+    bufs = eng.unet_buffers(B, D, H, W)
+    src = [vol, 0, 1, 2, 3, 4, 5, 6, 4, 2]
+    dst = [0, 1, 2, 3, 4, 5, 6, 4, 2, 0]
+    for layer in range(10):
+        inp = vol if layer == 0 else bufs[src[layer]]
+        eng.unet_layer(layer, D, H, W, inp, bufs[dst[layer]])
+    ref = bufs[0].float().cpu().numpy()  # conv0 + conv11, bf16
+    os.environ["DAMVS_HEAD_FUSE"] = "1"
+    feats_f = []
+    for _ in range(2):
+        dg = torch.zeros(B, D, H, W, 8, device="cuda")
+        lib.damvs_head_diag_set(dg.data_ptr())
+        eng.forward(nhwc, P, hyps)
+        torch.cuda.synchronize()
+        lib.damvs_head_diag_set(None)
+        feats_f.append(dg.to(dt).float().cpu().numpy())
+    for i, f in enumerate(feats_f):
+        d = np.abs(f - ref).max(-1)
+        bad = np.argwhere(d > 0)
+        print("run %d: feature vs unfused conv11: %d / %d voxels differ, max %.3g" % (i, len(bad), d.size, d.max()))
+        if len(bad):
+            print("   d:", np.bincount(bad[:, 1], minlength=D).tolist(), " y", bad[:, 2].min(), bad[:, 2].max(), " x",
+                  bad[:, 3].min(), bad[:, 3].max())
+            print("   first:", bad[:5].tolist())
+    print("run 0 vs run 1: %d voxels differ" % int((np.abs(feats_f[0] - feats_f[1]).max(-1) > 0).sum()))
+
+
+if __name__ == "__main__":
+    main()
