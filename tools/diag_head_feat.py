@@ -31,9 +31,12 @@ def main(s=2, D=8, B=1, H=48, W=96):
     bufs = eng.unet_buffers(B, D, H, W)
     src = [vol, 0, 1, 2, 3, 4, 5, 6, 4, 2]
     dst = [0, 1, 2, 3, 4, 5, 6, 4, 2, 0]
+    saved = {}
     for layer in range(10):
         inp = vol if layer == 0 else bufs[src[layer]]
         eng.unet_layer(layer, D, H, W, inp, bufs[dst[layer]])
+        if layer in (0, 8):
+            saved[layer] = bufs[dst[layer]].float().cpu().numpy()  # conv0 output, conv9 output
     ref = bufs[0].float().cpu().numpy()  # conv0 + conv11, bf16
     os.environ["DAMVS_HEAD_FUSE"] = "1"
     feats_f = []
@@ -53,6 +56,23 @@ def main(s=2, D=8, B=1, H=48, W=96):
                   bad[:, 3].min(), bad[:, 3].max())
             print("   first:", bad[:5].tolist())
     print("run 0 vs run 1: %d voxels differ" % int((np.abs(feats_f[0] - feats_f[1]).max(-1) > 0).sum()))
+    # the forward's workspace after the fused forward: c0 (conv0 output, the skip) and c2 (conv9 output, the input)
+    al = lambda x: (x + 255) // 256 * 256
+    V, es, N = B * D * H * W, 2, 3
+    o = al(B * (N - 1) * 12 * 4) + al(V * C * es)  # rt, vol (8-channel / 16-byte pixels are not blocked)
+    sz = [V * 8, V // 8 * 16, V // 8 * 16]
+    offs = []
+    for i in range(3):
+        offs.append(o)
+        o += al(sz[i] * es)
+    ws = eng.workspace(B, N, D, H, W)
+    c0 = ws[offs[0]:offs[0] + sz[0] * 2].view(dt).float().cpu().numpy().reshape(B, D, H, W, 8)
+    c2 = ws[offs[2]:offs[2] + sz[2] * 2].view(dt).float().cpu().numpy().reshape(B, D // 2, H // 2, W // 2, 16)
+    for name, got, want in (("c0 (skip)", c0, saved[0]), ("c2 (conv9 out)", c2, saved[8])):
+        d = np.abs(got - want).max(-1)
+        bad = np.argwhere(d > 0)
+        print("workspace %s vs layer path: %d / %d differ" % (name, len(bad), d.size),
+              ("x %d..%d" % (bad[:, 3].min(), bad[:, 3].max())) if len(bad) else "")
 
 
 if __name__ == "__main__":
