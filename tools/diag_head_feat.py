@@ -66,13 +66,27 @@ def main(s=2, D=8, B=1, H=48, W=96):
         offs.append(o)
         o += al(sz[i] * es)
     ws = eng.workspace(B, N, D, H, W)
-    c0 = ws[offs[0]:offs[0] + sz[0] * 2].view(dt).float().cpu().numpy().reshape(B, D, H, W, 8)
-    c2 = ws[offs[2]:offs[2] + sz[2] * 2].view(dt).float().cpu().numpy().reshape(B, D // 2, H // 2, W // 2, 16)
-    for name, got, want in (("c0 (skip)", c0, saved[0]), ("c2 (conv9 out)", c2, saved[8])):
-        d = np.abs(got - want).max(-1)
-        bad = np.argwhere(d > 0)
-        print("workspace %s vs layer path: %d / %d differ" % (name, len(bad), d.size),
-              ("x %d..%d" % (bad[:, 3].min(), bad[:, 3].max())) if len(bad) else "")
+
+    def check(tag):
+        c0 = ws[offs[0]:offs[0] + sz[0] * 2].view(dt).float().cpu().numpy().reshape(B, D, H, W, 8)
+        c2 = ws[offs[2]:offs[2] + sz[2] * 2].view(dt).float().cpu().numpy().reshape(B, D // 2, H // 2, W // 2, 16)
+        for name, got, want in (("c0", c0, saved[0] if tag == "fused" else ref), ("c2 (conv9 out)", c2, saved[8])):
+            d = np.abs(got - want).max(-1)
+            bad = np.argwhere(d > 0)
+            print("%s forward: workspace %s vs layer path: %d / %d differ" % (tag, name, len(bad), d.size),
+                  ("x %d..%d y %d..%d" % (bad[:, 3].min(), bad[:, 3].max(), bad[:, 2].min(), bad[:, 2].max()))
+                  if len(bad) else "", flush=True)
+
+    check("fused")
+    os.environ["DAMVS_HEAD_FUSE"] = "0"
+    eng.forward(nhwc, P, hyps)
+    torch.cuda.synchronize()
+    check("unfused")
+    os.environ["DAMVS_HEAD_FUSE"] = "1"
+    # the U-Net alone on the forward's own volume (damvs_costreg_logits: all ten layers, then the prob conv)
+    eng.costreg_logits(vol)
+    torch.cuda.synchronize()
+    check("costreg_logits")
 
 
 if __name__ == "__main__":
