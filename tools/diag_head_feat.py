@@ -35,8 +35,7 @@ def main(s=2, D=8, B=1, H=48, W=96):
     for layer in range(10):
         inp = vol if layer == 0 else bufs[src[layer]]
         eng.unet_layer(layer, D, H, W, inp, bufs[dst[layer]])
-        if layer in (0, 8):
-            saved[layer] = bufs[dst[layer]].float().cpu().numpy()  # conv0 output, conv9 output
+        saved[layer] = bufs[dst[layer]].float().cpu().numpy()  # every layer's output as written
     ref = bufs[0].float().cpu().numpy()  # conv0 + conv11, bf16
     os.environ["DAMVS_HEAD_FUSE"] = "1"
     feats_f = []
@@ -87,6 +86,18 @@ def main(s=2, D=8, B=1, H=48, W=96):
     eng.costreg_logits(vol)
     torch.cuda.synchronize()
     check("costreg_logits")
+    # every level of the workspace after costreg_logits against the layer that wrote it last
+    Ls = [(0, 9, 8, 0), (1, 1, 16, 1), (2, 8, 16, 1), (3, 3, 32, 2), (4, 7, 32, 2), (5, 5, 64, 3), (6, 6, 64, 3)]
+    szs = [V * 8, V // 8 * 16, V // 8 * 16, V // 64 * 32, V // 64 * 32, V // 512 * 64, V // 512 * 64]
+    o = al(B * (N - 1) * 12 * 4) + al(V * C * es)
+    for ci, li, ch, lev in Ls:
+        off = o + sum(al(szs[j] * es) for j in range(ci))
+        got = ws[off:off + szs[ci] * 2].view(dt).float().cpu().numpy().reshape(B, D >> lev, H >> lev, W >> lev, ch)
+        d = np.abs(got - saved[li]).max(-1)
+        bad = np.argwhere(d > 0)
+        print("c%d (layer %d out, level %d): %d / %d differ" % (ci, li, lev, len(bad), d.size),
+              ("z %d..%d y %d..%d x %d..%d" % (bad[:, 1].min(), bad[:, 1].max(), bad[:, 2].min(), bad[:, 2].max(),
+                                             bad[:, 3].min(), bad[:, 3].max())) if len(bad) else "", flush=True)
 
 
 if __name__ == "__main__":
