@@ -32,7 +32,7 @@ def carve(B, D, H, W, dt, guard_bytes):
     return raw, out
 
 
-def main(s=2, D=8, B=1, H=48, W=96):
+def main(s=2, D=8, B=1, H=48, W=96, chained=False):
     from damvsnet_amd import _capi
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import StageEngine
@@ -50,6 +50,8 @@ def main(s=2, D=8, B=1, H=48, W=96):
     for layer in range(10):
         # identical inputs: copy the separate path's current input / in-place output into both carved sets
         for _, bufs in keep:
+            if chained:
+                break
             if layer > 0:
                 bufs[SRC[layer]].copy_(sep[SRC[layer]])
             if layer >= 7:
@@ -69,4 +71,7 @@ def main(s=2, D=8, B=1, H=48, W=96):
 
 
 if __name__ == "__main__":
+    print("-- inputs copied from the separate path before every layer")
     main()
+    print("-- chained: each carved set runs the whole U-Net on its own outputs")
+    main(chained=True)
