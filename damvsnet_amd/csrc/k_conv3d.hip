@@ -1049,8 +1049,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : 1) void conv_
       for (int r = 0; r < 2; ++r)
 #pragma unroll
         for (int xg = 0; xg < TXG; ++xg)
-          Z::mma(wreg[s], Z::bread(src + r * PW * (PL == 1 ? CH : S) + 16 * xg * (PL == 1 ? CH : S), gc, CH, sw),
-                 acc[r][xg]);
+          Z::mma(wreg[s],
+                 Z::bread(src + r * PW * (PL == 1 ? CH : S) + 16 * xg * (PL == 1 ? CH : S), PL == 1 ? 0 : gc, CH, sw),
+                 acc[r][xg]);  // bf16: lbase already holds the lane's chunk
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r)
