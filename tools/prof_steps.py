@@ -1,6 +1,6 @@
 """Per-kernel time inside the timed bench steps from a rocprofv3 kernel trace (csv).
 
-Steps are delimited by the regression kernels (one prob_regress / prob_mfma launch per stage, 3 per
+Steps are delimited by the regression kernels (one prob_regress / prob_mfma / head launch per stage, 3 per
 forward). Also prints the average of the last `roofline_iters` launches of the roofline kernel
 (bench.py's warp_roofline loop runs last), to check against the bench line's roofline.ms_per_launch."""
 import collections
@@ -13,7 +13,7 @@ ROOFLINE_KERNEL = "warp_split_kernel<unsigned short, 16,"  # stage 2 (C = 16), b
 
 def main(path, warmup=2, steps=5, top=40, roofline_iters=20):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    reg = [i for i, r in enumerate(rows) if "regress_kernel" in r["Kernel_Name"] or "prob_mfma_kernel" in r["Kernel_Name"]]
+    reg = [i for i, r in enumerate(rows) if any(k in r["Kernel_Name"] for k in ("regress_kernel", "prob_mfma_kernel", "head_kernel"))]
     ends = reg[2::3]  # last regress of each forward
     first = ends[warmup - 1] + 1
     last = ends[warmup + steps - 1]
