@@ -162,12 +162,13 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(2) void head_kernel(const HeadArgs
     off = in ? (uint32_t)((((b * D + oz) * h + oy) * w + ox) * 8) * (uint32_t)ES : kOOB;
     return lead ? pd * FPLANE + (2 * r + py) * kHFX + 2 * n + (g >> 1) : -1;
   };
-  uint4 rq[5][PL];
-  auto load_skip = [&](int p) {
+  // skip records of q-plane p's five outputs into rq (past the last plane: out-of-range loads, no traffic)
+  auto load_skip = [&](int p, uint4 (&rq)[5][PL]) {
 #pragma unroll
     for (int u = 0; u < 5; ++u) {
       uint32_t off;
       (void)out_geom(p, u < 4 ? wave : 4, u < 4 ? u : wave, off);
+      if (p >= Di) off = kOOB;
 #pragma unroll
       for (int hh = 0; hh < PL; ++hh) rq[u][hh] = BufIO<bf16_t>::frag(rs, off == kOOB ? kOOB : off + 16u * hh);
     }
@@ -184,15 +185,21 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(2) void head_kernel(const HeadArgs
   }
   const bool bpad = g >= 2;
 
-  // ---- prologue: q-planes 0, 1 into the ring, 2 into registers; zero the feature tiles (columns 32, 33 stay zero)
-  uint4 pa[PL];
+  // ---- prologue: q-planes 0, 1 into the ring, 2 and 3 into the two register sets, the skip records of q-planes 0
+  // and 1, all requested together; zero the feature tiles (columns 32, 33 stay zero). From here on every global
+  // load has two q-plane steps of cover: step p consumes the skip records and stores the ring plane requested at
+  // step p - 2 (the per-step work is short: one exposed memory latency per step bound the first form).
+  uint4 pa[PL], pb[PL];
+  uint4 rqa[5][PL], rqb[5][PL];
   load_plane(0, pa);
-  store_plane(0, pa);
-  load_plane(1, pa);
-  store_plane(1, pa);
-  load_plane(2, pa);
+  load_plane(1, pb);
+  load_skip(0, rqa);
+  load_skip(1, rqb);
   for (int i = tid; i < NFB * 2 * FPLANE; i += 256) ftile[i] = make_uint4(0u, 0u, 0u, 0u);
-  load_skip(0);
+  store_plane(0, pa);
+  store_plane(1, pb);
+  load_plane(2, pa);
+  load_plane(3, pb);
   __syncthreads();
 
   float am1 = 0.f, a0 = 0.f;
@@ -229,7 +236,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(2) void head_kernel(const HeadArgs
     a0 = sum[0];
   };
 
-  for (int p = 0; p < Di; ++p) {
+  auto step = [&](int p, uint4 (&rq)[5][PL], uint4 (&pl)[PL]) {
     uint4* ft = ftile + (p % NFB) * 2 * FPLANE;
     const uint4* r0 = ring + (p % 3) * RPLANE + lofs;        // q-plane p (z offset 0)
     const uint4* r1 = ring + ((p + 1) % 3) * RPLANE + lofs;  // q-plane p + 1 (z offset +1)
@@ -309,14 +316,19 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(2) void head_kernel(const HeadArgs
       case 2: unit(IC<2>{}, IC<4>{}, 4); break;
       default: unit(IC<3>{}, IC<4>{}, 4); break;
     }
-    if (p + 1 < Di) load_skip(p + 1);
-    // ring: q-plane p + 2 into the slot of p - 1 (last read before the previous barrier), fetch p + 3
-    store_plane(p + 2, pa);
-    load_plane(p + 3, pa);
+    load_skip(p + 2, rq);
+    // ring: q-plane p + 2 (requested at step p - 2) into the slot of p - 1 (last read before the previous barrier),
+    // then request p + 4 into the same registers
+    store_plane(p + 2, pl);
+    load_plane(p + 4, pl);
     __syncthreads();
     prob_plane(ft, 2 * p);
     prob_plane(ft + FPLANE, 2 * p + 1);
     if constexpr (NFB == 1) __syncthreads();
+  };
+  for (int p = 0; p < Di; p += 2) {  // unrolled by two: the register sets alternate statically
+    step(p, rqa, pa);
+    if (p + 1 < Di) step(p + 1, rqb, pb);
   }
   float last = am1;  // plane D - 1
 
