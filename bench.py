@@ -430,6 +430,11 @@ def main():
         if world > 1:
             torch.distributed.barrier()
 
+    pp = None
+    # DAMVS_BENCH_PARITY_FIRST=1 (A/B of the in-process order): the parity path before the headline steps
+    parity_first = os.environ.get("DAMVS_BENCH_PARITY_FIRST", "0") == "1"
+    if parity_first and dtype == torch.bfloat16 and not args.no_parity_path:
+        pp = parity_path(args, nd, device, imgs, proj, dv, ins, world)
     with torch.no_grad():
         for _ in range(args.warmup):
             net(imgs, proj, dv, ins, streams=args.streams)
@@ -455,8 +460,7 @@ def main():
     from damvsnet_amd.dist import max_over_ranks
     elapsed = max_over_ranks(elapsed, device=device)
     maps = args.steps * args.batch * world
-    pp = None
-    if dtype == torch.bfloat16 and not args.no_parity_path:  # every rank takes part (max over ranks)
+    if not parity_first and dtype == torch.bfloat16 and not args.no_parity_path:  # every rank takes part (max over ranks)
         pp = parity_path(args, nd, device, imgs, proj, dv, ins, world)
     phases = {k: round(statistics.mean(v), 3) for k, v in timer.per_phase_ms().items()}
 
