@@ -41,6 +41,8 @@ class RefineNet(nn.Module):
         self.res = ConvBNReLU2d(32, 1, 3, 1, 1)
 
 
+_SIDE_STREAMS = {}  # device index -> sub-batch streams shared by all models (CascadeMVSNet._side_streams)
+
 class CascadeMVSNet(nn.Module):
     def __init__(self, refine=False, ndepths=[64, 32, 8], depth_interals_ratio=[4, 2, 1], share_cr=False,
                  grad_method="detach", arch_mode="fpn", cr_base_chs=[8, 8, 8], agg_mode="adaptive",
@@ -110,9 +112,15 @@ class CascadeMVSNet(nn.Module):
         return [{k: v.reshape(B, N, *v.shape[1:])[:, i] for k, v in f.items()} for i in range(N)]
 
     def _side_streams(self, n, device):
-        pool = getattr(self, "_streams", None)
-        if pool is None or len(pool) < n or pool[0].device != device:
-            pool = self._streams = [torch.cuda.Stream(device) for _ in range(n)]
+        """The sub-batch streams, one process-wide set per device shared by every model: torch.cuda.Stream() hands out
+        the next stream of PyTorch's pool, and HIP places streams on its hardware queues in creation order, so a second
+        model with streams of its own could land a sub-batch on the main stream's queue (measured: whichever of the
+        bf16 and fp32 models ran second in one bench process lost 10-14 %, the fp32 parity path 78 against 86 maps/s)."""
+        key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+        pool = _SIDE_STREAMS.get(key)
+        if pool is None or len(pool) < n:
+            pool = (pool or []) + [torch.cuda.Stream(device) for _ in range(n - len(pool or []))]
+            _SIDE_STREAMS[key] = pool
         return pool[:n]
 
     def _forward_streams(self, imgs, proj_matrices, depth_values, intrinsics_matrices, nstreams):

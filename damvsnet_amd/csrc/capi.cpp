@@ -466,11 +466,12 @@ int regress_tail(const damvs_stage* st, hipStream_t s, int B, int D, int h, int 
 }
 
 // The fused head (k_head.hip: conv11 + skip + prob conv + regression, the full-resolution U-Net output never in
-// HBM) for base 8 stages whose logit column fits LDS; DAMVS_HEAD_FUSE=0 (read per call: tests flip it) keeps the
-// separate conv11 and regress_tail launches.
+// HBM) for base 8 stages whose logit column fits LDS, with DAMVS_HEAD_FUSE=1 (read per call: tests flip it). Off by
+// default: measured slower than conv11's z-streamed kernel + prob_mfma / prob_regress (cfgC B=4: bf16 196.6 against
+// 202.7 maps/s, fp32 86.2 against 87.7; profiles/r04/ab_head_r04h.jsonl).
 bool head_fusable(const damvs_stage* st, int D, int h, int w) {
   const char* v = getenv("DAMVS_HEAD_FUSE");
-  if (v && v[0] == '0') return false;
+  if (!(v && v[0] == '1')) return false;
   const void* pk = st->dtype == DAMVS_BF16 ? st->prob_pack : st->prob_split;
   if (!pk || st->base != 8 || prob_mfma_disabled()) return false;
   if (D % 2 || h % 2 || w % 2) return false;
