@@ -451,9 +451,11 @@ WarpArgs warp_args(const damvs_stage* st, int B, int N, int C, int D, int h, int
 // (models/cas_mvsnet.py:105-124) on the U-Net output c0 [B][D][h][w][base].
 int regress_tail(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, const void* feat, const float* hyps,
                  const float* prob_init, float* logits, float* depth, float* conf, float* var, float* prob) {
-  // bf16, base 8: the prob conv on MFMA (logits in an LDS column, as the VALU kernel below)
-  if (st->prob_pack && prob_mfma_smem(D) <= 160 * 1024 && !prob_mfma_disabled())
-    return hip_check(launch_prob_mfma(s, B, D, h, w, feat, st->prob_pack, prob_init, hyps, depth, conf, var, prob),
+  // base 8: the prob conv on MFMA (logits in an LDS column, as the VALU kernel below); fp32 as split-f16 MFMAs
+  const void* pk = st->dtype == DAMVS_BF16 ? st->prob_pack : st->prob_split;
+  if (pk && prob_mfma_smem(st->dtype, D) <= 160 * 1024 && !prob_mfma_disabled())
+    return hip_check(launch_prob_mfma(s, st->dtype, B, D, h, w, feat, pk, st->dtype == DAMVS_BF16 ? 1.f : st->prob_scale,
+                                      prob_init, hyps, depth, conf, var, prob),
                      "prob_mfma launch");
   if (prob_regress_smem_bytes(st->dtype, st->base, D) <= 160 * 1024)  // fused: logits stay in LDS
     return hip_check(launch_prob_regress(s, st->dtype, B, st->base, D, h, w, feat, st->prob_w, prob_init, hyps, depth,
@@ -473,7 +475,7 @@ bool head_fusable(const damvs_stage* st, int D, int h, int w) {
   const char* v = getenv("DAMVS_HEAD_FUSE");
   if (!(v && v[0] == '1')) return false;
   const void* pk = st->dtype == DAMVS_BF16 ? st->prob_pack : st->prob_split;
-  if (!pk || st->base != 8 || prob_mfma_disabled()) return false;
+  if (!pk || st->base != 8 || prob_mfma_disabled()) return false;  // (pk: the head's prob A operand)
   if (D % 2 || h % 2 || w % 2) return false;
   return head_smem(st->dtype, D) <= 160 * 1024;
 }

@@ -184,10 +184,11 @@ size_t prob_regress_smem_bytes(int store, int Cb, int D);
 #define DAMVS_PROB_TERMS 2  // bf16 terms per fp32 prob-conv weight (3: exact fp32 weights; A/B builds)
 #endif
 constexpr int kProbRowChunks = 5, kProbRowTerms = DAMVS_PROB_TERMS;  // prob_mfma_kernel: 18 voxel slots x 8 channels
-hipError_t launch_prob_mfma(hipStream_t s, int B, int D, int h, int w, const void* feat, const void* apack,
-                            const float* prob_init, const float* hyps, float* depth, float* conf, float* var,
-                            float* prob);
-size_t prob_mfma_smem(int D);
+// store ST_F32: the split-f16 form (apack = damvs_stage prob_split, pscale its 2^-k)
+hipError_t launch_prob_mfma(hipStream_t s, int store, int B, int D, int h, int w, const void* feat, const void* apack,
+                            float pscale, const float* prob_init, const float* hyps, float* depth, float* conf,
+                            float* var, float* prob);
+size_t prob_mfma_smem(int store, int D);
 bool prob_mfma_disabled();  // DAMVS_PROB_MFMA=0 (A/B testing)
 hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float* logits, const float* hyps,
                           float* depth, float* conf, float* var, float* prob);

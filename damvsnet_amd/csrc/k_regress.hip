@@ -300,28 +300,40 @@ constexpr int kPRVox = kHY * kHX;  // 340 staged voxels per plane
 #endif
 constexpr int kPRAhead = DAMVS_PROB_AHEAD;  // input planes in flight per block
 
-__global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int w, const bf16_t* __restrict__ feat,
-                                                        const uint4* __restrict__ apack,
+// T = float (the fp32 path): the same plan on split-f16 MFMAs (damvs_device.h mma_split32): each staged fp32 voxel
+// (32 bytes, two loads) is split into its f16 hi / lo halves at the LDS write (two planes of 340 slots), the weights
+// are the rows above split on the host (2^k scaled, pscale = 2^-k; damvs_stage prob_split), three MFMAs per chunk.
+template <typename T>
+__global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int w, const T* __restrict__ feat,
+                                                        const uint4* __restrict__ apack, float pscale,
                                                         const float* __restrict__ prob_init,
                                                         const float* __restrict__ hyps, float* __restrict__ depth,
                                                         float* __restrict__ conf, float* __restrict__ var,
                                                         float* __restrict__ prob, int vec_ok) {
+  constexpr int PL = sizeof(T) == 4 ? 2 : 1;  // 16-byte pieces per voxel (and LDS planes per tile)
+  constexpr int NA = PL == 1 ? kPRChunks * kPRTerms : kPRChunks * 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint4* tile = reinterpret_cast<uint4*>(smem);                 // 2 x 340 voxels (double buffer)
-  float* lg = reinterpret_cast<float*>(tile + 2 * kPRVox);      // [D][256] logits, column per pixel
+  uint4* tile = reinterpret_cast<uint4*>(smem);                 // 2 x PL x 340 voxels (double buffer)
+  float* lg = reinterpret_cast<float*>(tile + 2 * PL * kPRVox); // [D][256] logits, column per pixel
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, g = lane >> 4;
   const int y0 = blockIdx.y * kTY, x0 = blockIdx.x * kTX;
   const int b = blockIdx.z;
   const int R0 = 4 * (wave >> 1), C0 = 16 * (wave & 1);
   const int pix = (R0 + g) * kTX + C0 + n;  // this lane's pixel in the tile: its logit column
-  const __amdgpu_buffer_rsrc_t rf = make_rsrc(feat, (long long)B * D * h * w * 16);
+  const __amdgpu_buffer_rsrc_t rf = make_rsrc(feat, (long long)B * D * h * w * 16 * PL);
 
-  uint4 af[kPRChunks][kPRTerms];
+  uint4 af[NA];  // bf16: [chunk][term]; fp32: [chunk][hi, lo]
 #pragma unroll
-  for (int k = 0; k < kPRChunks; ++k)
+  for (int k = 0; k < kPRChunks; ++k) {
+    if constexpr (PL == 1) {
 #pragma unroll
-    for (int t = 0; t < kPRTerms; ++t) af[k][t] = apack[(k * kPRTerms + t) * 64 + lane];
+      for (int t = 0; t < kPRTerms; ++t) af[k * kPRTerms + t] = apack[(k * kPRTerms + t) * 64 + lane];
+    } else {
+      af[2 * k] = apack[k * 128 + lane];
+      af[2 * k + 1] = apack[k * 128 + 64 + lane];
+    }
+  }
   int boff[kPRChunks];  // LDS voxel of this lane's slot in every chunk
 #pragma unroll
   for (int k = 0; k < kPRChunks; ++k) {
@@ -337,22 +349,34 @@ __global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int
     const int v = tid + 256 * k, row = v / kHX, col = v - row * kHX;
     const int yy = y0 - 1 + row, xx = x0 - 1 + col;
     const bool ok = v < kPRVox && (unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w;
-    goff[k] = ok ? (uint32_t)(((size_t)b * D * h + yy) * w + xx) * 16u : kOOB;
+    goff[k] = ok ? (uint32_t)(((size_t)b * D * h + yy) * w + xx) * (16u * PL) : kOOB;
   }
   // Input planes are fetched kPRAhead planes ahead into a register ring (the per-plane work is ~20 instructions:
   // one fetch in flight per block left every plane waiting out a full memory latency); fetches past the last plane
   // are out-of-range buffer loads (no traffic, but counted like the others, so the wait counts stay static).
-  const uint32_t pstride = (uint32_t)h * w * 16u;
-  uint4 ring[kPRAhead][2];
-  auto gload = [&](int pl, uint4 (&st)[2]) {
+  const uint32_t pstride = (uint32_t)h * w * 16u * PL;
+  uint4 ring[kPRAhead][2][PL];
+  auto gload = [&](int pl, uint4 (&st)[2][PL]) {
 #pragma unroll
     for (int k = 0; k < 2; ++k)
-      st[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            rf, goff[k] == kOOB || pl >= D ? kOOB : goff[k] + (uint32_t)pl * pstride, 0, 0));
+#pragma unroll
+      for (int hh = 0; hh < PL; ++hh)
+        st[k][hh] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  rf, goff[k] == kOOB || pl >= D ? kOOB : goff[k] + (uint32_t)pl * pstride + 16u * hh, 0, 0));
   };
-  auto lstore = [&](int bi, const uint4 (&st)[2]) {
-    tile[bi * kPRVox + tid] = st[0];
-    if (tid + 256 < kPRVox) tile[bi * kPRVox + tid + 256] = st[1];
+  auto lstore = [&](int bi, const uint4 (&st)[2][PL]) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int v = tid + 256 * k;
+      if (k == 1 && v >= kPRVox) break;
+      if constexpr (PL == 1) {
+        tile[bi * kPRVox + v] = st[k][0];
+      } else {
+        const F16Pair p = split8(__builtin_bit_cast(float4, st[k][0]), __builtin_bit_cast(float4, st[k][1]));
+        tile[(bi * 2) * kPRVox + v] = p.h;
+        tile[(bi * 2 + 1) * kPRVox + v] = p.l;
+      }
+    }
   };
 
 #pragma unroll
@@ -366,22 +390,36 @@ __global__ __launch_bounds__(256) void prob_mfma_kernel(int B, int D, int h, int
     for (int u = 0; u < kPRAhead; ++u) {
       const int pl = pl0 + u;
       if (pl >= D) break;
-      const uint4* tb = tile + (pl & 1) * kPRVox;
-      f32x4_t acc[kPRTerms];
+      f32x4_t sum;
+      if constexpr (PL == 1) {
+        const uint4* tb = tile + (pl & 1) * kPRVox;
+        f32x4_t acc[kPRTerms];
 #pragma unroll
-      for (int t = 0; t < kPRTerms; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < kPRTerms; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < kPRChunks; ++k) {
-        uint4 bv = tb[boff[k]];
-        if (k == kPRChunks - 1 && bpad) bv = make_uint4(0u, 0u, 0u, 0u);
+        for (int k = 0; k < kPRChunks; ++k) {
+          uint4 bv = tb[boff[k]];
+          if (k == kPRChunks - 1 && bpad) bv = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-        for (int t = 0; t < kPRTerms; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[k][t]),
-                                                           __builtin_bit_cast(bf16x8_t, bv), acc[t], 0, 0, 0);
+          for (int t = 0; t < kPRTerms; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[k * kPRTerms + t]),
+                                                             __builtin_bit_cast(bf16x8_t, bv), acc[t], 0, 0, 0);
+        }
+        sum = acc[kPRTerms - 1];  // hi + lo (+ mid)
+#pragma unroll
+        for (int t = kPRTerms - 2; t >= 0; --t) sum = acc[t] + sum;
+      } else {
+        const uint4* th = tile + ((pl & 1) * 2) * kPRVox;
+        const uint4* tl = th + kPRVox;
+        f32x4_t acc = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < kPRChunks; ++k) {
+          F16Pair bv{th[boff[k]], tl[boff[k]]};
+          if (k == kPRChunks - 1 && bpad) bv = F16Pair{make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u)};
+          mma_split32(F16Pair{af[2 * k], af[2 * k + 1]}, bv, acc);
+        }
+        sum = acc * pscale;  // 2^-k: exact
       }
-      f32x4_t sum = acc[kPRTerms - 1];  // hi + lo (+ mid)
-#pragma unroll
-      for (int t = kPRTerms - 2; t >= 0; --t) sum = acc[t] + sum;
       if (pl >= 1) lg[(pl - 1) * 256 + pix] = am1 + sum[2];
       am1 = a0 + sum[1];
       a0 = sum[0];
@@ -556,25 +594,35 @@ hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float
 
 namespace damvs {
 
-size_t prob_mfma_smem(int D) { return 2 * (size_t)kPRVox * 16 + (size_t)(D > 0 ? D : 0) * 256 * 4; }
+size_t prob_mfma_smem(int store, int D) {
+  return 2 * (size_t)kPRVox * 16 * (store == ST_BF16 ? 1 : 2) + (size_t)(D > 0 ? D : 0) * 256 * 4;
+}
 
-hipError_t launch_prob_mfma(hipStream_t s, int B, int D, int h, int w, const void* feat, const void* apack,
-                            const float* prob_init, const float* hyps, float* depth, float* conf, float* var,
-                            float* prob) {
-  const size_t smem = prob_mfma_smem(D);
+hipError_t launch_prob_mfma(hipStream_t s, int store, int B, int D, int h, int w, const void* feat, const void* apack,
+                            float pscale, const float* prob_init, const float* hyps, float* depth, float* conf,
+                            float* var, float* prob) {
+  const size_t smem = prob_mfma_smem(store, D);
+  const int PL = store == ST_BF16 ? 1 : 2;
   if (D < 1 || smem > 160 * 1024) return hipErrorInvalidValue;
-  if ((long long)B * D * h * w * 16 >= (1LL << 32) - 16) return hipErrorInvalidValue;  // 32-bit buffer offsets
+  if ((long long)B * D * h * w * 16 * PL >= (1LL << 31)) return hipErrorInvalidValue;  // 32-bit buffer offsets
+  const void* k = store == ST_BF16 ? reinterpret_cast<const void*>(prob_mfma_kernel<bf16_t>)
+                                   : reinterpret_cast<const void*>(prob_mfma_kernel<float>);
   if (smem > 64 * 1024) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(prob_mfma_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
   }
   const dim3 grid((w + kTX - 1) / kTX, (h + kTY - 1) / kTY, B);
   // 16-byte probability stores need w % 4 == 0 (DAMVS_PROB_VEC=0, read per call: one 4-byte store per pixel and plane)
   const char* pv = getenv("DAMVS_PROB_VEC");
   const int vec_ok = (w & 3) == 0 && !(pv && pv[0] == '0');
-  hipLaunchKernelGGL(prob_mfma_kernel, grid, dim3(256), smem, s, B, D, h, w, reinterpret_cast<const bf16_t*>(feat),
-                     reinterpret_cast<const uint4*>(apack), prob_init, hyps, depth, conf, var, prob, vec_ok);
+  if (store == ST_BF16)
+    hipLaunchKernelGGL(prob_mfma_kernel<bf16_t>, grid, dim3(256), smem, s, B, D, h, w,
+                       reinterpret_cast<const bf16_t*>(feat), reinterpret_cast<const uint4*>(apack), 1.f, prob_init,
+                       hyps, depth, conf, var, prob, vec_ok);
+  else
+    hipLaunchKernelGGL(prob_mfma_kernel<float>, grid, dim3(256), smem, s, B, D, h, w,
+                       reinterpret_cast<const float*>(feat), reinterpret_cast<const uint4*>(apack), pscale, prob_init,
+                       hyps, depth, conf, var, prob, vec_ok);
   return hipGetLastError();
 }
 

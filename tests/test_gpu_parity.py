@@ -275,24 +275,26 @@ def test_prob_mfma_vector_stores_match(monkeypatch):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("s,D,W", [(0, 48, 80), (1, 32, 80), (0, 64, 80), (2, 8, 72), (1, 16, 104)])
 @pytest.mark.parametrize("with_init", [False, True])
-def test_prob_mfma_vs_split_path(s, D, W, with_init):
+def test_prob_mfma_vs_split_path(s, D, W, with_init, dtype):
     """bf16 stage regression (prob conv on MFMA + regression, prob_mfma_kernel in k_regress.hip: the default for
     bf16 storage) against the split path on the same U-Net output (damvs_costreg_logits: fp32-weight VALU prob
     conv, then damvs_regress). The MFMA form multiplies the bf16 voxels exactly by the fp32 weights carried as two
     bf16 terms (relative weight error < 2^-17); W = 72 / 104 leave ragged 32-pixel tiles; with_init adds a
     prob_volume_init (models/cas_mvsnet.py:107-108) to the logits. The probabilities leave as 16-byte runs (the stage
-    width is a multiple of 8); test_prob_mfma_vector_stores_match covers the 4-byte form."""
+    width is a multiple of 8); test_prob_mfma_vector_stores_match covers the 4-byte form. fp32: the split-f16 form
+    (prob_mfma_kernel<float>: the fp32 voxels as f16 hi / lo halves, the weights split on the host) against the fp32
+    VALU prob conv of the split path."""
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import StageEngine, regress
     C = (32, 16, 8)[s]
     net = CascadeMVSNet(ndepths=[48, 32, 8])
     net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
     feats, P, hyps = depthnet_inputs(B=2, N=3, H=32, W=W, D=D, stage_idx=s, C=C)
-    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.bfloat16,
-                      torch.device(DEV))
-    nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)) for f in feats]
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", dtype, torch.device(DEV))
+    nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(dtype)) for f in feats]
     hyps = cuda(hyps)
     logits = eng.costreg_logits(eng.warp_aggregate(nhwc, cuda(P), hyps))
     init = None
