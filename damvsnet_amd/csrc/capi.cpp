@@ -1159,10 +1159,10 @@ int damvs_conv2d_create(const damvs_conv2d_desc* desc, const float* weight, cons
       const int kexp = split_exponent(pk);
       L->wscale = std::ldexp(1.f, -kexp);
       rc = upload_split(pk, kexp, &L->wpack);
-      // the wide kernel's form (conv2d_wide_kernel<float>): phases and weights at 32 K per chunk
+      // the 32-K split form of the wide kernel (conv2d_wide_kernel<float>) and of the narrow halo kernel
+      // (conv2d_halo_kernel<float, ..., W32>): phases and weights at 32 K per chunk
       const int ctot = d.c0 + d.c1;
-      if (rc == DAMVS_OK && !L->xpair && d.c0 % 32 == 0 && d.c1 % 32 == 0 && ctot >= 64 && d.cout % 32 == 0 &&
-          d.ngeo <= 1) {
+      if (rc == DAMVS_OK && !L->xpair && d.c0 % 32 == 0 && d.c1 % 32 == 0 && ctot >= 32 && d.ngeo <= 1) {
         damvs_conv2d T32 = *L;
         T32.wpack = nullptr;
         T32.kchunk_k = 32;
@@ -1347,13 +1347,13 @@ int damvs_conv2d_forward(const damvs_conv2d* L, void* stream, int B, int Hi, int
   a.div_wq = make_fastdiv(a.Wq);
   a.div_hq = make_fastdiv(a.Hq);
   std::memcpy(a.ph, L->ph, sizeof(a.ph));
-  if (L->wpack32) {  // fp32: the wide kernel on the 32-K split packing when it takes the shape
+  if (L->wpack32 && !conv2d_wide32_disabled()) {  // fp32: the 32-K split packing when the wide or halo kernel takes it
     Conv2dArgs a32 = a;
     std::memcpy(a32.ph, L->ph32, sizeof(a32.ph));
     a32.wpack = L->wpack32;
     a32.wide32 = 1;
-    if (conv2d_wide_shape_ok(a32) && !conv2d_wide32_disabled())
-      return hip_check(launch_conv2d(reinterpret_cast<hipStream_t>(stream), L->dtype, a32), "conv2d launch");
+    const hipError_t e = launch_conv2d(reinterpret_cast<hipStream_t>(stream), L->dtype, a32);
+    if (e != hipErrorNotSupported) return hip_check(e, "conv2d launch");
   }
   return hip_check(launch_conv2d(reinterpret_cast<hipStream_t>(stream), L->dtype, a), "conv2d launch");
 }

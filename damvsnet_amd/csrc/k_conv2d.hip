@@ -11,6 +11,8 @@
 // phases, each a dense sub-convolution over the input grid (no structural zeros on MFMA).
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "damvs_device.h"
 
 namespace damvs {
@@ -468,18 +470,29 @@ constexpr int HGR = 4, HGC = 64;  // q-tile rows (one per group) x columns (16 p
 // WM: waves stacked along the output channels (1: 4 waves side by side over the 4 column groups,
 // each with MT cout tiles x 4 rows; 2: a 2 x 2 wave grid, each wave MT cout tiles x 2 column groups x
 // 4 rows — half the A (weight) stream per MFMA for the wide layers).
-template <typename T, int MT, int WM, bool TWO>
+// W32 (T = float, the fp32 path's 32-K form: a.wide32, the layer's 32-K split packing): K chunks of 32 channels as
+// split-f16 MFMAs (mma_split32, 16x16x32 at full rate) instead of the 16-K form's three 16x16x16 per 16 channels; a
+// halo pixel keeps each 8-channel chunk as its f16 hi / lo halves in 8 slots, slot s at s ^ ((pixel >> 1) & 7) (the
+// 16 lanes of an N-group read 16 consecutive pixels); one halo buffer, rewritten between two barriers after a slice's
+// last tap (twice the bytes of the bf16 tile).
+template <typename T, int MT, int WM, bool TWO, bool W32 = false>
 __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int nsl,
                                                           int dmin, int span) {
   typedef BufIO<T> IO;
   typedef typename IO::raw raw;
+  typedef typename std::conditional<W32, F16Pair, raw>::type frag;
+  static_assert(!W32 || sizeof(T) == 4, "32-K split form: fp32 storage");
   constexpr int E = Stor<T>::E;
-  constexpr int KC = 4 * E;
+  constexpr int KC = W32 ? 32 : 4 * E;
+  constexpr int SL = W32 ? 8 : 4;   // 16-byte LDS slots per halo pixel and slice
+  constexpr int CE = KC / 4;        // channels per lane group and chunk
   constexpr uint32_t ES = sizeof(T);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   raw* buf = reinterpret_cast<raw*>(smem);
+  uint4* ubuf = reinterpret_cast<uint4*>(smem);
   const int HR = HGR + span - 1, HC = HGC + span - 1;  // halo rows / columns
   const int HP = HR * HC;                               // halo pixels (4 chunks each)
+  auto wslot = [](int p, int q) { return q ^ ((p >> 1) & 7); };
 
   // logical block = (tile, phase), phase fastest, XCD-contiguous
   const int ntile = tiles_x * tiles_y * a.B;
@@ -498,13 +511,14 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
   if (threadIdx.x < 25)
     s_toff[threadIdx.x] = threadIdx.x < ph.ntaps ? (ph.tap[threadIdx.x][0] - dmin) * HC + (ph.tap[threadIdx.x][1] - dmin) : 0;
 
-  // halo fill of slice c into buffer bi: pixel p = (row, col), 4 chunks of E channels
+  // halo fill of slice c into buffer bi: pixel p = (row, col), 4 chunks of CE channels
   const int npix = a.B * a.Hi * a.Wi;
   const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.in0, (long long)npix * a.c0 * ES);
   const __amdgpu_buffer_rsrc_t r1 = make_rsrc(TWO ? a.in1 : a.in0, TWO ? (long long)npix * a.c1 * ES : 0);
   const int iy0 = qy0 + dmin, ix0 = qx0 + dmin, pb = b * a.Hi * a.Wi;
-  constexpr int PER = 8;  // 16-byte pieces per thread per fill (covers 2048 pieces = 512 halo pixels)
-  raw regs[PER];
+  constexpr int PER = 8;             // chunks per thread per fill (covers 2048 chunks = 512 halo pixels)
+  constexpr int NR = W32 ? 2 : 1;    // 16-byte loads per chunk
+  raw regs[PER][NR];
   auto gfill = [&](int c) {
     const bool second = TWO && c * KC >= a.c0;
     const int cs = second ? a.c1 : a.c0, cb = (second ? c * KC - a.c0 : c * KC);
@@ -515,15 +529,28 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
       const int row = p / HC, col = p - row * HC;
       const int iy = iy0 + row, ix = ix0 + col;
       const bool ok = p < HP && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
-      const uint32_t off = (uint32_t)((pb + iy * a.Wi + ix) * cs + cb + part * E) * ES;
-      regs[k] = (TWO && second) ? IO::frag(r1, ok ? off : kOOB) : IO::frag(r0, ok ? off : kOOB);
+      const uint32_t off = (uint32_t)((pb + iy * a.Wi + ix) * cs + cb + part * CE) * ES;
+#pragma unroll
+      for (int h = 0; h < NR; ++h) {
+        const uint32_t o = ok ? off + 16u * h : kOOB;
+        regs[k][h] = (TWO && second) ? IO::frag(r1, o) : IO::frag(r0, o);
+      }
     }
   };
   auto lstore = [&](int bi) {
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int i = threadIdx.x + k * 256;
-      if ((i >> 2) < HP) buf[bi * HP * 4 + i] = Frag2<T>::stage(regs[k]);
+      const int p = i >> 2, part = i & 3;
+      if (p >= HP) continue;
+      if constexpr (W32) {
+        const F16Pair v = split8(regs[k][0], regs[k][1]);
+        uint4* px = ubuf + (bi * HP + p) * 8;
+        px[wslot(p, part)] = v.h;
+        px[wslot(p, part + 4)] = v.l;
+      } else {
+        buf[bi * HP * 4 + i] = Frag2<T>::stage(regs[k][0]);
+      }
     }
   };
 
@@ -534,9 +561,22 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
   for (int j = 0; j < GW; ++j)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  // A: 16-K form [chunk][tile][lane] raw fragments; W32 [chunk][tile][hi: 64 lanes][lo: 64 lanes]
   const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + ((size_t)ph.w_off * a.MTtot + mt0) * 64 + lane;
+  const uint4* __restrict__ wp32 =
+      reinterpret_cast<const uint4*>(a.wpack) + ((size_t)ph.w_off * a.MTtot + mt0) * 128 + lane;
+  auto wload = [&](int chunk, int m) -> frag {
+    if constexpr (W32) {
+      const uint4* q = wp32 + ((size_t)chunk * a.MTtot + m) * 128;
+      return F16Pair{q[0], q[64]};
+    } else {
+      return wp[((size_t)chunk * a.MTtot + m) * 64];
+    }
+  };
   const int nt = ph.ntaps;
-  const int lbase = (wn * CG * 16 + n) * 4 + g;  // this lane's chunk at halo pixel (0, first column + n)
+  const int pcol = wn * CG * 16 + n;             // this lane's halo pixel column offset (row 0, first column + n)
+  const int lbase = pcol * 4 + g;                // 16-K form: its chunk
+  constexpr int NHB = W32 ? 1 : 2;
   (void)wave;
 
   gfill(0);
@@ -544,48 +584,61 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
   __syncthreads();
   for (int c = 0; c < nsl; ++c) {
     if (c + 1 < nsl) gfill(c + 1);
-    const raw* hb = buf + (c & 1) * HP * 4 + lbase;
-    raw wf[MT];
+    const int bi = NHB == 2 ? (c & 1) : 0;
+    frag wf[MT];
 #pragma unroll
-    for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(c * a.MTtot + m) * 64];  // chunk (tap 0, slice c)
+    for (int m = 0; m < MT; ++m) wf[m] = wload(c, m);  // chunk (tap 0, slice c)
     for (int t = 0; t < nt; ++t) {
-      raw wn[MT];
+      frag wn2[MT];
       if (t + 1 < nt) {
 #pragma unroll
-        for (int m = 0; m < MT; ++m) wn[m] = wp[(size_t)(((t + 1) * nsl + c) * a.MTtot + m) * 64];
+        for (int m = 0; m < MT; ++m) wn2[m] = wload((t + 1) * nsl + c, m);
       }
-      const int to = s_toff[t] * 4;
-      raw xf[GW];  // group j: row j % HGR, column group j / HGR of this wave
+      frag xf[GW];  // group j: row j % HGR, column group j / HGR of this wave
+      if constexpr (W32) {
 #pragma unroll
-      for (int j = 0; j < GW; ++j) xf[j] = hb[to + ((j % HGR) * HC + (j / HGR) * 16) * 4];
+        for (int j = 0; j < GW; ++j) {
+          const int pl = s_toff[t] + (j % HGR) * HC + (j / HGR) * 16 + pcol;
+          const uint4* px = ubuf + (bi * HP + pl) * 8;
+          xf[j] = F16Pair{px[wslot(pl, g)], px[wslot(pl, g + 4)]};
+        }
+      } else {
+        const raw* hb = buf + bi * HP * 4 + lbase;
+        const int to = s_toff[t] * 4;
+#pragma unroll
+        for (int j = 0; j < GW; ++j) xf[j] = hb[to + ((j % HGR) * HC + (j / HGR) * 16) * 4];
+      }
 #pragma unroll
       for (int j = 0; j < GW; ++j)
 #pragma unroll
-        for (int m = 0; m < MT; ++m) Frag2<T>::mma_staged(wf[m], xf[j], acc[j][m]);
+        for (int m = 0; m < MT; ++m) {
+          if constexpr (W32) mma_split32(wf[m], xf[j], acc[j][m]);
+          else Frag2<T>::mma_staged(wf[m], xf[j], acc[j][m]);
+        }
       if (t + 1 < nt) {
 #pragma unroll
-        for (int m = 0; m < MT; ++m) wf[m] = wn[m];
+        for (int m = 0; m < MT; ++m) wf[m] = wn2[m];
       }
     }
-    if (c + 1 < nsl) {  // buffer (c + 1) & 1 was last read before the previous barrier
-      lstore((c + 1) & 1);
+    if (c + 1 < nsl) {
+      if (NHB == 1) __syncthreads();  // every wave is done with slice c's halo
+      lstore(NHB == 2 ? (c + 1) & 1 : 0);  // (NHB 2: buffer (c + 1) & 1 was last read before the previous barrier)
       __syncthreads();
     }
   }
 
   // the fp32 plane as trailing K chunks (tap x plane), as in conv2d_mfma_kernel
   if (ph.gchunks > 0) {
-    const raw* __restrict__ wg = wp + (size_t)ph.kchunks * a.MTtot * 64;
     const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.geo[0], ((long long)(a.B - 1) * a.geo_bstride[0] + a.Hi * a.Wi) * 4);
     const int pg0 = b * (int)a.geo_bstride[0];
     for (int s = 0; s < ph.gchunks; ++s) {
-      raw wf[MT];
+      frag wf[MT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) wf[m] = wg[(size_t)(s * a.MTtot + m) * 64];
-      float v[GW][E];
+      for (int m = 0; m < MT; ++m) wf[m] = wload(ph.kchunks + s, m);
+      float v[GW][CE];
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int t = s * KC + g * E + e;
+      for (int e = 0; e < CE; ++e) {
+        const int t = s * KC + g * CE + e;
         const bool tv = t < nt;
         const int dy = tv ? ph.tap[t][0] : 0, dx = tv ? ph.tap[t][1] : 0;
 #pragma unroll
@@ -598,13 +651,18 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
       }
 #pragma unroll
       for (int j = 0; j < GW; ++j) {
-        const raw xf = pack_vals<T>(v[j]);
+        if constexpr (W32) {
+          const F16Pair xf = split8(v[j]);
 #pragma unroll
-        for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf, acc[j][m]);
+          for (int m = 0; m < MT; ++m) mma_split32(wf[m], xf, acc[j][m]);
+        } else {
+          const raw xf = pack_vals<T>(v[j]);
+#pragma unroll
+          for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf, acc[j][m]);
+        }
       }
     }
   }
-
   // epilogue (as conv2d_mfma_kernel)
   typedef typename IO::quad quad;
   const int up = a.post_up, us = a.post_up >> 1;
@@ -653,25 +711,29 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
   }
 }
 
-template <typename T, int MT, int WM>
+template <typename T, int MT, int WM, bool W32 = false>
 hipError_t launch_halo_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span) {
-  constexpr int KC = 4 * Stor<T>::E;
+  constexpr int KC = W32 ? 32 : 4 * Stor<T>::E;
   const int tx = (a.Wq + HGC - 1) / HGC, ty = (a.Hq + HGR - 1) / HGR;
   const int nsl = (a.c0 + a.c1) / KC;
-  const size_t smem = (nsl > 1 ? 2 : 1) * (size_t)(HGR + span - 1) * (HGC + span - 1) * 4 * 16;  // one slice: one buffer
+  const size_t hp = (size_t)(HGR + span - 1) * (HGC + span - 1);
+  const size_t smem = W32 ? hp * 8 * 16 : (nsl > 1 ? 2 : 1) * hp * 4 * 16;  // one slice (or W32): one buffer
   const long long nblk = (long long)tx * ty * a.B * a.nphase;
   const dim3 grid((unsigned)nblk, (unsigned)(a.MTtot / (MT * WM)));
-  if (a.c1 > 0)
-    hipLaunchKernelGGL((conv2d_halo_kernel<T, MT, WM, true>), grid, dim3(256), smem, s, a, tx, ty, nsl, dmin, span);
-  else
-    hipLaunchKernelGGL((conv2d_halo_kernel<T, MT, WM, false>), grid, dim3(256), smem, s, a, tx, ty, nsl, dmin, span);
+  auto k = a.c1 > 0 ? conv2d_halo_kernel<T, MT, WM, true, W32> : conv2d_halo_kernel<T, MT, WM, false, W32>;
+  if (smem > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)smem);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, grid, dim3(256), smem, s, a, tx, ty, nsl, dmin, span);
   return hipGetLastError();
 }
 
-// Returns hipErrorNotSupported when the halo kernel does not take the layer.
-template <typename T>
+// Returns hipErrorNotSupported when the halo kernel does not take the layer. W32: the fp32 layer's 32-K split form.
+template <typename T, bool W32 = false>
 hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a) {
-  constexpr int KC = 4 * Stor<T>::E;
+  constexpr int KC = W32 ? 32 : 4 * Stor<T>::E;
   // largest cout tile count (MTtot) the halo kernel takes: its B reuse pays off for narrow outputs,
   // while wide outputs are bound by the A (weight) stream the gather kernel already amortises
   static const int max_mt = [] {
@@ -699,6 +761,11 @@ hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a) {
   if ((HGR + span - 1) * (HGC + span - 1) > 512) return hipErrorNotSupported;  // PER = 8 fill pieces a thread
   // cout tile as wide as keeps about one wave per SIMD busy (the tile count is small for these layers)
   const long long tiles = (long long)((a.Wq + HGC - 1) / HGC) * ((a.Hq + HGR - 1) / HGR) * a.B * a.nphase;
+  if constexpr (W32) {  // fp32 32-K form: the narrow layers (cout <= 32)
+    if (a.MTtot == 2) return launch_halo_t<T, 2, 1, true>(s, a, dmin, span);
+    if (a.MTtot == 1) return launch_halo_t<T, 1, 1, true>(s, a, dmin, span);
+    return hipErrorNotSupported;
+  }
   if (a.MTtot >= 8) {  // wide: 2 x 2 wave grid, 4 cout tiles x 128 pixels a wave
     if (a.MTtot % 8 == 0) return launch_halo_t<T, 4, 2>(s, a, dmin, span);
     return hipErrorNotSupported;
@@ -1511,8 +1578,13 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
     return hipGetLastError();
   }
   if (a.ngeo > 1) return hipErrorInvalidValue;  // the MFMA path takes at most one plane
-  if (a.wide32) {  // fp32 layer with its 32-K split packing (damvs_conv2d_forward checked conv2d_wide_shape_ok)
-    if constexpr (sizeof(T) == 4) return launch_wide<T>(s, a);
+  if (a.wide32) {  // fp32 layer with its 32-K split packing: the wide kernel, else the narrow halo kernel, else
+                   // hipErrorNotSupported (damvs_conv2d_forward then runs the 16-K packing)
+    if constexpr (sizeof(T) == 4) {
+      const hipError_t e = launch_wide<T>(s, a);
+      if (e != hipErrorNotSupported) return e;
+      return launch_halo<T, true>(s, a);
+    }
     return hipErrorInvalidValue;
   }
   if (a.xpair) {  // x-pair phases (built at layer creation): only the XP gather kernel runs them
