@@ -59,9 +59,10 @@ def cascade_cost(H: int, W: int, N: int, ndepths, e: int, channels=(32, 16, 8), 
 
 
 def head_fused() -> bool:
-    """Whether the library runs the fused head (damvs_stage_forward; DAMVS_HEAD_FUSE=0 turns it off)."""
+    """Whether the library runs the fused head (damvs_stage_forward: only with DAMVS_HEAD_FUSE=1, capi.cpp
+    head_fusable)."""
     import os
-    return os.environ.get("DAMVS_HEAD_FUSE", "1")[:1] != "0"
+    return os.environ.get("DAMVS_HEAD_FUSE", "0")[:1] == "1"
 
 
 def roofline_time(nbytes: float, flops: float, dtype: str = "bf16") -> float:

@@ -453,7 +453,7 @@ int regress_tail(const damvs_stage* st, hipStream_t s, int B, int D, int h, int 
                  const float* prob_init, float* logits, float* depth, float* conf, float* var, float* prob) {
   // base 8: the prob conv on MFMA (logits in an LDS column, as the VALU kernel below); fp32 as split-f16 MFMAs
   const void* pk = st->dtype == DAMVS_BF16 ? st->prob_pack : st->prob_split;
-  if (pk && prob_mfma_smem(st->dtype, D) <= 160 * 1024 && !prob_mfma_disabled())
+  if (pk && prob_mfma_smem(st->dtype, D) <= 160 * 1024 && prob_mfma_enabled(st->dtype))
     return hip_check(launch_prob_mfma(s, st->dtype, B, D, h, w, feat, pk, st->dtype == DAMVS_BF16 ? 1.f : st->prob_scale,
                                       prob_init, hyps, depth, conf, var, prob),
                      "prob_mfma launch");

@@ -190,6 +190,7 @@ hipError_t launch_prob_mfma(hipStream_t s, int store, int B, int D, int h, int w
                             float* var, float* prob);
 size_t prob_mfma_smem(int store, int D);
 bool prob_mfma_disabled();  // DAMVS_PROB_MFMA=0 (A/B testing)
+bool prob_mfma_enabled(int store);  // bf16 unless DAMVS_PROB_MFMA=0; fp32 only with DAMVS_PROB_MFMA=1
 hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float* logits, const float* hyps,
                           float* depth, float* conf, float* var, float* prob);
 

@@ -632,4 +632,13 @@ bool prob_mfma_disabled() {
   return v && v[0] == '0';
 }
 
+// The stage regression's prob conv on MFMA for this storage type: bf16 by default; fp32 (the split-f16 form) only
+// with DAMVS_PROB_MFMA=1 -- three MFMAs per product measured slower than the VALU kernel (cfgC B=4 fp32: 1.66
+// against 1.56 ms per step, profiles/r04/prof_steps_f32_r04j.txt).
+bool prob_mfma_enabled(int store) {
+  const char* v = getenv("DAMVS_PROB_MFMA");
+  if (v && v[0] == '0') return false;
+  return store == ST_BF16 || (v && v[0] == '1');
+}
+
 }  // namespace damvs

@@ -278,7 +278,7 @@ def test_prob_mfma_vector_stores_match(monkeypatch):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("s,D,W", [(0, 48, 80), (1, 32, 80), (0, 64, 80), (2, 8, 72), (1, 16, 104)])
 @pytest.mark.parametrize("with_init", [False, True])
-def test_prob_mfma_vs_split_path(s, D, W, with_init, dtype):
+def test_prob_mfma_vs_split_path(s, D, W, with_init, dtype, monkeypatch):
     """bf16 stage regression (prob conv on MFMA + regression, prob_mfma_kernel in k_regress.hip: the default for
     bf16 storage) against the split path on the same U-Net output (damvs_costreg_logits: fp32-weight VALU prob
     conv, then damvs_regress). The MFMA form multiplies the bf16 voxels exactly by the fp32 weights carried as two
@@ -286,7 +286,8 @@ def test_prob_mfma_vs_split_path(s, D, W, with_init, dtype):
     prob_volume_init (models/cas_mvsnet.py:107-108) to the logits. The probabilities leave as 16-byte runs (the stage
     width is a multiple of 8); test_prob_mfma_vector_stores_match covers the 4-byte form. fp32: the split-f16 form
     (prob_mfma_kernel<float>: the fp32 voxels as f16 hi / lo halves, the weights split on the host) against the fp32
-    VALU prob conv of the split path."""
+    VALU prob conv of the split path (the fp32 form runs only with DAMVS_PROB_MFMA=1: measured slower)."""
+    monkeypatch.setenv("DAMVS_PROB_MFMA", "1")
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import StageEngine, regress
     C = (32, 16, 8)[s]
