@@ -183,6 +183,12 @@ __device__ __forceinline__ void store_vec(T* p, const float* v) {
 #define DAMVS_WAVES(n) __attribute__((amdgpu_waves_per_eu(n)))
 #endif
 
+// For kernel-local lambdas with large bodies used at two or more call sites: hipcc may otherwise emit them as
+// functions, the by-reference closure then lives in scratch and LDS pointers reaching them turn generic (flat
+// stores). conv2d_wide_kernel<float> at input stride 2 had exactly that (512 B of scratch, flat halo stores:
+// 5-7x the bf16 kernel's time instead of ~3x).
+#define DAMVS_INLINE __attribute__((always_inline))
+
 typedef unsigned int v4u32_t __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u32_t __attribute__((ext_vector_type(2)));
 

@@ -854,7 +854,7 @@ template <> struct WideForm<float> {
 // 4-row halo would not fit): a 2 x 64 q-tile, the 4 waves a 2 x 2 grid (q-row, 32-column half).
 // T = float: the fp32 parity path's form (one halo buffer, rewritten between two barriers after a slice's last tap).
 template <typename T, bool TWO, int IS, int WM>
-__global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : IS == 1 ? 3 : 2) void conv2d_wide_kernel(
+__global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1) : IS == 1 ? 3 : 2) void conv2d_wide_kernel(
     const Conv2dArgs a, int tiles_x, int tiles_y, int nsl, int dmin, int span) {
   typedef uint4 raw;
   typedef WideForm<T> Fm;
@@ -925,7 +925,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : IS == 1 ? 3 :
     }
   }
   raw hreg[WPER][PL];
-  auto hload = [&](int c) {
+  auto hload = [&](int c) DAMVS_INLINE {
     const bool second = TWO && c * 32 >= a.c0;
     const int cs = second ? a.c1 : a.c0, cb = second ? c * 32 - a.c0 : c * 32;
 #pragma unroll
@@ -938,7 +938,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : IS == 1 ? 3 :
       }
     }
   };
-  auto hstore = [&](int bi) {
+  auto hstore = [&](int bi) DAMVS_INLINE {
 #pragma unroll
     for (int k = 0; k < WPER; ++k) {
       if (hsl[k] < 0) continue;
@@ -988,7 +988,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : IS == 1 ? 3 :
       cc = cc + 1 < nsl ? cc + 1 : cc;  // past the end: stays on the last slice (clamped re-read)
     }
   };
-  auto wld = [&](raw (&x)[NA]) {
+  auto wld = [&](raw (&x)[NA]) DAMVS_INLINE {
     const uint32_t so = wbase + (uint32_t)(lt * nsl + lc) * cbytes;
 #pragma unroll
     for (int i = 0; i < NA; ++i)
@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : IS == 1 ? 3 :
   __syncthreads();
   const int lanepix = wn * IS * hg.pitch + wc + n;
   int k = 0;
-  auto step = [&](int c, int t, raw (&ld)[NA], const raw (&st)[NA]) {
+  auto step = [&](int c, int t, raw (&ld)[NA], const raw (&st)[NA]) DAMVS_INLINE {
     if (!(DAMVS_WIDE_DIAG & 8)) wld(ld);
     const int p0x = s_toff[t] + lanepix;
     const raw* hb = hbuf + (NHB == 2 ? (c & 1) * HP * SLOTS : 0) + p0x * SLOTS;

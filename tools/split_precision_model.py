@@ -27,7 +27,9 @@ from common import model_state, forward_inputs  # noqa: E402
 from conftest import golden  # noqa: E402
 
 PAIRS = {"h3": [(0, 0), (0, 1), (1, 0)], "h4": [(0, 0), (0, 1), (1, 0), (1, 1)], "2": [(0, 0)], "3": [(0, 0), (0, 1), (1, 0)], "4": [(0, 0), (0, 1), (1, 0), (1, 1)],
-         "6": [(0, 0), (0, 1), (1, 0), (0, 2), (2, 0), (1, 1)]}
+         "6": [(0, 0), (0, 1), (1, 0), (0, 2), (2, 0), (1, 1)],
+         "h1": [(0, 0)], "h2w": [(0, 0), (0, 1)], "h2x": [(0, 0), (1, 0)]}
+F16 = ("h1", "h2w", "h2x", "h3", "h4")  # pieces in f16 (the split-f16 MFMA forms); the others bf16
 
 
 def pieces(x, n, dt=torch.bfloat16):
@@ -49,7 +51,7 @@ def make(fn, pairs, xpieces=None):
         else:
             b = k.pop("bias", None)
         n = 1 + max(max(p) for p in pairs)
-        dt = torch.float16 if pairs is PAIRS["h3"] or pairs is PAIRS["h4"] else torch.bfloat16
+        dt = torch.float16 if any(pairs is PAIRS[k] for k in F16) else torch.bfloat16
         xp = pieces(x, n if xpieces is None else xpieces, dt)
         wp = pieces(w, n, dt)
         y = 0
