@@ -1071,11 +1071,18 @@ __global__ __launch_bounds__(256) void block_channels_kernel(const FeatPtrs src,
   }
   const uint4* sp = reinterpret_cast<const uint4*>(sv) + ((size_t)b * hw + p) * NQ;
   uint4* dp = const_cast<uint4*>(reinterpret_cast<const uint4*>(dv)) + (size_t)b * NQ * hw + p;
-  uint4 r[NQ];
+  // groups of at most 4 chunks: a register array of 6-8 uint4 was kept in scratch by hipcc
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) r[q] = sp[q];
+  for (int q0 = 0; q0 < NQ; q0 += 4) {
+    constexpr int G = NQ < 4 ? NQ : 4;
+    uint4 r[G];
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) dp[(size_t)q * hw] = r[q];
+    for (int q = 0; q < G; ++q)
+      if (q0 + q < NQ) r[q] = sp[q0 + q];
+#pragma unroll
+    for (int q = 0; q < G; ++q)
+      if (q0 + q < NQ) dp[(size_t)(q0 + q) * hw] = r[q];
+  }
 }
 
 }  // namespace
