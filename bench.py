@@ -127,6 +127,8 @@ def hot_path_roofline(per_stage_ms, H, W, N, nd, B, dtype_name):
             groups[g] = {"ms": round(ms[g], 4), "GB/s": round(nbytes / t / 1e9, 1), "TFLOP/s": round(flops / t / 1e12, 2),
                          "hbm_frac": round(nbytes / t / CM.HBM_PEAK, 4),
                          "mfma_frac": round(flops / t / CM.MFMA_PEAK[dtype_name], 4),
+                         **({"mfma_frac_vs_exact_f32": round(flops / t / CM.MFMA_PEAK["f32_exact"], 4)}
+                            if dtype_name == "f32" else {}),
                          "roofline_frac": round(CM.roofline_time(nbytes, flops, dtype_name) / t, 4)}
         sb = sum(B * cost[s][g][0] for g in groups)
         sf = sum(B * cost[s][g][1] for g in groups)

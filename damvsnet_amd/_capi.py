@@ -127,7 +127,10 @@ def load_library(path: str = LIB_PATH):
         raise RuntimeError("libdamvs.so not found at %s — build it with `python -m damvsnet_amd.build` "
                            "(the product has no CPU/eager fallback)" % path)
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    ab = os.path.abspath(path) != os.path.abspath(os.path.join(_HERE, "libdamvs.so"))
     for name, res, args in SIGNATURES:
+        if ab and not hasattr(lib, name):  # an A/B build of an older commit may lack later entry points
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = list(args)

@@ -19,7 +19,10 @@ from __future__ import annotations
 
 HBM_PEAK = 8.0e12              # B/s, MI355X HBM3E (MI355X_MICROARCH.md chip table, spec)
 MFMA_PEAK = {"bf16": 2.5e15,   # FLOP/s dense bf16 MFMA (spec, no sparsity)
-             "f32": 157.3e12}  # FLOP/s exact-f32 MFMA (= the FP32 vector rate)
+             # the fp32 path computes every conv product as three f16 MFMAs (split operands, DESIGN.md "The fp32
+             # path"): its instruction ceiling is a third of the dense f16 rate, not the exact-f32 MFMA's
+             "f32": 2.5e15 / 3,
+             "f32_exact": 157.3e12}  # FLOP/s exact-f32 MFMA (= the FP32 vector rate), reported beside it
 
 
 def unet_layers(C: int, base: int = 8):

@@ -100,18 +100,6 @@ template <> struct Rec16<bf16_t> {
 // batch element's map (rec bytes per record) and their weights. A corner outside the map gets the offset
 // kOOB, so its buffer load returns 0: grid_sample's zero padding without a weight select. Samples far
 // outside (or NaN) are moved to (-4, -4), where all four corners are outside.
-// Spelled-out multiply-adds shared by the warp kernels: with contraction left to the compiler, a*b + c*d + e may
-// fuse as fma(a, b, c*d) in one kernel and fma(c, d, a*b) in another, and the kernels that must agree bit for bit
-// (warp_split / warp_sweep) differed in the last bit of a coordinate. Every product-sum on the sampling path goes
-// through these.
-__device__ __forceinline__ float ray3(float m0, float m1, float m2, float fx, float fy) {
-  return fmaf(m0, fx, fmaf(m1, fy, m2));
-}
-__device__ __forceinline__ float src_coord(float q, float iz, float k) { return fmaf(q * iz, k, -0.5f); }
-__device__ __forceinline__ float bilerp(float v0, float v1, float v2, float v3, const float* wt) {
-  return fmaf(v3, wt[3], fmaf(v2, wt[2], fmaf(v1, wt[1], v0 * wt[0])));
-}
-
 struct Taps {
   uint32_t off[4];
   float wt[4];
@@ -246,13 +234,13 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
       for (int k = 0; k < 4; ++k) Rec16<T>::unpack(rv[q * 4 + k], v[k]);
       float s[E];
 #pragma unroll
-      for (int e = 0; e < E; ++e) s[e] = bilerp(v[0][e], v[1][e], v[2][e], v[3][e], wt);
+      for (int e = 0; e < E; ++e) s[e] = ((v[0][e] * wt[0] + v[1][e] * wt[1]) + v[2][e] * wt[2]) + v[3][e] * wt[3];
       if (MODE == AGG_WARP_ONLY) {
 #pragma unroll
         for (int e = 0; e < E; ++e) acc[q * E + e] = s[e];
       } else if (MODE == AGG_VARIANCE) {
 #pragma unroll
-        for (int e = 0; e < E; ++e) { acc[q * E + e] += s[e]; sq[q * E + e] = fmaf(s[e], s[e], sq[q * E + e]); }
+        for (int e = 0; e < E; ++e) { acc[q * E + e] += s[e]; sq[q * E + e] += s[e] * s[e]; }
       } else {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
@@ -264,11 +252,11 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
     if (MODE == AGG_ADAPTIVE) {
       float dot = 0.f;
 #pragma unroll
-      for (int c = 0; c < C; ++c) dot = fmaf(a.k1[c], sq[c], dot);
-      const float a1 = fmaxf(fmaf(dot, a.s1, a.t1), 0.f);
-      const float wv = fmaxf(fmaf(a1, a.s2, a.t2), 0.f) + 1.f;
+      for (int c = 0; c < C; ++c) dot += a.k1[c] * sq[c];
+      const float a1 = fmaxf(dot * a.s1 + a.t1, 0.f);
+      const float wv = fmaxf(a1 * a.s2 + a.t2, 0.f) + 1.f;
 #pragma unroll
-      for (int c = 0; c < C; ++c) acc[c] = fmaf(wv, sq[c], acc[c]);
+      for (int c = 0; c < C; ++c) acc[c] += wv * sq[c];
     }
   };
   auto finish = [&](int d, float* acc, float* sq) {
@@ -309,9 +297,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
 #pragma unroll
       for (int v = 0; v < NVC; ++v) {
         const float* m = cam + v * 12;
-        rx[v] = ray3(m[0], m[1], m[2], fx, fy);
-        ry[v] = ray3(m[3], m[4], m[5], fx, fy);
-        rz[v] = ray3(m[6], m[7], m[8], fx, fy);
+        rx[v] = m[0] * fx + m[1] * fy + m[2];
+        ry[v] = m[3] * fx + m[4] * fy + m[5];
+        rz[v] = m[6] * fx + m[7] * fy + m[8];
         tx[v] = m[9];
         ty[v] = m[10];
         tz[v] = m[11];
@@ -323,7 +311,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
 #pragma unroll
       for (int v = 0; v < NVC; ++v) {
         const float* g = gcam + v * 12;
-        const float e[6] = {ray3(g[0], g[1], g[2], fx, fy), ray3(g[3], g[4], g[5], fx, fy), ray3(g[6], g[7], g[8], fx, fy),
+        const float e[6] = {g[0] * fx + g[1] * fy + g[2], g[3] * fx + g[4] * fy + g[5], g[6] * fx + g[7] * fy + g[8],
                             g[9], g[10], g[11]};
         const float h[6] = {rx[v], ry[v], rz[v], tx[v], ty[v], tz[v]};
 #pragma unroll
@@ -336,18 +324,18 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
     auto taps = [&](int v, float hyp) {
       float qx, qy, qz;
       if constexpr (NVC > 0) {
-        qx = fmaf(rx[v], hyp, tx[v]), qy = fmaf(ry[v], hyp, ty[v]), qz = fmaf(rz[v], hyp, tz[v]);
+        qx = rx[v] * hyp + tx[v], qy = ry[v] * hyp + ty[v], qz = rz[v] * hyp + tz[v];
       } else {
         const float* m = cam + v * 12;
-        const float vx = ray3(m[0], m[1], m[2], fx, fy);
-        const float vy = ray3(m[3], m[4], m[5], fx, fy);
-        const float vz = ray3(m[6], m[7], m[8], fx, fy);
-        qx = fmaf(vx, hyp, m[9]), qy = fmaf(vy, hyp, m[10]), qz = fmaf(vz, hyp, m[11]);
+        const float vx = m[0] * fx + m[1] * fy + m[2];
+        const float vy = m[3] * fx + m[4] * fy + m[5];
+        const float vz = m[6] * fx + m[7] * fy + m[8];
+        qx = vx * hyp + m[9], qy = vy * hyp + m[10], qz = vz * hyp + m[11];
       }
       // g = (q/qz) / ((W-1)/2) - 1 and ix = ((g + 1) W - 1) / 2 fold to ix = (q/qz) W/(W-1) - 1/2:
       // one reciprocal instead of four IEEE divisions (coordinates agree to ~1 ulp)
       const float iz = __builtin_amdgcn_rcpf(qz);
-      return bilinear_taps(a.h, a.w, rec, src_coord(qx, iz, kx), src_coord(qy, iz, ky));
+      return bilinear_taps(a.h, a.w, rec, qx * iz * kx - 0.5f, qy * iz * ky - 0.5f);
     };
     auto issue = [&](int v, const Taps& t, uint4* rv, float* wt) {
       __amdgpu_buffer_rsrc_t r;
@@ -404,12 +392,12 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
       init(acc, sq);
       for (int j = 1; j < nviews; ++j) {
         const float* m = cam + (j - 1) * 12;
-        const float rx = ray3(m[0], m[1], m[2], fx, fy);
-        const float ry = ray3(m[3], m[4], m[5], fx, fy);
-        const float rz = ray3(m[6], m[7], m[8], fx, fy);
-        const float qx = fmaf(rx, hyp, m[9]), qy = fmaf(ry, hyp, m[10]), qz = fmaf(rz, hyp, m[11]);
+        const float rx = m[0] * fx + m[1] * fy + m[2];
+        const float ry = m[3] * fx + m[4] * fy + m[5];
+        const float rz = m[6] * fx + m[7] * fy + m[8];
+        const float qx = rx * hyp + m[9], qy = ry * hyp + m[10], qz = rz * hyp + m[11];
         const float iz = __builtin_amdgcn_rcpf(qz);
-        const Taps t = bilinear_taps(a.h, a.w, rec, src_coord(qx, iz, kx), src_coord(qy, iz, ky));
+        const Taps t = bilinear_taps(a.h, a.w, rec, qx * iz * kx - 0.5f, qy * iz * ky - 0.5f);
         const __amdgpu_buffer_rsrc_t r = make_rsrc(a.feats[j], fbytes);
         uint4 rv[4 * NQ];
 #pragma unroll
@@ -505,28 +493,28 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
     for (int k = 0; k < 4; ++k) Rec16<T>::unpack(rv[k], v[k]);
     float s[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) s[e] = bilerp(v[0][e], v[1][e], v[2][e], v[3][e], wt);
+    for (int e = 0; e < E; ++e) s[e] = ((v[0][e] * wt[0] + v[1][e] * wt[1]) + v[2][e] * wt[2]) + v[3][e] * wt[3];
     if (MODE == AGG_WARP_ONLY) {
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[e] = s[e];
     } else if (MODE == AGG_VARIANCE) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) { acc[e] += s[e]; sq[e] = fmaf(s[e], s[e], sq[e]); }
+      for (int e = 0; e < E; ++e) { acc[e] += s[e]; sq[e] += s[e] * s[e]; }
     } else {
       float dot = 0.f;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const float df = ref[e] - s[e];
         sq[e] = df * df;
-        dot = fmaf(kq[e], sq[e], dot);
+        dot += kq[e] * sq[e];
       }
       dot += dpp_xor1(dot);
       if (S >= 4) dot += dpp_xor2(dot);
       if (S == 8) dot += swz_xor4(dot);
-      const float a1 = fmaxf(fmaf(dot, a.s1, a.t1), 0.f);
-      const float wv = fmaxf(fmaf(a1, a.s2, a.t2), 0.f) + 1.f;
+      const float a1 = fmaxf(dot * a.s1 + a.t1, 0.f);
+      const float wv = fmaxf(a1 * a.s2 + a.t2, 0.f) + 1.f;
 #pragma unroll
-      for (int e = 0; e < E; ++e) acc[e] = fmaf(wv, sq[e], acc[e]);
+      for (int e = 0; e < E; ++e) acc[e] += wv * sq[e];
     }
   };
   auto finish = [&](int d, float* acc, float* sq) {
@@ -560,9 +548,9 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
 #pragma unroll
     for (int v = 0; v < NVC; ++v) {
       const float* m = cam + v * 12;
-      rx[v] = ray3(m[0], m[1], m[2], fx, fy);
-      ry[v] = ray3(m[3], m[4], m[5], fx, fy);
-      rz[v] = ray3(m[6], m[7], m[8], fx, fy);
+      rx[v] = m[0] * fx + m[1] * fy + m[2];
+      ry[v] = m[3] * fx + m[4] * fy + m[5];
+      rz[v] = m[6] * fx + m[7] * fy + m[8];
       tx[v] = m[9];
       ty[v] = m[10];
       tz[v] = m[11];
@@ -572,16 +560,16 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
   auto taps = [&](int v, float hyp) {
     float qx, qy, qz;
     if constexpr (NVC > 0) {
-      qx = fmaf(rx[v], hyp, tx[v]), qy = fmaf(ry[v], hyp, ty[v]), qz = fmaf(rz[v], hyp, tz[v]);
+      qx = rx[v] * hyp + tx[v], qy = ry[v] * hyp + ty[v], qz = rz[v] * hyp + tz[v];
     } else {
       const float* m = cam + v * 12;
-      const float vx = ray3(m[0], m[1], m[2], fx, fy);
-      const float vy = ray3(m[3], m[4], m[5], fx, fy);
-      const float vz = ray3(m[6], m[7], m[8], fx, fy);
-      qx = fmaf(vx, hyp, m[9]), qy = fmaf(vy, hyp, m[10]), qz = fmaf(vz, hyp, m[11]);
+      const float vx = m[0] * fx + m[1] * fy + m[2];
+      const float vy = m[3] * fx + m[4] * fy + m[5];
+      const float vz = m[6] * fx + m[7] * fy + m[8];
+      qx = vx * hyp + m[9], qy = vy * hyp + m[10], qz = vz * hyp + m[11];
     }
     const float iz = __builtin_amdgcn_rcpf(qz);
-    return bilinear_taps(a.h, a.w, rec, src_coord(qx, iz, kx), src_coord(qy, iz, ky));
+    return bilinear_taps(a.h, a.w, rec, qx * iz * kx - 0.5f, qy * iz * ky - 0.5f);
   };
   auto issue = [&](int v, const Taps& t, uint4* rv, float* wt) {
     __amdgpu_buffer_rsrc_t r;
@@ -629,281 +617,6 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
 #endif
 }
 
-// Plane-sweep form of the channel-split warp: S = C * sizeof(T) / 16 lanes per voxel as in
-// warp_split_kernel, but a block owns a tile of 8 x TC reference pixels over ALL depth planes and, for each chunk of K
-// planes and each source view, first stages the source footprint of the tile -- the pixels any of its samples can touch
-// -- in LDS with coalesced 16-byte loads, then bilinear-samples it with per-lane 16-byte LDS reads (no wide broadcast
-// reads) instead of 4 gathers per lane and sample through the texture addresser. The footprint of (chunk, view) is the
-// bounding box of the tile's 4 corner pixels projected at the chunk's smallest and largest hypothesis of the tile (every
-// sample lies on its pixel's epipolar segment between those two depths, so inside the hull of those 8 points), widened
-// by one pixel and clipped to the image. At stage 1 (one depth per plane, models/module.py:1003-1010) it is a
-// compact strip; a footprint beyond the LDS budget (noisy per-pixel hypotheses) makes that (chunk, view) gather from
-// global memory as warp_split does. The footprint of the next (chunk, view) is loaded into registers while the current
-// one is sampled (two LDS buffers, one barrier per (chunk, view)). Same sampling arithmetic, reduction and view order
-// as warp_split_kernel: bitwise its results.
-constexpr int kSweepPieces = 6;  // 16-byte footprint pieces per thread and buffer (24 KB per buffer)
-
-template <typename T, int C, int MODE, int K>
-__global__ __launch_bounds__(256) void warp_sweep_kernel(const WarpArgs a, const float* __restrict__ cams, int tiles_x,
-                                                         int tiles_y) {
-  constexpr int E = Stor<T>::E, S = C / E, PPB = 256 / S, TR = 8, TC = PPB / TR;
-  constexpr uint32_t rec = C * sizeof(T);
-  constexpr int NP = kSweepPieces, FPX = NP * 256 / S;  // footprint capacity in pixel records
-  static_assert(S == 2 || S == 4 || S == 8, "channel-split lanes");
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint4* fbuf = reinterpret_cast<uint4*>(smem);                         // 2 x FPX x S pieces
-  float* red = reinterpret_cast<float*>(fbuf + 2 * FPX * S);            // [chunk][wave][min, max]
-
-  const int nblk = tiles_x * tiles_y * a.B;
-  const int q8 = nblk / 8, r8 = nblk % 8, xcd = blockIdx.x % 8;
-  int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
-  const int tx = L % tiles_x; L /= tiles_x;
-  const int ty = L % tiles_y;
-  const int b = L / tiles_y;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int q = tid & (S - 1), i = tid / S;
-  const int xl = tx * TC + i % TC, yl = ty * TR + i / TC;
-  const bool pv = xl < a.w && yl < a.rows;  // lanes past the computed rows sample a valid pixel and store nothing
-  const int x = pv ? xl : a.w - 1, y = a.y0 + (pv ? yl : a.rows - 1);
-  const int p = (y - a.y0) * a.w + x;
-  const float fx = (float)x, fy = (float)y;
-  const float kx = (float)a.w / (float)(a.w - 1), ky = (float)a.h / (float)(a.h - 1);
-  const int hw = a.h * a.w;
-  const uint32_t bbytes = (uint32_t)hw * rec, sb = (uint32_t)b * bbytes, qoff = (uint32_t)q * 16u;
-  const long long fbytes = (long long)a.B * bbytes;
-  const float* __restrict__ cam = cams + (size_t)b * (a.N - 1) * 12;
-  const int nv = a.N - 1, NC = (a.D + K - 1) / K;
-  auto vox_of = [&](int d) { return (((size_t)b * a.D + d) * a.out_rows + a.out_y) * a.w + p; };
-
-  float ref[E];
-  if (MODE != AGG_WARP_ONLY) {
-    const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.feats[0], fbytes);
-    Rec16<T>::unpack(__builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r0, (uint32_t)(y * a.w + x) * rec + qoff, sb, 0)),
-                     ref);
-  }
-  float kq[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    float k = a.k1[e];
-#pragma unroll
-    for (int j = 1; j < S; ++j) k = q == j ? a.k1[j * E + e] : k;
-    kq[e] = k;
-  }
-  const float inv_n = 1.f / (float)a.N, inv_n1 = 1.f / (float)(a.N - 1);
-
-  // hypothesis range of the tile per chunk: lane min / max -> wave (xor shuffles) -> LDS, one barrier for all chunks
-  for (int c = 0; c < NC; ++c) {
-    float lo = 3.4e38f, hi = -3.4e38f;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int d = c * K + k;
-      if (d < a.D) {
-        const float h = a.hyps[vox_of(d)];
-        lo = fminf(lo, h);
-        hi = fmaxf(hi, h);
-      }
-    }
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) {
-      lo = fminf(lo, __shfl_xor(lo, m));
-      hi = fmaxf(hi, __shfl_xor(hi, m));
-    }
-    if (lane == 0) {
-      red[(c * 4 + wave) * 2] = lo;
-      red[(c * 4 + wave) * 2 + 1] = hi;
-    }
-  }
-  __syncthreads();
-
-  // footprint of (chunk c, view v): origin (bx0, by0), width bw, rows bh (bw * bh <= FPX), or fits = false
-  struct Box {
-    int bx0, by0, bw, bh;
-    bool fits;
-  };
-  const int tx0 = tx * TC, ty0 = a.y0 + ty * TR;
-  const int tx1 = min(tx0 + TC - 1, a.w - 1), ty1 = min(ty0 + TR - 1, a.y0 + a.rows - 1);
-  auto box = [&](int c, int v) {
-    float zlo = red[c * 8], zhi = red[c * 8 + 1];
-#pragma unroll
-    for (int w = 1; w < 4; ++w) {
-      zlo = fminf(zlo, red[(c * 4 + w) * 2]);
-      zhi = fmaxf(zhi, red[(c * 4 + w) * 2 + 1]);
-    }
-    const float* m = cam + v * 12;
-    float xmin = 3.4e38f, xmax = -3.4e38f, ymin = 3.4e38f, ymax = -3.4e38f;
-    bool ok = true;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float cx = (float)((k & 1) ? tx1 : tx0), cy = (float)((k & 2) ? ty1 : ty0), z = (k & 4) ? zhi : zlo;
-      const float X = (m[0] * cx + m[1] * cy + m[2]) * z + m[9];
-      const float Y = (m[3] * cx + m[4] * cy + m[5]) * z + m[10];
-      const float Z = (m[6] * cx + m[7] * cy + m[8]) * z + m[11];
-      ok = ok && Z > 1e-6f;
-      const float iz = 1.f / Z;
-      const float ix = X * iz * kx - 0.5f, iy = Y * iz * ky - 0.5f;
-      xmin = fminf(xmin, ix); xmax = fmaxf(xmax, ix);
-      ymin = fminf(ymin, iy); ymax = fmaxf(ymax, iy);
-    }
-    Box r;
-    // one pixel of margin beyond the bilinear corners (the corner projections and the samples round differently)
-    ok = ok && xmin > -1e6f && xmax < 1e6f && ymin > -1e6f && ymax < 1e6f;  // also false for NaN
-    const int x0 = ok ? max((int)floorf(xmin) - 1, 0) : 0, x1 = ok ? min((int)floorf(xmax) + 2, a.w - 1) : -1;
-    const int y0 = ok ? max((int)floorf(ymin) - 1, 0) : 0, y1 = ok ? min((int)floorf(ymax) + 2, a.h - 1) : -1;
-    r.bx0 = x0;
-    r.by0 = y0;
-    r.bw = max(x1 - x0 + 1, 0);
-    r.bh = max(y1 - y0 + 1, 0);
-    r.fits = ok && r.bw * r.bh <= FPX;
-    return r;
-  };
-  uint4 pr[NP];
-  auto fload = [&](const Box& bx, int v) {
-    const __amdgpu_buffer_rsrc_t r = make_rsrc(a.feats[v + 1], fbytes);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int idx = tid + 256 * j, pix = idx / S, ch = idx - pix * S;
-      const int row = pix / max(bx.bw, 1), col = pix - row * max(bx.bw, 1);
-      const bool ok = bx.fits && pix < bx.bw * bx.bh;
-      const uint32_t off = ok ? (uint32_t)((bx.by0 + row) * a.w + bx.bx0 + col) * rec + (uint32_t)ch * 16u : kOOB;
-      pr[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, sb, 0));
-    }
-  };
-  auto fstore = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < NP; ++j) fbuf[buf * FPX * S + tid + 256 * j] = pr[j];
-  };
-
-  float acc[K][E], sq[K][E], hk[K];
-  auto reduce = [&](int k, const uint4* rv, const float* wt) {
-    float v4[4][E];
-#pragma unroll
-    for (int c4 = 0; c4 < 4; ++c4) Rec16<T>::unpack(rv[c4], v4[c4]);
-    float s[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) s[e] = bilerp(v4[0][e], v4[1][e], v4[2][e], v4[3][e], wt);
-    if (MODE == AGG_WARP_ONLY) {
-#pragma unroll
-      for (int e = 0; e < E; ++e) acc[k][e] = s[e];
-    } else if (MODE == AGG_VARIANCE) {
-#pragma unroll
-      for (int e = 0; e < E; ++e) { acc[k][e] += s[e]; sq[k][e] = fmaf(s[e], s[e], sq[k][e]); }
-    } else {
-      float dot = 0.f, t[E];
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const float df = ref[e] - s[e];
-        t[e] = df * df;
-        dot = fmaf(kq[e], t[e], dot);
-      }
-      dot += dpp_xor1(dot);
-      if (S >= 4) dot += dpp_xor2(dot);
-      if (S == 8) dot += swz_xor4(dot);
-      const float a1 = fmaxf(fmaf(dot, a.s1, a.t1), 0.f);
-      const float wv = fmaxf(fmaf(a1, a.s2, a.t2), 0.f) + 1.f;
-#pragma unroll
-      for (int e = 0; e < E; ++e) acc[k][e] = fmaf(wv, t[e], acc[k][e]);
-    }
-  };
-
-  const int J = NC * nv;
-  Box cur = box(0, 0);
-  fload(cur, 0);
-  fstore(0);
-  __syncthreads();
-  for (int j = 0; j < J; ++j) {
-    const int c = j / nv, v = j - c * nv;
-    if (v == 0) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int d = min(c * K + k, a.D - 1);
-        hk[k] = a.hyps[vox_of(d)];
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          acc[k][e] = (MODE == AGG_VARIANCE) ? ref[e] : 0.f;
-          sq[k][e] = (MODE == AGG_VARIANCE) ? ref[e] * ref[e] : 0.f;
-        }
-      }
-    }
-    Box nxt;
-    if (j + 1 < J) {
-      const int c1 = (j + 1) / nv;
-      nxt = box(c1, (j + 1) - c1 * nv);
-      fload(nxt, (j + 1) - c1 * nv);
-    }
-    const float* m = cam + v * 12;
-    const float rxv = ray3(m[0], m[1], m[2], fx, fy), ryv = ray3(m[3], m[4], m[5], fx, fy), rzv = ray3(m[6], m[7], m[8], fx, fy);
-    if (cur.fits) {
-      const uint4* fb = fbuf + (j & 1) * FPX * S + q;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const float hyp = hk[k];
-        const float qx = fmaf(rxv, hyp, m[9]), qy = fmaf(ryv, hyp, m[10]), qz = fmaf(rzv, hyp, m[11]);
-        const float iz = __builtin_amdgcn_rcpf(qz);
-        const float ix = src_coord(qx, iz, kx), iy = src_coord(qy, iz, ky);
-        // bilinear_taps' arithmetic, corners read from the footprint (outside the image: 0)
-        const bool inside = ix > -2.f && ix < (float)a.w + 1.f && iy > -2.f && iy < (float)a.h + 1.f;
-        const float cx = inside ? ix : -4.f, cy = inside ? iy : -4.f;
-        const float x0f = floorf(cx), y0f = floorf(cy);
-        const int x0 = (int)x0f, y0 = (int)y0f;
-        const float wx1 = cx - x0f, wx0 = (x0f + 1.f) - cx;
-        const float wy1 = cy - y0f, wy0 = (y0f + 1.f) - cy;
-        const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};
-        uint4 rv[4];
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4) {
-          const int cxx = x0 + (c4 & 1), cyy = y0 + (c4 >> 1);
-          const int fxl = cxx - cur.bx0, fyl = cyy - cur.by0;
-          const bool in = (unsigned)cxx < (unsigned)a.w && (unsigned)cyy < (unsigned)a.h;
-          const bool inb = (unsigned)fxl < (unsigned)cur.bw && (unsigned)fyl < (unsigned)cur.bh;
-          const uint4 vv = fb[(inb ? fyl * cur.bw + fxl : 0) * S];
-          // an in-image corner outside the footprint cannot occur (one pixel of margin); it would read 0
-          rv[c4] = in && inb ? vv : make_uint4(0u, 0u, 0u, 0u);
-        }
-        reduce(k, rv, wt);
-      }
-    } else {
-      const __amdgpu_buffer_rsrc_t r = make_rsrc(a.feats[v + 1], fbytes);
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const float hyp = hk[k];
-        const float qx = fmaf(rxv, hyp, m[9]), qy = fmaf(ryv, hyp, m[10]), qz = fmaf(rzv, hyp, m[11]);
-        const float iz = __builtin_amdgcn_rcpf(qz);
-        const Taps tp = bilinear_taps(a.h, a.w, rec, src_coord(qx, iz, kx), src_coord(qy, iz, ky));
-        uint4 rv[4];
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4)
-          rv[c4] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, tp.off[c4] + qoff, sb, 0));
-        reduce(k, rv, tp.wt);
-      }
-    }
-    if (v == nv - 1) {  // chunk done: the K planes' voxels
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int d = c * K + k;
-        if (d >= a.D || !pv) continue;
-        float o[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          if (MODE == AGG_VARIANCE) {
-            const float mean = acc[k][e] * inv_n;
-            o[e] = sq[k][e] * inv_n - mean * mean;
-          } else if (MODE == AGG_ADAPTIVE) {
-            o[e] = acc[k][e] * inv_n1;
-          } else {
-            o[e] = acc[k][e];
-          }
-        }
-        store_vol<T, E>(reinterpret_cast<T*>(a.out) + vox_of(d) * C + q * E, o);
-      }
-    }
-    if (j + 1 < J) {
-      fstore((j + 1) & 1);  // the buffer sampled two steps ago, released by the last barrier
-      cur = nxt;
-    }
-    __syncthreads();
-  }
-}
-
 // Lanes per voxel the launcher uses for C-channel maps: the channel-split kernel for NHWC maps of 2 or 4 16-byte chunks
 // per pixel when the view pipeline takes the view count (odd N >= 3), else 1 (the one-lane kernel).
 // DAMVS_WARP_SPLIT=0 (one lane per voxel everywhere) and DAMVS_WARP_NO_PIPE=1 (no view pipeline) both give 1, so the
@@ -914,13 +627,6 @@ bool warp_no_pipe() {
     return e && e[0] == '1';
   }();
   return v;
-}
-// Planes per footprint chunk of the plane-sweep kernel, 0 when it does not run: DAMVS_WARP_SWEEP = 4 or 8 (A/B; read
-// per call: tests flip it between launches), default off
-int sweep_k(const WarpArgs& a) {
-  const char* v = getenv("DAMVS_WARP_SWEEP");
-  const int n = v ? atoi(v) : 0;
-  return (n == 4 || n == 8) && a.D >= 1 && a.N >= 2 ? n : 0;
 }
 template <typename T, int C, bool BLK>
 int split_lanes(const WarpArgs& a) {
@@ -942,19 +648,6 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
     return v && v[0] == '1';
   }();
   if constexpr (!BLK && (C * sizeof(T) == 32 || C * sizeof(T) == 64 || C * sizeof(T) == 128)) {
-    if (sweep_k(a) && !warp_no_pipe()) {  // plane-sweep form (footprints in LDS), one block per 8 x TC tile, all planes
-      constexpr int S = C * (int)sizeof(T) / 16, TC = 256 / S / 8;
-      const int tiles_x = (a.w + TC - 1) / TC, tiles_y = (a.rows + 7) / 8;
-      const int K = sweep_k(a);
-      const int NC = (a.D + K - 1) / K;
-      const size_t smem = 2 * (size_t)kSweepPieces * 256 * 16 + (size_t)NC * 32;
-      const dim3 g((unsigned)(tiles_x * tiles_y * a.B));
-      if (K == 4)
-        hipLaunchKernelGGL((warp_sweep_kernel<T, C, MODE, 4>), g, dim3(256), smem, s, a, a.rt, tiles_x, tiles_y);
-      else
-        hipLaunchKernelGGL((warp_sweep_kernel<T, C, MODE, 8>), g, dim3(256), smem, s, a, a.rt, tiles_x, tiles_y);
-      return;
-    }
     if (split_lanes<T, C, BLK>(a) > 1) {
       // DAMVS_WARP_LDS_PAD (A/B): unused dynamic LDS per block, capping the blocks per CU (fewer pixels in flight
       // per XCD, a smaller L2 working set)

@@ -111,15 +111,18 @@ class StageEngine:
         return depth, conf, var, prob
 
     # ---- split entry points (parity tests / sharded execution)
-    def warp_aggregate(self, feats, proj, hyps, rt=None, layout=_capi.DAMVS_LAYOUT_NHWC):
+    def warp_aggregate(self, feats, proj, hyps, rt=None, layout=_capi.DAMVS_LAYOUT_NHWC, out=None):
         """feats: N NHWC (B,h,w,C) tensors, or channel-blocked ones (see block_channels) with
-        layout=DAMVS_LAYOUT_CBLOCK; rt from proj_prepare (computed from proj when None)."""
+        layout=DAMVS_LAYOUT_CBLOCK; rt from proj_prepare (computed from proj when None); out: the (B,D,h,w,C)
+        volume to write (allocated when None)."""
         N = len(feats)
         B, D, h, w = hyps.shape
         C = self.C
         if rt is None:
             rt = proj_prepare(proj)
-        vol = torch.empty(B, D, h, w, C, device=self.device, dtype=self.dtype)
+        vol = torch.empty(B, D, h, w, C, device=self.device, dtype=self.dtype) if out is None else out
+        if vol.shape != (B, D, h, w, C) or vol.dtype != self.dtype or not vol.is_contiguous():
+            raise ValueError("warp_aggregate: out must be a contiguous %s tensor of shape %s" % (self.dtype, (B, D, h, w, C)))
         fptrs = (ctypes.c_void_p * N)(*[f.data_ptr() for f in feats])
         check(self._lib.damvs_warp_aggregate(self.handle, _capi.stream_ptr(self.device), B, N, D, h, w, fptrs, layout,
                                              ptr(rt), ptr(hyps), ptr(vol)))

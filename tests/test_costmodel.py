@@ -49,4 +49,5 @@ def test_fused_head_moves_conv11_and_drops_its_output():
 def test_roofline_time_bound():
     assert CM.roofline_time(8e12, 1.0) == pytest.approx(1.0)
     assert CM.roofline_time(1.0, 2.5e15) == pytest.approx(1.0)
-    assert CM.roofline_time(1.0, 157.3e12, "f32") == pytest.approx(1.0)
+    assert CM.roofline_time(1.0, 2.5e15 / 3, "f32") == pytest.approx(1.0)
+    assert CM.roofline_time(1.0, 157.3e12, "f32_exact") == pytest.approx(1.0)

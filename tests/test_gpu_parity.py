@@ -184,37 +184,6 @@ def test_prob_mfma_vs_oracle(D, h, w, with_init):
     assert np.abs(np_(conf) - ref["photometric_confidence"].numpy())[m].max() < 1e-4
 
 
-@pytest.mark.parametrize("mode", ["adaptive", "variance"])
-@pytest.mark.parametrize("C,dtype", [(32, torch.bfloat16), (16, torch.bfloat16), (32, torch.float32),
-                                     (16, torch.float32), (8, torch.float32)])
-@pytest.mark.parametrize("K", [4, 8])
-def test_warp_sweep_matches_split(K, C, dtype, mode, monkeypatch):
-    """The plane-sweep warp (footprints of 8 x TC pixel tiles staged in LDS per (plane chunk, view)) against the
-    channel-split gather kernel: bitwise, with stage-1 hypotheses (one depth per plane: compact footprints, the LDS
-    path) and with per-pixel noisy ones (footprints beyond the LDS budget: the gather fallback), D not a multiple of K,
-    ragged tiles (h 36, w 44)."""
-    from damvsnet_amd.cascade import CascadeMVSNet
-    from damvsnet_amd.engine import StageEngine
-    s = {32: 0, 16: 1, 8: 2}[C]
-    net = CascadeMVSNet(ndepths=[48, 32, 8], agg_mode=mode)
-    net.load_state_dict(model_state("depthnet_cfgA_" + mode), strict=True)
-    B, N, H, W, D = 2, 5, 36, 44, 12
-    feats, P, hyps = depthnet_inputs(B=B, N=N, H=H, W=W, D=D, stage_idx=s, C=C)
-    g = torch.Generator().manual_seed(C + D)
-    planes = torch.linspace(450.0, 900.0, D).view(1, D, 1, 1).repeat(B, 1, H, W)
-    noisy = hyps * (1.0 + 0.2 * torch.rand(hyps.shape, generator=g))
-    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s] if mode == "adaptive" else None, mode,
-                      dtype, torch.device(DEV))
-    nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(dtype)) for f in feats]
-    for hy in (planes, noisy):
-        monkeypatch.delenv("DAMVS_WARP_SWEEP", raising=False)
-        ref = eng.warp_aggregate(nhwc, cuda(P), cuda(hy)).clone()
-        monkeypatch.setenv("DAMVS_WARP_SWEEP", str(K))
-        got = eng.warp_aggregate(nhwc, cuda(P), cuda(hy)).clone()
-        torch.cuda.synchronize()
-        assert torch.equal(got, ref), float((got.float() - ref.float()).abs().max())
-
-
 @pytest.mark.parametrize("C,dtype", [(32, torch.bfloat16), (16, torch.bfloat16), (32, torch.float32),
                                      (16, torch.float32), (8, torch.float32)])
 def test_warp_aggregate_channel_blocked_layout(C, dtype):
