@@ -871,10 +871,12 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
   raw* abuf = reinterpret_cast<raw*>(smem);  // 2 x AR slots
   const WideHalo<IS, WRT> hg(span);
   const int HP = hg.hp;
-  // bf16 stride 1: the next slice's halo goes to the other of two buffers; otherwise (stride 2: 2.5x the pixels;
-  // fp32: twice the bytes) one buffer, rewritten between two barriers after the slice's last tap
-  constexpr int NHB = IS == 1 && !SP ? 2 : 1;
-  raw* hbuf = abuf + 2 * AR;                 // NHB x HP * SLOTS slots
+  // fp32 (AG, below): A fragments from L1 / L2 per wave, no A buffer in LDS
+  constexpr bool AG = SP;
+  // stride 1: the next slice's halo goes to the other of two buffers; stride 2 (2.5x the pixels) and the fp32 64-channel
+  // block: one buffer, rewritten between two barriers after the slice's last tap
+  constexpr int NHB = IS == 1 && !(SP && WM == 1) ? 2 : 1;  // fp32 64-channel block: its 4-row halo twice = 1 block / CU
+  raw* hbuf = abuf + (AG ? 0 : 2 * AR);      // NHB x HP * SLOTS slots
 
   // logical block = (tile, phase), phase fastest, XCD-contiguous
   const int ntile = tiles_x * tiles_y * a.B;
@@ -995,11 +997,20 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
       x[i] = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(tid + 256 * i) * 16u, so, 0));
     if (!(lc == nsl - 1 && lt == nt - 1)) next(lc, lt);
   };
-  wld(pa);
-  wld(qa);
+  // fp32 (AG): no block-wide A copy. Each wave reads its own 4 cout tiles' A pairs of a chunk from
+  // L1 / L2 (the two waves of a cout half share them through L1), one chunk ahead in alternating register sets, so
+  // the K loop needs no barrier inside a slice: the next slice's halo goes to the other halo buffer after the slice's
+  // last tap and one barrier per 32-channel slice switches buffers (instead of one barrier per chunk). The split form's
+  // 48 MFMAs per chunk and wave cover the loads.
+  if constexpr (!AG) {
+    wld(pa);
+    wld(qa);
+  }
   hload(0);
+  if constexpr (!AG) {
 #pragma unroll
-  for (int i = 0; i < NA; ++i) abuf[tid + 256 * i] = pa[i];
+    for (int i = 0; i < NA; ++i) abuf[tid + 256 * i] = pa[i];
+  }
   hstore(0);
   __syncthreads();
   const int lanepix = wn * IS * hg.pitch + wc + n;
@@ -1054,12 +1065,56 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
   };
   int c = 0, t = 0;
   const int nk = nt * nsl;
-  for (int kk = 0; kk < nk; kk += 2) {  // unrolled by two: the register sets alternate statically
-    step(c, t, pa, qa);
-    if (++t == nt) { t = 0; ++c; }
-    if (kk + 1 < nk) {
-      step(c, t, qa, pa);
+  if constexpr (AG) {
+    const raw* wa = wsrc + wm * 512 + lane;  // the wave's cout half: tile m's hi at m * 128, lo at m * 128 + 64
+    auto aload = [&](F16Pair (&x)[4], int cc, int tt) DAMVS_INLINE {
+      const raw* q = wa + (size_t)(tt * nsl + cc) * cstride;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) x[m] = F16Pair{q[m * 128], q[m * 128 + 64]};
+    };
+    // chunk (c, t) with A in `cur`; chunk (c, t) + 1 (clamped to the last) loaded into `nxt` first
+    auto gstep = [&](const F16Pair (&cur)[4], F16Pair (&nxt)[4]) DAMVS_INLINE {
+      int c1 = c, t1 = t + 1;
+      if (t1 == nt) {
+        t1 = 0;
+        c1 = c + 1 < nsl ? c + 1 : c;
+        t1 = c + 1 < nsl ? 0 : nt - 1;
+      }
+      aload(nxt, c1, t1);
+      const int p0x = s_toff[t] + lanepix;
+      const raw* hb = hbuf + (NHB == 2 ? (c & 1) * HP * SLOTS : 0) + p0x * SLOTS;
+      const int sh = Fm::slot(p0x, g), sl = Fm::slot(p0x, g + 4);
+      F16Pair bf[NGW];
+#pragma unroll
+      for (int j = 0; j < NGW; ++j) bf[j] = F16Pair{hb[j * 16 * SLOTS + sh], hb[j * 16 * SLOTS + sl]};
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int j = 0; j < NGW; ++j) mma_split32(cur[m], bf[j], acc[m][j]);
+      if (t == 0 && c + 1 < nsl) hload(c + 1);
+      if (t == nt - 1 && c + 1 < nsl) {
+        // two buffers: the one slice c - 1 used, which every wave left at the previous slice switch
+        if (NHB == 1) __syncthreads();  // one buffer: every wave is done with slice c's halo
+        hstore(NHB == 2 ? (c + 1) & 1 : 0);
+        __syncthreads();
+      }
       if (++t == nt) { t = 0; ++c; }
+    };
+    F16Pair a0[4], a1[4];
+    aload(a0, 0, 0);
+    for (int kk = 0; kk < nk; kk += 2) {  // unrolled by two: the register sets alternate statically
+      gstep(a0, a1);
+      if (kk + 1 < nk) gstep(a1, a0);
+    }
+    __syncthreads();  // the epilogue's staging tiles overwrite the halo region other waves may still read
+  } else {
+    for (int kk = 0; kk < nk; kk += 2) {  // unrolled by two: the register sets alternate statically
+      step(c, t, pa, qa);
+      if (++t == nt) { t = 0; ++c; }
+      if (kk + 1 < nk) {
+        step(c, t, qa, pa);
+        if (++t == nt) { t = 0; ++c; }
+      }
     }
   }
 
@@ -1205,9 +1260,10 @@ hipError_t launch_wide_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span)
   constexpr bool SP = sizeof(T) == 4;
   constexpr int WRT = WM == 1 && IS == 2 ? 2 : 4 / WM, AR = WM * 256 * WideForm<T>::PL, SLOTS = WideForm<T>::SLOTS;
   const WideHalo<IS, WRT> hg(span);
-  constexpr int NHB = IS == 1 && !SP ? 2 : 1, WPER = IS == 1 ? 7 : 11;
+  constexpr int NHB = IS == 1 && !(SP && WM == 1) ? 2 : 1, WPER = IS == 1 ? 7 : 11;
+  constexpr bool AG = SP;  // fp32: A fragments from L1 / L2, no A buffers in LDS
   if (hg.hp * 4 > WPER * 256) return hipErrorNotSupported;
-  const size_t below_plane = 2 * (size_t)AR * 16 + NHB * (size_t)hg.hp * SLOTS * 16;
+  const size_t below_plane = (AG ? 0 : 2 * (size_t)AR * 16) + NHB * (size_t)hg.hp * SLOTS * 16;
   if (below_plane < 4 * 32 * 68 * 4) return hipErrorNotSupported;  // the epilogue's staging tiles stay below the plane halo
   const int tx = (a.Wq + WC - 1) / WC, ty = (a.Hq + WRT - 1) / WRT;
   const int nsl = (a.c0 + a.c1) / 32;
