@@ -727,19 +727,24 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 && CIN <= 16 ? 2 : 
 // depth 1's from plane z, then depth 2's from plane z + 1, chunks ascending; zero planes outside the volume
 // included): bitwise the same results. Same weights; a 2-slot ring (loads two planes ahead) and, at CIN 32, 8 x 32
 // output windows (TXG 2: twice the MFMAs per plane step).
-template <int CIN, int TXG>
-__global__ __launch_bounds__(256) DAMVS_WAVES(CIN == 32 ? 2 : CIN == 16 ? 3 : 1) void conv3d_zreuse_pair_kernel(const ConvArgs a, int tiles_x, int tiles_y,
-                                                                 int nzc, int zc, int ntiles) {
-  typedef uint4 raw;
-  constexpr int E = 8, KC = 32, CH = CIN / E;
+template <typename T, int CIN, int TXG>
+__global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (CIN == 32 ? 1 : 2) : CIN == 32 ? 2 : CIN == 16 ? 3 : 1) void conv3d_zreuse_pair_kernel(
+    const ConvArgs a, int tiles_x, int tiles_y, int nzc, int zc, int ntiles) {
+  // T = float: the split-f16 form of conv3d_zslide_pair_kernel<float> (ZForm<float>: hi / lo slots, column swizzle; the
+  // 32-K row-pair packing wpack32) on the same input-plane walk: each plane's B fragments (hi and lo) are read from LDS
+  // once for the three output planes they feed, a third of the zslide kernel's LDS reads
+  typedef ZForm<T> Z;
+  typedef typename Z::frag frag;
+  constexpr int PL = Z::PL, ES = sizeof(T);
+  constexpr int E = 8, KC = 32, CH = CIN / E, S = CH * PL;
   constexpr int TX = 16 * TXG, PW = TX + 2, PH = LTH + 2;
-  constexpr int PLANE = PH * PW * CH;  // 16-byte chunks per halo plane
-  constexpr int NLD = (PLANE + 255) / 256;
+  constexpr int PLANE = PH * PW * S;            // 16-byte slots per halo plane
+  constexpr int NLD = (PH * PW * CH + 255) / 256;  // 8-channel chunks per thread per plane
   constexpr int KCHUNKS = 36 * CIN / KC;
   constexpr int NJ = KCHUNKS / 3;  // K chunks per kernel depth
   static_assert(KC % CIN == 0 || CIN % KC == 0, "chunking");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  raw* ring = reinterpret_cast<raw*>(smem);
+  uint4* ring = reinterpret_cast<uint4*>(smem);
 
   const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
   int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
@@ -750,34 +755,43 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(CIN == 32 ? 2 : CIN == 16 ? 3 : 1)
   const int x0 = tx * TX, y0 = ty * LTH, zb = tz * zc;
   const int zend = min(zb + zc, a.Do);
 
-  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * 2);
-  auto load_plane = [&](int iz, raw* v) {
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * ES);
+  auto load_plane = [&](int iz, uint4 (*v)[PL]) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int c = threadIdx.x + i * 256;
       const int row = c / (PW * CH), col = c - row * (PW * CH);
       const int iy = y0 - 1 + row, ix = x0 - 1 + col / CH;
-      const bool ok = c < PLANE && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+      const bool ok = c < PH * PW * CH && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
                       (unsigned)ix < (unsigned)a.Wi;
-      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16u;
-      v[i] = BufIO<bf16_t>::frag(rin, ok ? off : kOOB);
+      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * (16u * PL);
+#pragma unroll
+      for (int h = 0; h < PL; ++h) v[i][h] = BufIO<bf16_t>::frag(rin, ok ? off + 16u * h : kOOB);
     }
   };
-  auto store_plane = [&](int iz, const raw* v) {
-    raw* dst = ring + ((iz + 2) & 1) * PLANE;  // two slots: plane p + 1 goes where plane p - 1 was
+  auto store_plane = [&](int iz, const uint4 (*v)[PL]) {
+    uint4* dst = ring + ((iz + 2) & 1) * PLANE;  // two slots: plane p + 1 goes where plane p - 1 was
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int c = threadIdx.x + i * 256;
-      if (c < PLANE) dst[c] = v[i];
+      if (c >= PH * PW * CH) continue;
+      if constexpr (PL == 1) {
+        dst[c] = v[i][0];
+      } else {
+        const int vox = c / CH, q = c - vox * CH, sw = Z::template zsw<S>(vox % PW);
+        const F16Pair p = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+        dst[vox * S + (q ^ sw)] = p.h;
+        dst[vox * S + ((CH + q) ^ sw)] = p.l;
+      }
     }
   };
-  raw wreg[KCHUNKS];
+  frag wreg[KCHUNKS];
   {
-    const raw* __restrict__ wsrc = reinterpret_cast<const raw*>(a.wpack_pair) + (threadIdx.x & 63);
+    const uint4* __restrict__ wsrc = reinterpret_cast<const uint4*>(PL == 1 ? a.wpack_pair : a.wpack32) + (threadIdx.x & 63);
 #pragma unroll
-    for (int s = 0; s < KCHUNKS; ++s) wreg[s] = wsrc[(size_t)s * 64];
+    for (int s = 0; s < KCHUNKS; ++s) wreg[s] = Z::wload(wsrc, s, 0);
   }
-  raw pa[NLD], pb[NLD];
+  uint4 pa[NLD][PL], pb[NLD][PL];
   load_plane(zb - 1, pa);
   store_plane(zb - 1, pa);
   load_plane(zb, pa);  // stored at the end of step zb - 1; from there on planes are fetched two steps ahead
@@ -786,8 +800,10 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(CIN == 32 ? 2 : CIN == 16 ? 3 : 1)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
   const int gi = (g * E) / CIN, gc = (g * E) % CIN / E;
-  const int lbase = (2 * wave * PW + n) * CH + gc;  // this lane's chunk at tap (dy' = 0, dx = 0)
-  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * 2;
+  // bf16: this lane's chunk at tap (dy' = 0, dx = 0); fp32: its voxel (the chunk and its column swizzle per tap)
+  const int lbase = PL == 1 ? (2 * wave * PW + n) * CH + gc : (2 * wave * PW + n) * S;
+  const int sw0 = Z::template zsw<S>(n), sw1 = Z::template zsw<S>(n + 1), sw2 = Z::template zsw<S>(n + 2);
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * ES;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
   const int co = (g & 1) * 4, r = g >> 1;
   float bias[4];
@@ -804,37 +820,44 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(CIN == 32 ? 2 : CIN == 16 ? 3 : 1)
     for (int xg = 0; xg < TXG; ++xg) {
       const int ox = x0 + 16 * xg + n;
       const bool vok = oy < a.Ho && ox < a.Wo && co < a.Cout;
-      const uint32_t off = (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * a.Cout + co) * 2u;
+      const uint32_t off = (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * a.Cout + co) * (uint32_t)ES;
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        v[i] = acc[xg][i] + bias[i];
+        v[i] = (PL == 1 ? acc[xg][i] : acc[xg][i] * a.wscale) + bias[i];  // 2^-k: exact
         if (a.relu) v[i] = fmaxf(v[i], 0.f);
       }
-      BufIO<bf16_t>::stq(ro, vok ? off : kOOB, v);
+      BufIO<T>::stq(ro, vok ? off : kOOB, v);
     }
   };
   // step p: plane p + 1 (in `cur`) goes to the ring after the MFMAs, plane p + 2 is fetched into `nxt` before them
-  auto step = [&](int p, raw* cur, raw* nxt) {
+  auto step = [&](int p, uint4 (*cur)[PL], uint4 (*nxt)[PL]) {
     if (p + 2 <= zend) load_plane(p + 2, nxt);
-    const raw* src = ring + ((p + 2) & 1) * PLANE + lbase;
+    const uint4* src = ring + ((p + 2) & 1) * PLANE + lbase;
     const bool d0 = p + 1 < zend, d1 = p >= zb && p < zend, d2 = p - 1 >= zb;  // outputs p + 1, p, p - 1 here
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int kt = (j * KC) / CIN, kc = ((j * KC) % CIN) / E;
-      auto toff = [](int t) { return (((t / 3) % 4) * PW + t % 3) * CH; };
-      int off = toff(kt);
+      auto toff = [](int t) { return (((t / 3) % 4) * PW + t % 3) * (PL == 1 ? CH : S); };
+      int off = toff(kt), dx = kt % 3;
       if (KC > CIN) {
         off = gi == 1 ? toff(kt + 1) : off;
         off = gi == 2 ? toff(kt + 2) : off;
         off = gi == 3 ? toff(kt + 3) : off;
+        if (PL == 2) dx = (kt + gi) % 3;
       }
 #pragma unroll
       for (int xg = 0; xg < TXG; ++xg) {
-        const raw bv = src[off + kc + 16 * xg * CH];
-        if (d0) Frag<bf16_t>::mma(wreg[j], bv, an[xg]);           // kernel depth 0
-        if (d1) Frag<bf16_t>::mma(wreg[NJ + j], bv, ac[xg]);      // kernel depth 1
-        if (d2) Frag<bf16_t>::mma(wreg[2 * NJ + j], bv, ap[xg]);  // kernel depth 2
+        frag bv;
+        if constexpr (PL == 1) {
+          bv = src[off + kc + 16 * xg * CH];
+        } else {
+          const int sw = dx == 0 ? sw0 : dx == 1 ? sw1 : sw2;  // +16 columns keep the swizzle
+          bv = Z::bread(src + off + 16 * xg * S, kc + gc, CH, sw);
+        }
+        if (d0) Z::mma(wreg[j], bv, an[xg]);           // kernel depth 0
+        if (d1) Z::mma(wreg[NJ + j], bv, ac[xg]);      // kernel depth 1
+        if (d2) Z::mma(wreg[2 * NJ + j], bv, ap[xg]);  // kernel depth 2
       }
     }
     if (d2) epilogue(p - 1, ap);  // output p - 1 is complete
@@ -880,14 +903,14 @@ hipError_t launch_zslide_pair_t(hipStream_t s, const ConvArgs& a) {
 }
 
 // conv0 on the input-plane walk (conv3d_zreuse_pair_kernel, 2-slot ring)
-template <int CIN, int TXG>
+template <typename T, int CIN, int TXG>
 hipError_t launch_zreuse_pair_t(hipStream_t s, const ConvArgs& a) {
-  constexpr int PLANE = (LTH + 2) * (16 * TXG + 2) * (CIN / 8);
+  constexpr int PLANE = (LTH + 2) * (16 * TXG + 2) * (CIN / 8) * ZForm<T>::PL;
   const size_t smem = 2 * PLANE * 16;
   constexpr int zc = 16;
   const int tx = (a.Wo + 16 * TXG - 1) / (16 * TXG), ty = (a.Ho + LTH - 1) / LTH, nzc = (a.Do + zc - 1) / zc;
   const long long nt = (long long)tx * ty * nzc * a.B;
-  hipLaunchKernelGGL((conv3d_zreuse_pair_kernel<CIN, TXG>), dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc,
+  hipLaunchKernelGGL((conv3d_zreuse_pair_kernel<T, CIN, TXG>), dim3((unsigned)nt), dim3(256), smem, s, a, tx, ty, nzc, zc,
                      (int)nt);
   return hipGetLastError();
 }
@@ -900,7 +923,7 @@ hipError_t launch_lds_pair_t(hipStream_t s, const ConvArgs& a) {
       // (at CIN 8 / 16 its registers cost a wave per SIMD: stage 2 / 3 U-Net 2.09 / 1.89 -> 2.22 / 2.01 ms)
       const char* rv = getenv("DAMVS_CONV0_REUSE");
       const bool reuse = rv ? rv[0] == '1' : CIN == 32;
-      if (reuse) return launch_zreuse_pair_t<CIN, 2>(s, a);
+      if (reuse) return launch_zreuse_pair_t<T, CIN, 2>(s, a);
       if constexpr (CIN == 32) return launch_zslide_pair_t<T, CIN, 1>(s, a);
       else return launch_zslide_pair_t<T, CIN, 2>(s, a);
     }
@@ -908,6 +931,11 @@ hipError_t launch_lds_pair_t(hipStream_t s, const ConvArgs& a) {
     // fp32: the split-f16 z-streamed kernel on the 32-K row-pair packing, A fragments in registers (CIN 32: 36 pairs,
     // 288 VGPRs, with the 92 KB ring one block and one wave per SIMD)
     if (!a.resid && a.wpack32 && !zslide_disabled()) {
+      // DAMVS_CONV0_REUSE (read per call): 1 = the input-plane walk, 0 = the output-plane walk; default: the walk at CIN
+      // 16 / 32 (bitwise equal, test_conv0_reuse_fp32_bitwise)
+      const char* rv = getenv("DAMVS_CONV0_REUSE");
+      const bool reuse = rv ? rv[0] == '1' : CIN >= 16;
+      if (reuse && CIN >= 16) return launch_zreuse_pair_t<T, CIN, 1>(s, a);
       if constexpr (CIN >= 16) return launch_zslide_pair_t<T, CIN, 1>(s, a);  // 8 x 16 windows, no spill
       else return launch_zslide_pair_t<T, CIN, 2>(s, a);
     }

@@ -684,6 +684,28 @@ def test_zslide_split_kernels_vs_tile_kernels_fp32(s, D, H, W, monkeypatch):
     assert err < 2e-5
 
 
+@pytest.mark.parametrize("s,D,H,W", [(0, 48, 40, 72), (1, 24, 40, 72), (1, 32, 32, 80), (0, 40, 24, 104)])
+def test_conv0_reuse_fp32_bitwise(s, D, H, W, monkeypatch):
+    """fp32 conv0 at CIN 32 / 16: the input-plane walk (each plane's split-f16 B fragments read from LDS once for the
+    three output planes they feed) against the output-plane z-streamed kernel: the same MFMA chain per output plane
+    (kernel depth 0, 1, 2; chunks ascending; three split products per chunk), so the logits agree bitwise; D not a
+    multiple of the 16-plane chunk and ragged tiles included."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine
+    C = (32, 16, 8)[s]
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    feats, P, hyps = depthnet_inputs(B=2, N=3, H=H, W=W, D=D, stage_idx=s, C=C)
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.float32,
+                      torch.device(DEV))
+    vol = eng.warp_aggregate([cuda(f.permute(0, 2, 3, 1).contiguous()) for f in feats], cuda(P), cuda(hyps))
+    monkeypatch.setenv("DAMVS_CONV0_REUSE", "1")
+    a = eng.costreg_logits(vol).clone()
+    monkeypatch.setenv("DAMVS_CONV0_REUSE", "0")
+    b = eng.costreg_logits(vol).clone()
+    assert torch.equal(a, b)
+
+
 def test_forward_batch2_matches_batch1():
     """B=2 of the same sample equals B=1 (batch independence of the HIP path)."""
     torch.backends.cudnn.deterministic = True
