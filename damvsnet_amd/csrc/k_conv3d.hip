@@ -1515,7 +1515,10 @@ __global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a
   constexpr int NPIX = PH * PW;         // 8-channel pixels per halo plane
   constexpr int PLANE = PH * PWE * PL;  // 16-byte slots per ring plane
   constexpr int NLD = (NPIX + 255) / 256;
-  constexpr int NS = 5;
+  // ring slots: bf16 5 (planes 2z - 1 .. 2z + 3: the next two planes stored after the MFMAs, one barrier per plane);
+  // fp32 4 (74 KB instead of 92: two blocks per CU instead of one), plane 2z + 3 then goes into the slot of 2z - 1
+  // behind a second barrier
+  constexpr int NS = PL == 1 ? 5 : 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint4* ring = reinterpret_cast<uint4*>(smem);
 
@@ -1634,8 +1637,9 @@ __global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a
       }
       BufIO<T>::stq(ro, ok ? (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * 16 + g * 4) * (uint32_t)ES : kOOB, v);
     }
-    if (more) {  // slots of planes 2z - 3 and 2z - 2, last read before the previous barrier
+    if (more) {  // NS 5: slots of planes 2z - 3 and 2z - 2, last read before the previous barrier
       store_plane(2 * z + 2, na);
+      if (NS == 4) __syncthreads();  // plane 2z + 3 goes where 2z - 1 was, read by this step's MFMAs
       store_plane(2 * z + 3, nb);
     }
     __syncthreads();
@@ -1669,7 +1673,7 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
     constexpr int zc = 8;
     const int tx = (a.Wo + 15) / 16, ty = (a.Ho + 7) / 8, nzc = (a.Do + zc - 1) / zc;
     const long long nt = (long long)tx * ty * nzc * a.B;
-    const size_t smem = sizeof(T) == 2 ? 5 * 17 * 33 * 16 : 5 * 17 * 34 * 32;
+    const size_t smem = sizeof(T) == 2 ? 5 * 17 * 33 * 16 : 4 * 17 * 34 * 32;  // ring slots (NS) x plane
     auto k = conv_s2_c8_zslide_kernel<T>;
     if (smem > 64 * 1024) {
       const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
