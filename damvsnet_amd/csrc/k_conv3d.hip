@@ -935,7 +935,7 @@ hipError_t launch_lds_pair_t(hipStream_t s, const ConvArgs& a) {
       // 16 / 32 (bitwise equal, test_conv0_reuse_fp32_bitwise)
       const char* rv = getenv("DAMVS_CONV0_REUSE");
       const bool reuse = rv ? rv[0] == '1' : CIN >= 16;
-      if (reuse && CIN >= 16) return launch_zreuse_pair_t<T, CIN, 1>(s, a);
+      if (reuse) return launch_zreuse_pair_t<T, CIN, CIN >= 16 ? 1 : 2>(s, a);
       if constexpr (CIN >= 16) return launch_zslide_pair_t<T, CIN, 1>(s, a);  // 8 x 16 windows, no spill
       else return launch_zslide_pair_t<T, CIN, 2>(s, a);
     }

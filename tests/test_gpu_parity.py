@@ -684,9 +684,10 @@ def test_zslide_split_kernels_vs_tile_kernels_fp32(s, D, H, W, monkeypatch):
     assert err < 2e-5
 
 
-@pytest.mark.parametrize("s,D,H,W", [(0, 48, 40, 72), (1, 24, 40, 72), (1, 32, 32, 80), (0, 40, 24, 104)])
+@pytest.mark.parametrize("s,D,H,W", [(0, 48, 40, 72), (1, 24, 40, 72), (1, 32, 32, 80), (0, 40, 24, 104), (2, 8, 48, 96),
+                                     (2, 24, 24, 104)])
 def test_conv0_reuse_fp32_bitwise(s, D, H, W, monkeypatch):
-    """fp32 conv0 at CIN 32 / 16: the input-plane walk (each plane's split-f16 B fragments read from LDS once for the
+    """fp32 conv0 at CIN 32 / 16 / 8: the input-plane walk (each plane's split-f16 B fragments read from LDS once for the
     three output planes they feed) against the output-plane z-streamed kernel: the same MFMA chain per output plane
     (kernel depth 0, 1, 2; chunks ascending; three split products per chunk), so the logits agree bitwise; D not a
     multiple of the 16-plane chunk and ragged tiles included."""
