@@ -62,6 +62,7 @@ struct LayerPlan {
   float* bias = nullptr;
   float wscale = 1.f;  // fp32: 2^-k of the split-f16 weights (split_weights)
   void* wpack32 = nullptr;  // fp32: the z-streamed kernel's 32-K split packing (ConvArgs::wpack32)
+  void* wgat32 = nullptr;   // fp32: the gather kernel's 32-K split packing (ConvArgs::wgat32; may alias wpack32)
 };
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -376,6 +377,7 @@ ConvArgs conv_args(const damvs_stage* st, int li, int B, const Shapes& S, int li
   a.wpack = P.wpack;
   a.wpack_pair = P.wpack_pair;
   a.wpack32 = P.wpack32;
+  a.wgat32 = P.wgat32;
   a.bias = P.bias;
   a.B = B;
   a.Cin = P.cin;
@@ -599,6 +601,16 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
       pack_layer<float>(P32, wf, 8, p32, cvt_f32);
       const std::vector<uint16_t> h = split_weights_blocked(p32, kexp);
       rc = upload(h.data(), h.size() * 2, &P.wpack32);
+      P.wgat32 = P.wpack32;  // the same plain 32-K packing serves the gather kernel
+    } else if (rc == DAMVS_OK && dtype != DAMVS_BF16 && P.cout > 8) {
+      // the gather kernel's 32-K form (conv3d_mfma_kernel<float, MT, false, true>: 16x16x32 f16 split products, twice the
+      // 16-K form's MFMA rate) for the layers that run on it (conv3, conv5, conv6, conv7 and the tile kernels' fallbacks)
+      LayerPlan P32 = P;
+      build_phases(P32, 32);
+      std::vector<float> p32;
+      pack_layer<float>(P32, wf, 8, p32, cvt_f32);
+      const std::vector<uint16_t> h = split_weights_blocked(p32, kexp);
+      rc = upload(h.data(), h.size() * 2, &P.wgat32);
     }
     if (rc == DAMVS_OK && P.kind == DECONV_S2 && P.cout <= 8) {
       build_phases_xpair(P, 4 * E);
@@ -714,6 +726,7 @@ int damvs_stage_destroy(damvs_stage* st) {
   for (auto& P : st->L) {
     if (P.wpack) (void)hipFree(P.wpack);
     if (P.wpack_pair) (void)hipFree(P.wpack_pair);
+    if (P.wgat32 && P.wgat32 != P.wpack32) (void)hipFree(P.wgat32);
     if (P.wpack32) (void)hipFree(P.wpack32);
     if (P.bias) (void)hipFree(P.bias);
   }

@@ -77,6 +77,7 @@ struct ConvArgs {
   const void* wpack;   // packed A fragments, see pack_conv_weights()
   const void* wpack_pair;  // row-pair packing (stride-1, Cout <= 8), nullptr if none
   const void* wpack32;     // fp32: the z-streamed kernel's packing of this layer, 32 K per chunk, split-f16
+  const void* wgat32;      // fp32: the gather kernel's packing at 32 K per chunk (split-f16; phases of build_phases(., 32))
                            // [chunk][hi: 64 lanes][lo: 64 lanes] (x-pair for conv11, row pairs for conv0), or nullptr
   const float* bias;   // [Cout] (folded BN shift)
   int B, Cin, Cout, MT;

@@ -87,12 +87,15 @@ __device__ __forceinline__ void finish4(const ConvArgs& a, __amdgpu_buffer_rsrc_
 // voxel decomposition, range-checked buffer loads for the zero padding.
 // XP: x-parity-pair deconv phases (build_phases_xpair): MFMA row r = (x parity r >> 3, channel r & 7),
 // so lane group g stores channels (g & 1) * 4 .. +3 of output x = 2 qx + (g >> 1).
-template <typename T, int MT, bool XP>
+// K32 (fp32 only): 32 K per chunk as split-f16 16x16x32 MFMAs (8 channels per lane, split when loaded; A pairs from
+// ConvArgs::wgat32, phases re-chunked at 32 K by the launcher): half the MFMA issue of the 16-K form.
+template <typename T, int MT, bool XP, bool K32 = false>
 __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1)) void conv3d_mfma_kernel(const ConvArgs a, int nqblk) {
   constexpr int KG = kGroups;  // 16-voxel column groups per wave
   typedef BufIO<T> IO;
   typedef typename IO::raw raw;
-  constexpr int E = Stor<T>::E;  // input channels per lane per K-chunk
+  static_assert(!K32 || sizeof(T) == 4, "the 32-K split form is fp32 only");
+  constexpr int E = K32 ? 8 : Stor<T>::E;  // input channels per lane per K-chunk
   constexpr int KC = 4 * E;      // K per chunk (4 lane groups)
   constexpr uint32_t ES = sizeof(T);
   // Logical block = (q-block, phase) with the phase fastest, dealt XCD-contiguously: the 8 output
@@ -174,10 +177,39 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
 #pragma unroll
       for (int m = 0; m < MT; ++m) Frag<T>::mma(wf[m], xf[j], acc[j][m]);
   };
-  for (int s = 0; s < ph.kchunks; ++s) {
-    raw wf[MT], xf[KG];
-    load(s, wf, xf);
-    mma(wf, xf);
+  if constexpr (K32) {
+    const uint4* __restrict__ wq = reinterpret_cast<const uint4*>(a.wgat32) + (size_t)ph.w_off * 128 + lane;
+    for (int s = 0; s < ph.kchunks; ++s) {
+      F16Pair wf[MT], xf[KG];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) wf[m] = F16Pair{wq[(size_t)(s * MT + m) * 128], wq[(size_t)(s * MT + m) * 128 + 64]};
+      const bool tv = t < ph.ntaps;
+      const int code = s_tap[tv ? t : 0];
+      const int dz = (code & 0xff) - 8, dy = ((code >> 8) & 0xff) - 8, dx = ((code >> 16) & 0xff) - 8;
+      const int tapoff = dz * HW + dy * a.Wi + dx;
+#pragma unroll
+      for (int j = 0; j < KG; ++j) {
+        const int iz = zs[j] + dz, iy = ys[j] + dy, ix = xs[j] + dx;
+        const bool ok = valid[j] && tv && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+                        (unsigned)ix < (unsigned)a.Wi;
+        const uint32_t off = (uint32_t)((pin[j] + tapoff) * a.Cin + ci) * ES;
+        const float4 lo4 = IO::frag(r0, ok ? off : kOOB), hi4 = IO::frag(r0, ok ? off + 16u : kOOB);
+        xf[j] = split8(lo4, hi4);
+      }
+      ci += rc;
+      t += qt;
+      if (ci >= a.Cin) { ci -= a.Cin; ++t; }
+#pragma unroll
+      for (int j = 0; j < KG; ++j)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) mma_split32(wf[m], xf[j], acc[j][m]);
+    }
+  } else {
+    for (int s = 0; s < ph.kchunks; ++s) {
+      raw wf[MT], xf[KG];
+      load(s, wf, xf);
+      mma(wf, xf);
+    }
   }
 
   if constexpr (XP && DAMVS_DIAG_SKIP_EPI == 0) {
@@ -1707,6 +1739,26 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
     if (a.MT != 1 || a.Cout != 8) return hipErrorInvalidValue;
     hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, true>), grid, dim3(256), 0, s, a, nq);
     return hipGetLastError();
+  }
+  if constexpr (sizeof(T) == 4) {
+    // fp32: the 32-K split form where the layer has its packing (DAMVS_CONV3D_K16=1, read per call: the 16-K form)
+    const char* kv = getenv("DAMVS_CONV3D_K16");
+    if (a.wgat32 && !(kv && kv[0] == '1')) {
+      ConvArgs a2 = a;
+      int w = 0;
+      for (int p = 0; p < a.nphase; ++p) {  // the phases at 32 K per chunk (build_phases(., 32), pack_layer at E 8)
+        a2.ph[p].kchunks = (a.ph[p].ntaps * a.Cin + 31) / 32;
+        a2.ph[p].w_off = w;
+        w += a2.ph[p].kchunks * a.MT;
+      }
+      switch (a.MT) {
+        case 1: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, false, true>), grid, dim3(256), 0, s, a2, nq); break;
+        case 2: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 2, false, true>), grid, dim3(256), 0, s, a2, nq); break;
+        case 4: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 4, false, true>), grid, dim3(256), 0, s, a2, nq); break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
   }
   switch (a.MT) {
     case 1: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, false>), grid, dim3(256), 0, s, a, nq); break;

@@ -707,6 +707,30 @@ def test_conv0_reuse_fp32_bitwise(s, D, H, W, monkeypatch):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("s,D,H,W", [(1, 24, 40, 72), (2, 8, 48, 96), (0, 48, 40, 72)])
+def test_gather_conv3d_k32_vs_k16_fp32(s, D, H, W, monkeypatch):
+    """fp32 gather-kernel layers (conv3 / conv5 / conv6 / conv7 and the tile kernels' fallbacks): the 32-K split form
+    (16x16x32 f16 MFMAs, 8 channels per lane) against the 16-K split form (DAMVS_CONV3D_K16=1) on the same volume, conv1
+    and conv9 on the gather kernel too: different K order, equal to fp32 rounding (U-Net gate 2e-5)."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine
+    C = (32, 16, 8)[s]
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    feats, P, hyps = depthnet_inputs(B=2, N=3, H=H, W=W, D=D, stage_idx=s, C=C)
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.float32,
+                      torch.device(DEV))
+    vol = eng.warp_aggregate([cuda(f.permute(0, 2, 3, 1).contiguous()) for f in feats], cuda(P), cuda(hyps))
+    monkeypatch.setenv("DAMVS_CONV_NO_ZSLIDE", "1")  # conv0 / conv2 off their z-streamed kernels
+    monkeypatch.setenv("DAMVS_DECONV_NO_ZSLIDE", "1")  # conv1 / conv9 onto the gather kernel
+    a = eng.costreg_logits(vol).clone()
+    monkeypatch.setenv("DAMVS_CONV3D_K16", "1")
+    b = eng.costreg_logits(vol).clone()
+    err = rel_max(np_(a), np_(b))
+    print("gather conv3d 32-K vs 16-K stage %d: rel_max %.3e" % (s, err))
+    assert err < 2e-5
+
+
 def test_forward_batch2_matches_batch1():
     """B=2 of the same sample equals B=1 (batch independence of the HIP path)."""
     torch.backends.cudnn.deterministic = True
