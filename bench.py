@@ -47,6 +47,15 @@ SHARD_GUARD_S = 240  # N > 1: seconds the depth-sharded blocks may take before t
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
+def coll_device(device):
+    """Where collective tensors live: the GPU under RCCL ("nccl"), the host under gloo (tests/bench_dryrun.py runs
+    this script's N > 1 path as a CPU gloo job)."""
+    import torch.distributed as dist
+    if dist.is_initialized() and dist.get_backend() != "nccl":
+        return torch.device("cpu")
+    return device
+
+
 def build_model(ndepths, dtype, device, frontend="hip"):
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.weights import synthetic_state_dict, apply_bn_stats
@@ -200,7 +209,7 @@ def sharded_latency(net, H, W, N, device, comm=None, emulate=1, warp="depth", st
             ThreadGroup(emulate).run(lambda c: checked(c, timer if c.rank == 0 else None))
         torch.cuda.synchronize()
     from damvsnet_amd.dist import max_over_ranks
-    el = max_over_ranks(el, device=device) if comm is not None else el
+    el = max_over_ranks(el, device=coll_device(device)) if comm is not None else el
     return {"ms_per_map": round(el / steps * 1e3, 3), "ranks": world, "warp": warp,
             "transport": "rccl" if comm is not None else "threads on one GPU (rehearsal)",
             "bitwise_vs_unsharded": res.get("bitwise_vs_unsharded"),
@@ -220,9 +229,10 @@ def latency_b1(net, imgs, proj, dv, ins, steps=10):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(steps):
-            net(imgs, proj, dv, ins, stage_hook=timer)
+            net(imgs, proj, dv, ins, stage_hook=timer, check_range=False)
         e1.record()
         torch.cuda.synchronize()
+        net.DepthNet.check_range()
     return {"ms_per_map": round(e0.elapsed_time(e1) / steps, 3),
             "ms_per_stage": {k: round(statistics.mean(v), 3) for k, v in timer.per_phase_ms().items()}}
 
@@ -343,18 +353,20 @@ def parity_path(args, nd, device, imgs, proj, dv, ins, world, steps=20, warmup=3
             torch.distributed.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            net(imgs, proj, dv, ins, streams=args.streams)
+        for _ in range(steps):  # the range status accumulates over the steps and is read once after them
+            net(imgs, proj, dv, ins, streams=args.streams, check_range=False)
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
-        elapsed = max_over_ranks(time.perf_counter() - t0, device=device)
+        elapsed = max_over_ranks(time.perf_counter() - t0, device=coll_device(device))
+        net.DepthNet.check_range()  # raises DamvsRangeError if any timed forward produced non-finite maps
     del net
     torch.cuda.empty_cache()
     maps = steps * args.batch * world
     return {"value": round(maps / elapsed, 4), "unit": "depth maps/s", "ms_per_step": round(elapsed / steps * 1e3, 3),
             "steps": steps, "warmup": warmup, "dtype": "f32", "streams": args.streams, "batch_per_gpu": args.batch,
+            "range_status": "ok: every stage of every timed forward finite (damvs_stage_status, read after the steps)",
             "compute": "fp32 storage, fp32 warp / aggregation / regression; every conv product as split-f16 MFMAs "
                        "(x = hi + lo, hi*hi + hi*lo + lo*hi, fp32 accumulation; damvsnet_amd/csrc/damvs_device.h)",
             "gates": "north_star: depth within 1e-3 relative at every pixel on identical inputs "
@@ -444,23 +456,25 @@ def main():
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            net(imgs, proj, dv, ins, streams=args.streams)
+        for _ in range(args.steps):  # the range status accumulates over the steps and is read once after them
+            net(imgs, proj, dv, ins, streams=args.streams, check_range=False)
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        net.DepthNet.check_range()  # raises DamvsRangeError if any timed forward produced non-finite maps
         # attribution pass, one stream (per-phase and per-kernel-group times are not separable when sub-batches
         # overlap): HIP events at the phase boundaries and inside damvs_stage_forward_probed
         timer = StageTimer()
         probes = ProbeRecorder()
         net.DepthNet.probe = probes
         for _ in range(min(args.steps, 5)):
-            net(imgs, proj, dv, ins, stage_hook=timer)
+            net(imgs, proj, dv, ins, stage_hook=timer, check_range=False)
         torch.cuda.synchronize()
+        net.DepthNet.check_range()
         net.DepthNet.probe = None
     from damvsnet_amd.dist import max_over_ranks
-    elapsed = max_over_ranks(elapsed, device=device)
+    elapsed = max_over_ranks(elapsed, device=coll_device(device))
     maps = args.steps * args.batch * world
     if not parity_first and dtype == torch.bfloat16 and not args.no_parity_path:  # every rank takes part (max over ranks)
         pp = parity_path(args, nd, device, imgs, proj, dv, ins, world)
@@ -512,6 +526,7 @@ def main():
                          "isolated_ms_per_launch": round(iso_ms, 4),
                          "isolated_frac": round(alg / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "hot_path_roofline": hp,
+            "range_status": "ok: every stage of every timed forward finite (damvs_stage_status, read after the steps)",
             "mfma_utilisation": pmc_mfma(args.config, args.batch) if native else None,
         }
         if pp is not None:
@@ -544,7 +559,7 @@ def main():
                 err = repr(ex)[:300]
             # every rank leaves the block knowing whether any rank failed (a failure after the last exchange would
             # otherwise go unnoticed by the peers); a failure before an exchange ends at the collective timeout
-            flag = torch.tensor([1 if err else 0], device=device)
+            flag = torch.tensor([1 if err else 0], device=coll_device(device))
             torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.SUM)
             if int(flag.item()):
                 blk = {"error": err or "failed on %d other rank(s)" % int(flag.item()), "failed_ranks": int(flag.item())}

@@ -19,7 +19,8 @@ DAMVS_F32, DAMVS_BF16 = 0, 1
 DAMVS_AGG_ADAPTIVE, DAMVS_AGG_VARIANCE = 0, 1
 DAMVS_LAYOUT_NHWC, DAMVS_LAYOUT_CBLOCK = 0, 1
 ERRORS = {-1: "DAMVS_E_ARG", -2: "DAMVS_E_SHAPE", -3: "DAMVS_E_DTYPE", -4: "DAMVS_E_HIP", -5: "DAMVS_E_NOMEM",
-          -6: "DAMVS_E_WORKSPACE"}
+          -6: "DAMVS_E_WORKSPACE", -7: "DAMVS_E_RANGE"}
+DAMVS_E_RANGE = -7
 
 c_int, c_float, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 
@@ -69,6 +70,7 @@ SIGNATURES = (
     ("damvs_stage_forward_probed", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                            ctypes.POINTER(c_void_p), c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                            c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_void_p))),
+    ("damvs_stage_status", c_int, (c_void_p, c_void_p, c_void_p, c_size_t)),
     ("damvs_proj_prepare", c_int, (c_void_p, c_int, c_int, c_void_p, c_void_p)),
     ("damvs_homo_warp", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                 c_void_p)),
@@ -118,6 +120,10 @@ class DamvsError(RuntimeError):
         self.rc = rc
 
 
+class DamvsRangeError(DamvsError, FloatingPointError):
+    """DAMVS_E_RANGE: a stage forward produced non-finite depth / confidence / variance (damvs_stage_status)."""
+
+
 def load_library(path: str = LIB_PATH):
     """Load and type the HIP library; raises if it has not been built."""
     global _lib
@@ -153,7 +159,8 @@ def load_library(path: str = LIB_PATH):
 
 def check(rc: int):
     if rc != 0:
-        raise DamvsError(rc, _lib.damvs_last_error_string().decode(errors="replace"))
+        msg = _lib.damvs_last_error_string().decode(errors="replace")
+        raise (DamvsRangeError if rc == DAMVS_E_RANGE else DamvsError)(rc, msg)
 
 
 def ptr(t) -> int | None:

@@ -123,7 +123,7 @@ class CascadeMVSNet(nn.Module):
             _SIDE_STREAMS[key] = pool
         return pool[:n]
 
-    def _forward_streams(self, imgs, proj_matrices, depth_values, intrinsics_matrices, nstreams):
+    def _forward_streams(self, imgs, proj_matrices, depth_values, intrinsics_matrices, nstreams, check_range=True):
         """The batch as ``nstreams`` sub-batches of reference views on concurrent HIP streams, merged along the
         batch. Per sample every kernel sees the same inputs as in one batch, so the outputs are bitwise those of
         the single-stream forward (tests/test_gpu_streams.py); the gain is overlap between kernels with different
@@ -143,7 +143,7 @@ class CascadeMVSNet(nn.Module):
             st.wait_stream(main)
             with torch.cuda.stream(st):
                 outs.append(self.forward(part(imgs, a, b), part(proj_matrices, a, b), part(depth_values, a, b),
-                                         part(intrinsics_matrices, a, b)))
+                                         part(intrinsics_matrices, a, b), check_range=False))
 
         # batch-sized outputs allocated on the main stream, each stream copying its rows right after its own
         # forward (the copies overlap the other sub-batches' kernels instead of following all of them)
@@ -175,18 +175,22 @@ class CascadeMVSNet(nn.Module):
                 fill(full, outs[i], a, b, st, set())
         for st in pool:
             main.wait_stream(st)
+        if check_range:  # after every sub-batch is enqueued: one host sync for the whole forward
+            self.DepthNet.check_range()
         return full
 
     def forward(self, imgs, proj_matrices, depth_values, intrinsics_matrices=None, stage_hook=None, depthnet=None,
-                streams=1):
+                streams=1, check_range=True):
         """``depthnet``: optional stage runner (stage_idx, NHWC features, proj, hyps, cost_regularization) -> dict,
         e.g. sharded.DepthShardedDepthNet (one depth map over several GPUs); default: this model's DepthNet.
         ``streams`` > 1 runs the batch as that many sub-batches on concurrent streams (_forward_streams; not with
-        a stage hook or a custom stage runner)."""
+        a stage hook or a custom stage runner). ``check_range``: after the last stage, read every stage's range
+        status (damvs_stage_status, one host sync per forward) and raise damvsnet_amd._capi.DamvsRangeError if any
+        depth / confidence / variance is non-finite -- the fp32 path's split-f16 products hold |x| < 65520 only."""
         if streams > 1 and imgs.shape[0] > 1 and stage_hook is None and depthnet is None and imgs.is_cuda \
                 and not self.refine:
             return self._forward_streams(imgs, proj_matrices, depth_values, intrinsics_matrices,
-                                         min(int(streams), imgs.shape[0]))
+                                         min(int(streams), imgs.shape[0]), check_range)
         if self.refine:
             raise NotImplementedError("refine=True: the reference RefineNet forward is not runnable "
                                       "(models/module.py:602 calls F.cat)")
@@ -231,4 +235,6 @@ class CascadeMVSNet(nn.Module):
             outputs[name] = out
             outputs.update(out)
         hook("end")
+        if check_range and depthnet is None:
+            self.DepthNet.check_range()
         return outputs

@@ -306,7 +306,7 @@ Shapes level_shapes(int D, int h, int w) {
 }
 
 struct Workspace {
-  size_t rt, feat, vol, c[7], logits, total;
+  size_t status, rt, feat, vol, c[7], logits, total;
 };
 
 // c[i] holds conv_i's output for i = 0..6 (conv7/9/11 accumulate in place into c4/c2/c0).
@@ -342,6 +342,8 @@ Workspace plan_ws(const damvs_stage* st, int B, int N, int D, int h, int w) {
                         V / 512 * 8 * b};
   Workspace ws;
   size_t o = 0;
+  ws.status = o;  // the range status word at offset 0 (damvs_stage_status needs no shape)
+  o += align_up(4);
   ws.rt = o;
   o += align_up((size_t)B * (N > 1 ? N - 1 : 1) * 12 * 4);
   ws.feat = o;  // channel-blocked copies of the N feature maps (only when C spans several 16-B chunks)
@@ -765,6 +767,7 @@ int damvs_stage_forward_probed(const damvs_stage* st, void* stream, int B, int N
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   char* ws = reinterpret_cast<char*>(workspace);
   float* rt = reinterpret_cast<float*>(ws + W.rt);
+  int* status = reinterpret_cast<int*>(ws + W.status);
   DAMVS_TRY(hip_check(launch_proj_prepare(s, B, N, proj, rt), "proj_prepare launch"));
   const bool blk = feat_needs_blocking(st);
   const void* fv[kMaxViews];
@@ -791,13 +794,30 @@ int damvs_stage_forward_probed(const damvs_stage* st, void* stream, int B, int N
     DAMVS_TRY(run_unet(st, s, B, D, h, w, ws + W.vol, ws, W, 9));
     DAMVS_TRY(mark(2));
     DAMVS_TRY(run_head(st, s, B, D, h, w, ws + W.c[2], ws + W.c[0], hyps, prob_init, depth, conf, var, prob));
-    return mark(3);
+  } else {
+    DAMVS_TRY(run_unet(st, s, B, D, h, w, ws + W.vol, ws, W));
+    DAMVS_TRY(mark(2));
+    DAMVS_TRY(regress_tail(st, s, B, D, h, w, ws + W.c[0], hyps, prob_init, reinterpret_cast<float*>(ws + W.logits),
+                           depth, conf, var, prob));
   }
-  DAMVS_TRY(run_unet(st, s, B, D, h, w, ws + W.vol, ws, W));
-  DAMVS_TRY(mark(2));
-  DAMVS_TRY(regress_tail(st, s, B, D, h, w, ws + W.c[0], hyps, prob_init, reinterpret_cast<float*>(ws + W.logits), depth,
-                         conf, var, prob));
-  return mark(3);
+  DAMVS_TRY(mark(3));
+  // range check of the outputs (sticky status word, damvs_stage_status), after the last probe: not in the regression's time
+  return hip_check(launch_finite_check(s, depth, conf, var, (long long)B * h * w, status), "finite check launch");
+}
+
+int damvs_stage_status(const damvs_stage* st, void* stream, const void* workspace, size_t workspace_bytes) {
+  if (!st || !workspace) return fail(DAMVS_E_ARG, "null argument");
+  if (workspace_bytes < 4) return fail(DAMVS_E_WORKSPACE, "workspace %zu bytes", workspace_bytes);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int v = 0;
+  DAMVS_TRY(hip_check(hipMemcpyAsync(&v, workspace, 4, hipMemcpyDeviceToHost, s), "status copy"));
+  DAMVS_TRY(hip_check(hipMemsetAsync(const_cast<void*>(workspace), 0, 4, s), "status clear"));
+  DAMVS_TRY(hip_check(hipStreamSynchronize(s), "hipStreamSynchronize"));
+  if (v != 0)
+    return fail(DAMVS_E_RANGE,
+                "non-finite depth / confidence / variance in the stage output: an activation beyond the f16 range of "
+                "the fp32 path's split-f16 products (|x| >= 65520) or non-finite inputs");
+  return DAMVS_OK;
 }
 
 int damvs_proj_prepare(void* stream, int B, int N, const float* proj, float* rt) {

@@ -183,6 +183,11 @@ __device__ __forceinline__ void store_vec(T* p, const float* v) {
 #define DAMVS_WAVES(n) __attribute__((amdgpu_waves_per_eu(n)))
 #endif
 
+// ReLU with torch.relu's NaN semantics (NaN stays NaN; fmaxf(NaN, 0) would give 0 under IEEE maxNum). A NaN from an
+// out-of-range split-f16 product (|x| >= 65520, the fp32 path) thus reaches the stage outputs, where the range check
+// of damvs_stage_forward reports it (damvs_stage_status) instead of a finite wrong depth.
+__device__ __forceinline__ float relu(float x) { return x < 0.f ? 0.f : x; }
+
 // For kernel-local lambdas with large bodies used at two or more call sites: hipcc may otherwise emit them as
 // functions, the by-reference closure then lives in scratch and LDS pointers reaching them turn generic (flat
 // stores). conv2d_wide_kernel<float> at input stride 2 had exactly that (512 B of scratch, flat halo stores:

@@ -129,6 +129,8 @@ struct Conv2dArgs {
 
 // ---------------------------------------------------------------- launchers (return hipError_t)
 hipError_t launch_proj_prepare(hipStream_t s, int B, int N, const float* proj, float* rt);
+// status[0] = 1 when any of the n floats of a, b or c is non-finite (sticky: damvs_stage_status clears it)
+hipError_t launch_finite_check(hipStream_t s, const float* a, const float* b, const float* c, long long n, int* status);
 hipError_t launch_hyp_linear(hipStream_t s, int B, int D, int h, int w, const float* dv, int Dv, float* out);
 hipError_t launch_hyp_refine(hipStream_t s, int B, int D, int H, int W, int scale, const float* pd,
                              const float* pv, int hp, int wp, float* out);

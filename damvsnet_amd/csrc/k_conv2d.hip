@@ -71,7 +71,7 @@ __device__ __forceinline__ void tail4(const Conv2dArgs& a, int b, int oy, int ox
   }
   if (a.relu) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = fmaxf(r[i], 0.f);
+    for (int i = 0; i < 4; ++i) r[i] = relu(r[i]);
   }
   if (a.res_post) {
     const int up = a.post_up;  // 1, or 2 for a nearest-x2 upsampled source of half resolution
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
       if (a.res_pre) Vox8<T>::add(rpre, ok ? (uint32_t)(pout[j] * 8) * ES : kOOB, r);
       if (a.relu) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) r[i] = fmaxf(r[i], 0.f);
+        for (int i = 0; i < 8; ++i) r[i] = relu(r[i]);
       }
       if (a.res_post) Vox8<T>::add(rpost, ok ? (uint32_t)(ppost[j] * 8) * ES : kOOB, r);
       Vox8<T>::store(ro, ok ? (uint32_t)(pout[j] * 8) * ES : kOOB, r);
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
       if (a.res_pre) IO::addq(qpre[m], r);
       if (a.relu) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] = fmaxf(r[i], 0.f);
+        for (int i = 0; i < 4; ++i) r[i] = relu(r[i]);
       }
       if (a.res_post) IO::addq(qpost[m], r);
       const uint32_t off = (uint32_t)(pout[j] * a.cout + (mt0 + m) * 16 + g * 4) * ES;
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) != 2 ? 1 : CIN == 32 ? 
       if (a.res_pre) IO::addq(qpre[m], r);
       if (a.relu) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] = fmaxf(r[i], 0.f);
+        for (int i = 0; i < 4; ++i) r[i] = relu(r[i]);
       }
       if (a.res_post) IO::addq(qpost[m], r);
       const uint32_t off = (uint32_t)(pout * a.cout + m * 16 + g * 4) * ES;
@@ -702,7 +702,7 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
       if (a.res_pre) IO::addq(qpre[m], r);
       if (a.relu) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] = fmaxf(r[i], 0.f);
+        for (int i = 0; i < 4; ++i) r[i] = relu(r[i]);
       }
       if (a.res_post) IO::addq(qpost[m], r);
       const uint32_t off = (uint32_t)(pout * a.cout + (mt0 + m) * 16 + g * 4) * ES;
@@ -853,15 +853,19 @@ template <> struct WideForm<float> {
 // 64 output channels (cout 64 layers) x a 4 x 64 q-tile, the 4 waves one q-row each; WM = 1 at input stride 2 (the
 // 4-row halo would not fit): a 2 x 64 q-tile, the 4 waves a 2 x 2 grid (q-row, 32-column half).
 // T = float: the fp32 parity path's form (one halo buffer, rewritten between two barriers after a slice's last tap).
-template <typename T, bool TWO, int IS, int WM>
+// RS (fp32, input stride 1, 128-channel block, taps spanning <= 3 pixels, >= 4 taps per phase): the rolling K loop
+// below (A one chunk ahead, B of the next chunk read as each N-group's MFMAs finish, the next slice's halo in two
+// 8-channel pieces per tap for the first taps of a slice, one barrier per slice).
+template <typename T, bool TWO, int IS, int WM, bool RS = false>
 __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1) : IS == 1 ? 3 : 2) void conv2d_wide_kernel(
     const Conv2dArgs a, int tiles_x, int tiles_y, int nsl, int dmin, int span) {
   typedef uint4 raw;
   typedef WideForm<T> Fm;
   constexpr bool SP = sizeof(T) == 4;
+  static_assert(!RS || (SP && IS == 1 && WM == 2), "rolling K loop: fp32, input stride 1, 128-channel block");
   constexpr int PL = Fm::PL, SLOTS = Fm::SLOTS;
   constexpr uint32_t ES = sizeof(T);
-  constexpr int WPER = IS == 1 ? 7 : 11;  // 8-channel halo pieces per thread: up to 448 / 704 pixels
+  constexpr int WPER = RS ? 5 : IS == 1 ? 7 : 11;  // 8-channel halo pieces per thread: up to 320 / 448 / 704 pixels
   constexpr bool HALFW = WM == 1 && IS == 2;     // waves of 32 q-columns
   constexpr int NGW = HALFW ? 2 : 4;             // 16-column N-groups per wave
   constexpr int WRT = HALFW ? 2 : 4 / WM;        // q-tile rows
@@ -1065,7 +1069,125 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
   };
   int c = 0, t = 0;
   const int nk = nt * nsl;
-  if constexpr (AG) {
+  if constexpr (RS) {
+    // Rolling K loop. Per chunk (slice c, tap t) and wave: wait for the previous chunk's loads, store the halo pieces
+    // they brought (next slice, other buffer), at a slice's last tap one barrier (every piece of the next slice is in
+    // LDS, and every wave's reads of this slice were issued), then issue the next chunk's A pairs (buffer loads at an
+    // SGPR chunk offset) and this tap's piece loads, and run the 48 MFMAs N-group by N-group, each group's B pair
+    // re-read for the next chunk (its own slice and tap) as soon as its 12 MFMAs are issued. Pieces of slice c + 1:
+    // 0, 1 loaded at tap 0, 2, 3 at tap 1, 4 at tap 2, each stored one tap later (5 pieces = 1280 8-channel chunks >=
+    // the 4 x 264 of a span-3 halo). The last slice re-reads itself into the idle buffer (harmless, branch-free).
+    // Per accumulator the MFMA sequence is the AG loop's (chunks in (slice, tap) order, mma_split32), so the results
+    // are bitwise equal.
+    const int ltoff = lane < nt ? hg.pix(ph.tap[lane][0] - dmin, ph.tap[lane][1] - dmin) : 0;  // lane t: tap t's offset
+    const uint32_t av0 = (uint32_t)(wm * 512 + lane) * 16u, av1 = av0 + 4096u;  // tile m: hi at m * 2048, lo + 1024
+    auto aload = [&](F16Pair (&x)[4], int cc, int tt) DAMVS_INLINE {
+      const uint32_t so = wbase + (uint32_t)(tt * nsl + cc) * cbytes;
+      auto ld = [&](uint32_t v) DAMVS_INLINE { return __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(rw, v, so, 0)); };
+      x[0] = F16Pair{ld(av0), ld(av0 + 1024u)};
+      x[1] = F16Pair{ld(av0 + 2048u), ld(av0 + 3072u)};
+      x[2] = F16Pair{ld(av1), ld(av1 + 1024u)};
+      x[3] = F16Pair{ld(av1 + 2048u), ld(av1 + 3072u)};
+    };
+    raw pr[2][2];  // two halo pieces in flight (fp32: two 16-byte loads each)
+    auto pload = [&](int k, int slot, int cc) DAMVS_INLINE {
+      const bool second = TWO && cc * 32 >= a.c0;
+      const int cs = second ? a.c1 : a.c0, cb = second ? cc * 32 - a.c0 : cc * 32;
+      const uint32_t off = hpix[k] >= 0 ? (uint32_t)(hpix[k] * cs + cb + hch[k]) * ES : kOOB;
+      const __amdgpu_buffer_rsrc_t r = (TWO && second) ? r1 : r0;
+      pr[slot][0] = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+      pr[slot][1] = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(r, off == kOOB ? kOOB : off + 16u, 0, 0));
+    };
+    // a piece past the halo goes to 8 spare slots behind the plane halo (launch_wide_t reserves them): no branch, so
+    // the stores stay in the step's straight-line code
+    const int spare = NHB * HP * SLOTS + (HP * 4 + 15) / 16;
+    auto pstore = [&](int k, int slot, int bi) DAMVS_INLINE {
+      const bool ok = hsl[k] >= 0;
+      const int p = ok ? hsl[k] / SLOTS : 0, q = hch[k] >> 3;
+      const F16Pair v = split8(__builtin_bit_cast(float4, pr[slot][0]), __builtin_bit_cast(float4, pr[slot][1]));
+      raw* hb = hbuf + (ok ? bi * HP * SLOTS + hsl[k] : spare);
+      hb[Fm::slot(p, q)] = v.h;
+      hb[Fm::slot(p, q + 4)] = v.l;
+    };
+    // B pair of N-group j of chunk (cc, tt): halo buffer cc & 1, pixel tap offset + the lane's column (+ 16 j keeps
+    // the swizzle)
+    int bh = 0, bl = 0;
+    auto baddr = [&](int cc, int tt) DAMVS_INLINE {
+      const int p0x = __builtin_amdgcn_readlane(ltoff, tt) + lanepix;
+      const int base = ((cc & 1) * HP + p0x) * SLOTS;
+      bh = base + Fm::slot(p0x, g);
+      bl = base + Fm::slot(p0x, g + 4);
+    };
+    F16Pair b[NGW];
+    baddr(0, 0);
+#pragma unroll
+    for (int j = 0; j < NGW; ++j) b[j] = F16Pair{hbuf[bh + j * 16 * SLOTS], hbuf[bl + j * 16 * SLOTS]};
+    // PS: the tap's piece phase (0..2 load, 1..3 store; 4 none)
+    auto rstep = [&](auto PS, const F16Pair (&cur)[4], F16Pair (&nxt)[4]) DAMVS_INLINE {
+      constexpr int ps = decltype(PS)::value;
+      const int nb = (c + 1) & 1;               // the buffer the next slice's pieces go to
+      const int cn = c + 1 < nsl ? c + 1 : c;   // the slice they come from (the last slice: itself, unused)
+      if constexpr (ps == 1) { pstore(0, 0, nb); pstore(1, 1, nb); }
+      if constexpr (ps == 2) { pstore(2, 0, nb); pstore(3, 1, nb); }
+      if constexpr (ps == 3) pstore(4, 0, nb);
+      if (t == nt - 1) __syncthreads();
+      int c1 = c, t1 = t + 1;
+      if (t1 == nt) {
+        t1 = 0;
+        c1 = c + 1 < nsl ? c + 1 : c;
+      }
+      aload(nxt, c1, t1);
+      if constexpr (ps == 0) { pload(0, 0, cn); pload(1, 1, cn); }
+      if constexpr (ps == 1) { pload(2, 0, cn); pload(3, 1, cn); }
+      if constexpr (ps == 2) pload(4, 0, cn);
+      baddr(c1, t1);
+      // the loads above stay above the MFMAs (the scheduler would otherwise sink them next to their uses, a chunk later)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NGW; ++j) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) mma_split32(cur[m], b[j], acc[m][j]);
+        b[j] = F16Pair{hbuf[bh + j * 16 * SLOTS], hbuf[bl + j * 16 * SLOTS]};
+      }
+      // per N-group: its 12 MFMAs, then its two B reads for the next chunk
+#pragma unroll
+      for (int j = 0; j < NGW; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (++t == nt) { t = 0; ++c; }
+    };
+    F16Pair a0[4], a1[4];
+    aload(a0, 0, 0);
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    for (int cc = 0; cc < nsl; ++cc) {
+      // taps 0..3 carry the piece phases (nt >= 4); then the remaining taps two at a time (register sets alternate)
+      rstep(I0{}, a0, a1);
+      rstep(I1{}, a1, a0);
+      rstep(I2{}, a0, a1);
+      rstep(I3{}, a1, a0);
+      int tt = 4;
+      for (; tt + 1 < nt; tt += 2) {
+        rstep(I4{}, a0, a1);
+        rstep(I4{}, a1, a0);
+      }
+      if (tt < nt) {  // odd tap count: one more step, then the sets are swapped for the next slice
+        rstep(I4{}, a0, a1);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const F16Pair x = a0[m];
+          a0[m] = a1[m];
+          a1[m] = x;
+        }
+      }
+    }
+    __syncthreads();  // the epilogue's staging tiles overwrite the halo region other waves may still read
+  } else if constexpr (AG) {
     const raw* wa = wsrc + wm * 512 + lane;  // the wave's cout half: tile m's hi at m * 128, lo at m * 128 + 64
     auto aload = [&](F16Pair (&x)[4], int cc, int tt) DAMVS_INLINE {
       const raw* q = wa + (size_t)(tt * nsl + cc) * cstride;
@@ -1233,7 +1355,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
         if (a.res_pre) add8(pre[k2], r);
         if (a.relu) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) r[e] = fmaxf(r[e], 0.f);
+          for (int e = 0; e < 8; ++e) r[e] = relu(r[e]);
         }
         if (a.res_post) add8(post[k2], r);
         if constexpr (SP) {
@@ -1255,23 +1377,24 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
   }
 }
 
-template <typename T, int IS, int WM>
+template <typename T, int IS, int WM, bool RS = false>
 hipError_t launch_wide_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span) {
   constexpr bool SP = sizeof(T) == 4;
   constexpr int WRT = WM == 1 && IS == 2 ? 2 : 4 / WM, AR = WM * 256 * WideForm<T>::PL, SLOTS = WideForm<T>::SLOTS;
   const WideHalo<IS, WRT> hg(span);
-  constexpr int NHB = IS == 1 && !(SP && WM == 1) ? 2 : 1, WPER = IS == 1 ? 7 : 11;
+  constexpr int NHB = IS == 1 && !(SP && WM == 1) ? 2 : 1, WPER = RS ? 5 : IS == 1 ? 7 : 11;
   constexpr bool AG = SP;  // fp32: A fragments from L1 / L2, no A buffers in LDS
   if (hg.hp * 4 > WPER * 256) return hipErrorNotSupported;
   const size_t below_plane = (AG ? 0 : 2 * (size_t)AR * 16) + NHB * (size_t)hg.hp * SLOTS * 16;
   if (below_plane < 4 * 32 * 68 * 4) return hipErrorNotSupported;  // the epilogue's staging tiles stay below the plane halo
   const int tx = (a.Wq + WC - 1) / WC, ty = (a.Hq + WRT - 1) / WRT;
   const int nsl = (a.c0 + a.c1) / 32;
-  const size_t smem = below_plane + (size_t)hg.hp * 4;  // A chunks, halo slices, plane halo
+  const size_t smem = below_plane + (size_t)hg.hp * 4 + (RS ? 16 + SLOTS * 16 : 0);  // A chunks, halo slices, plane
+                                                                                    // halo (RS: spare piece slots)
   if (smem > 160 * 1024) return hipErrorNotSupported;
   const long long nblk = (long long)tx * ty * a.B * a.nphase;
   const dim3 grid((unsigned)nblk, (unsigned)(a.MTtot / (4 * WM)));
-  auto k = a.c1 > 0 ? conv2d_wide_kernel<T, true, IS, WM> : conv2d_wide_kernel<T, false, IS, WM>;
+  auto k = a.c1 > 0 ? conv2d_wide_kernel<T, true, IS, WM, RS> : conv2d_wide_kernel<T, false, IS, WM, RS>;
   if (smem > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)smem);
@@ -1320,9 +1443,16 @@ hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
     const char* v = getenv("DAMVS_CONV2D_WIDE");
     return v && v[0] == '0';
   }();
+  // fp32 rolling K loop (conv2d_wide_kernel RS) for the stride-1 128-channel block when its halo fits 5 pieces a thread
+  // (taps spanning <= 3 pixels); DAMVS_WIDE_RS=0 keeps the AG loop (read per call: the bitwise test flips it)
+  const char* rsv = getenv("DAMVS_WIDE_RS");
+  const bool rs_off = rsv && rsv[0] == '0';
   int dmin = 0, span = 0;
   if (off || !wide_shape_ok(a, dmin, span)) return hipErrorNotSupported;
   if (a.MTtot % 8) return a.in_stride == 1 ? launch_wide_t<T, 1, 1>(s, a, dmin, span) : launch_wide_t<T, 2, 1>(s, a, dmin, span);
+  if constexpr (sizeof(T) == 4) {
+    if (a.in_stride == 1 && span <= 3 && !rs_off) return launch_wide_t<T, 1, 2, true>(s, a, dmin, span);
+  }
   return a.in_stride == 1 ? launch_wide_t<T, 1, 2>(s, a, dmin, span) : launch_wide_t<T, 2, 2>(s, a, dmin, span);
 }
 

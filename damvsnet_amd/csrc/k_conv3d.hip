@@ -75,7 +75,7 @@ __device__ __forceinline__ void finish4(const ConvArgs& a, __amdgpu_buffer_rsrc_
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     r[i] = fmaf(acc[i], a.wscale, bias[i]);
-    if (a.relu) r[i] = fmaxf(r[i], 0.f);
+    if (a.relu) r[i] = relu(r[i]);
   }
   if (has_res) BufIO<T>::addq(q, r);
   BufIO<T>::stq(ro, ok ? off : kOOB, r);
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         r[i] = fmaf(r[i], a.wscale, b8[i]);
-        if (a.relu) r[i] = fmaxf(r[i], 0.f);
+        if (a.relu) r[i] = relu(r[i]);
       }
       const uint32_t off = valid[j] ? (uint32_t)(pout[j] * 8) * ES : kOOB;
       if (a.resid) Vox8<T>::add(rr, off, r);
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             r[i] += a.bias[co + i];
-            if (a.relu) r[i] = fmaxf(r[i], 0.f);
+            if (a.relu) r[i] = relu(r[i]);
           }
           const uint32_t off = valid[j] ? (uint32_t)(pout[j] * a.Cout + co) * ES : kOOB;
           if (a.resid) Vox8<T>::add(rr, off, r);
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 && CIN <= 16 ? 2 : 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         v[i] = (PL == 1 ? acc[xg][i] : acc[xg][i] * a.wscale) + bias[i];  // 2^-k: exact
-        if (a.relu) v[i] = fmaxf(v[i], 0.f);
+        if (a.relu) v[i] = relu(v[i]);
       }
       BufIO<T>::stq(ro, vok ? off : kOOB, v);
     }
@@ -857,7 +857,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (CIN == 32 ? 1 : 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         v[i] = (PL == 1 ? acc[xg][i] : acc[xg][i] * a.wscale) + bias[i];  // 2^-k: exact
-        if (a.relu) v[i] = fmaxf(v[i], 0.f);
+        if (a.relu) v[i] = relu(v[i]);
       }
       BufIO<T>::stq(ro, vok ? off : kOOB, v);
     }
@@ -1123,7 +1123,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : 1) void conv_
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           v[i] = (PL == 1 ? acc[r][xg][i] : acc[r][xg][i] * a.wscale) + bias[i];  // 2^-k: exact
-          if (a.relu) v[i] = fmaxf(v[i], 0.f);
+          if (a.relu) v[i] = relu(v[i]);
         }
         BufIO<T>::stq(ro, ok ? (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * 16 + g * 4) * (uint32_t)ES : kOOB, v);
       }
@@ -1323,7 +1323,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 2 ? 3 : 2) void decon
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           v[i] += b8[i];
-          if (a.relu) v[i] = fmaxf(v[i], 0.f);
+          if (a.relu) v[i] = relu(v[i]);
           v[i] += __uint_as_float((i & 1) ? (q4[i >> 1] & 0xffff0000u) : (q4[i >> 1] << 16));
         }
       } else {
@@ -1331,7 +1331,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 2 ? 3 : 2) void decon
         for (int i = 0; i < 8; ++i) {
           const float4 f = __builtin_bit_cast(float4, rq[k][i >> 2]);
           v[i] = v[i] * a.wscale + b8[i];  // 2^-k: exact
-          if (a.relu) v[i] = fmaxf(v[i], 0.f);
+          if (a.relu) v[i] = relu(v[i]);
           v[i] += (i & 3) == 0 ? f.x : (i & 3) == 1 ? f.y : (i & 3) == 2 ? f.z : f.w;
         }
       }
@@ -1505,7 +1505,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             v[i] += b8[i];
-            if (a.relu) v[i] = fmaxf(v[i], 0.f);
+            if (a.relu) v[i] = relu(v[i]);
             v[i] += __uint_as_float((i & 1) ? (q4[i >> 1] & 0xffff0000u) : (q4[i >> 1] << 16));
           }
         } else {
@@ -1513,7 +1513,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
           for (int i = 0; i < 8; ++i) {
             const float4 f = __builtin_bit_cast(float4, rq[k][i >> 2]);
             v[i] = v[i] * a.wscale + b8[i];  // 2^-k: exact
-            if (a.relu) v[i] = fmaxf(v[i], 0.f);
+            if (a.relu) v[i] = relu(v[i]);
             v[i] += (i & 3) == 0 ? f.x : (i & 3) == 1 ? f.y : (i & 3) == 2 ? f.z : f.w;
           }
         }
@@ -1665,7 +1665,7 @@ __global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         v[i] = (PL == 1 ? acc[r][i] : acc[r][i] * a.wscale) + bias[i];  // 2^-k: exact
-        if (a.relu) v[i] = fmaxf(v[i], 0.f);
+        if (a.relu) v[i] = relu(v[i]);
       }
       BufIO<T>::stq(ro, ok ? (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * 16 + g * 4) * (uint32_t)ES : kOOB, v);
     }

@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(2) void head_kernel(const HeadArgs
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           v[i] += b8[i];
-          v[i] = fmaxf(v[i], 0.f);
+          v[i] = relu(v[i]);
           v[i] += __uint_as_float((i & 1) ? (q4[i >> 1] & 0xffff0000u) : (q4[i >> 1] << 16));
         }
       } else {
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(2) void head_kernel(const HeadArgs
         for (int i = 0; i < 8; ++i) {
           const float4 f = __builtin_bit_cast(float4, rq[u][i >> 2]);
           v[i] = v[i] * a.wscale + b8[i];
-          v[i] = fmaxf(v[i], 0.f);
+          v[i] = relu(v[i]);
           v[i] += (i & 3) == 0 ? f.x : (i & 3) == 1 ? f.y : (i & 3) == 2 ? f.z : f.w;
         }
       }

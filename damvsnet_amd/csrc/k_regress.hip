@@ -582,11 +582,29 @@ size_t prob_regress_smem_bytes(int store, int Cb, int D) {
   return store == ST_BF16 ? prob_regress_smem<bf16_t, 16>(D) : prob_regress_smem<float, 16>(D);
 }
 
+// The range check at the end of damvs_stage_forward: depth, confidence and variance maps read once (a grid-stride loop
+// over ~2 blocks per CU, coalesced 4-byte loads: any alignment); any non-finite value sets status[0] = 1 by a vector
+// store (the status word was cleared by the stage's first kernel). 12 bytes per pixel: ~15 us at stage 3 of cfgC.
+__global__ __launch_bounds__(256) void finite_check_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                           const float* __restrict__ c, long long n, int* __restrict__ status) {
+  bool bad = false;
+  for (long long i = blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    bad |= (a[i] * 0.f + b[i] * 0.f + c[i] * 0.f) != 0.f;  // x * 0 is 0 unless x is inf or NaN
+  if (bad) __builtin_amdgcn_raw_buffer_store_b32(1u, make_rsrc(status, 4), 0, 0, 0);
+}
+
 hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float* logits, const float* hyps,
                           float* depth, float* conf, float* var, float* prob) {
   int hw = h * w;
   hipLaunchKernelGGL(regress_kernel, dim3((hw + 255) / 256, B), dim3(256), 0, s, B, D, hw, logits, hyps, depth, conf,
                      var, prob);
+  return hipGetLastError();
+}
+
+hipError_t launch_finite_check(hipStream_t s, const float* a, const float* b, const float* c, long long n, int* status) {
+  const long long nb = (n + 255) / 256;
+  hipLaunchKernelGGL(finite_check_kernel, dim3((unsigned)(nb < 512 ? (nb > 0 ? nb : 1) : 512)), dim3(256), 0, s, a, b, c,
+                     n, status);
   return hipGetLastError();
 }
 

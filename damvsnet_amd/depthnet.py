@@ -63,6 +63,13 @@ class DepthNet(nn.Module):
         self._engines = {}
         return super()._apply(fn, *a, **k)
 
+    def check_range(self):
+        """Raise damvsnet_amd._capi.DamvsRangeError when a stage forward since the last check produced non-finite
+        depth / confidence / variance (the fp32 path's split-f16 products are limited to |x| < 65520; the reference's
+        fp32 convolutions are not). Synchronises the streams those forwards ran on."""
+        for eng in list(self._engines.values()):
+            eng.check_range()
+
     def forward(self, stage_idx, features, proj_matrices, depth_values, num_depth, cost_regularization,
                 prob_volume_init=None, return_prob_volume=True):
         assert len(features) == proj_matrices.shape[1], "Different number of images and projection matrices"
@@ -73,11 +80,12 @@ class DepthNet(nn.Module):
         _require_gpu(depth_values, proj_matrices, *features)
         feats = [to_nhwc(f, self.compute_dtype) for f in features]
         return self.forward_nhwc(stage_idx, feats, proj_matrices, depth_values, cost_regularization,
-                                 prob_volume_init, return_prob_volume)
+                                 prob_volume_init, return_prob_volume, check_range=True)
 
     def forward_nhwc(self, stage_idx, feats_nhwc, proj_matrices, depth_values, cost_regularization,
-                     prob_volume_init=None, return_prob_volume=True):
-        """Same as forward() with features already NHWC (B,h,w,C) — the HIP front-end's output."""
+                     prob_volume_init=None, return_prob_volume=True, check_range=False):
+        """Same as forward() with features already NHWC (B,h,w,C) — the HIP front-end's output. ``check_range``:
+        raise DamvsRangeError on non-finite outputs right away (a host sync); CascadeMVSNet checks once per forward."""
         dev = depth_values.device
         eng = self.engine(stage_idx, cost_regularization, dev)
         feats = [f if f.dtype == self.compute_dtype and f.is_contiguous() else f.to(self.compute_dtype).contiguous()
@@ -87,6 +95,8 @@ class DepthNet(nn.Module):
         depth, conf, var, prob = eng.forward(feats, proj_matrices.float().contiguous(), hyps, pinit,
                                              want_prob=return_prob_volume,
                                              probe=self.probe(stage_idx) if self.probe is not None else None)
+        if check_range:
+            eng.check_range()
         return {"depth": depth, "photometric_confidence": conf, "variance": var, "prob_volume": prob,
                 "depth_values": depth_values}
 

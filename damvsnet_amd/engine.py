@@ -61,6 +61,7 @@ class StageEngine:
         self.handle = handle
         self._lib = lib
         self._ws = None
+        self._unchecked = {}  # stream pointer -> workspace of a forward whose range status was not read yet
         self.version = _param_version(costreg) + (_param_version(aggw) if aggw is not None else ())
 
     def __del__(self):
@@ -82,6 +83,7 @@ class StageEngine:
         ws = self._ws.get(key)
         if ws is None or ws.numel() < n.value:
             ws = self._ws[key] = torch.empty(n.value, dtype=torch.uint8, device=self.device)
+            ws[:4].zero_()  # the range status word (damvs_stage_status)
         return ws
 
     def forward(self, feats_nhwc, proj, hyps, prob_init=None, want_prob=True, probe=None):
@@ -97,6 +99,7 @@ class StageEngine:
         var = torch.empty_like(depth)
         prob = torch.empty(B, D, h, w, device=dev, dtype=torch.float32) if want_prob else None
         fptrs = (ctypes.c_void_p * N)(*[f.data_ptr() for f in feats_nhwc])
+        self._unchecked[_capi.stream_ptr(dev)] = ws
         if probe is None:
             check(self._lib.damvs_stage_forward(self.handle, _capi.stream_ptr(dev), B, N, D, h, w, fptrs, ptr(proj),
                                                 ptr(hyps), ptr(prob_init), ptr(ws), ws.numel(), ptr(depth), ptr(conf),
@@ -109,6 +112,13 @@ class StageEngine:
                                                        ptr(proj), ptr(hyps), ptr(prob_init), ptr(ws), ws.numel(),
                                                        ptr(depth), ptr(conf), ptr(var), ptr(prob), evs))
         return depth, conf, var, prob
+
+    def check_range(self):
+        """Raise DamvsRangeError if any forward since the last check wrote non-finite depth / confidence / variance
+        (damvs_stage_status: sticky per workspace until read; synchronises the streams those forwards ran on)."""
+        pending, self._unchecked = self._unchecked, {}
+        for stream, ws in pending.items():
+            check(self._lib.damvs_stage_status(self.handle, stream, ptr(ws), ws.numel()))
 
     # ---- split entry points (parity tests / sharded execution)
     def warp_aggregate(self, feats, proj, hyps, rt=None, layout=_capi.DAMVS_LAYOUT_NHWC, out=None):

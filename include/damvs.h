@@ -37,7 +37,8 @@ enum {
   DAMVS_E_DTYPE = -3,     /* unsupported storage type */
   DAMVS_E_HIP = -4,       /* HIP runtime error */
   DAMVS_E_NOMEM = -5,     /* device allocation failed (create only) */
-  DAMVS_E_WORKSPACE = -6  /* workspace too small */
+  DAMVS_E_WORKSPACE = -6, /* workspace too small */
+  DAMVS_E_RANGE = -7      /* non-finite depth / confidence / variance (damvs_stage_status) */
 };
 
 enum { DAMVS_F32 = 0, DAMVS_BF16 = 1 };                       /* storage of features / volumes */
@@ -103,6 +104,17 @@ int damvs_stage_forward(const damvs_stage* st, void* stream, int B, int N, int D
                         const void* const* feats, const float* proj, const float* hyps, const float* prob_init,
                         void* workspace, size_t workspace_bytes, float* depth, float* conf, float* var,
                         float* prob);
+
+/* Range status of the damvs_stage_forward calls that used `workspace` since the previous damvs_stage_status on it
+ * (synchronises `stream`, the stream they ran on, then clears the status): DAMVS_OK, or DAMVS_E_RANGE when any depth,
+ * confidence or variance value one of them wrote is non-finite. The status is the workspace's first 4 bytes: zero them
+ * when the workspace is allocated (hipMemset), or call damvs_stage_status once before the first forward and ignore the
+ * result. Why it exists: the fp32 path computes every conv product on split-f16 MFMAs (x = f16 hi + f16 lo), so an
+ * activation of magnitude >= 65520 (beyond the f16 range) turns into NaN there; ReLU keeps NaN as torch.relu does, and
+ * the stage's outputs carry it. The forward itself never synchronises (its last kernel checks the three output maps
+ * and sets the status); damvsnet_amd asks once per CascadeMVSNet.forward. The reference's fp32 convolutions have no
+ * such limit (the volume of models/cas_mvsnet.py:64-76 is the first tensor that can reach it). */
+int damvs_stage_status(const damvs_stage* st, void* stream, const void* workspace, size_t workspace_bytes);
 
 /* damvs_stage_forward with in-pipeline timing probes: events (NULL, or 4 hipEvent_t, any may be NULL) are
  * recorded on `stream` before the warp + aggregation launch, after it, after the U-Net and after the

@@ -349,3 +349,49 @@ def test_planes_four_columns_bitwise(k, ng, relu, pre, monkeypatch):
         outs.append(L(B, H, W, None, None, geo=gp, res_pre=res).clone())
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+# fp32 wide layers on the rolling K loop (conv2d_wide_kernel RS) against the AG loop (DAMVS_WIDE_RS=0): the same MFMA
+# sequence per accumulator, so bitwise equal. Stride-1 128-channel blocks: GeoBlock conv2 with the plane, two inputs +
+# plane + both residuals, the k5 s2 transposed decoder (phases of 9 / 6 / 6 / 4 taps), transposed k3 s1, ragged tiles.
+RS_CASES = [
+    (False, 3, 1, 1, 0, 128, 0, (0,), 128, True, True, 0, (37, 151)),
+    (False, 3, 1, 1, 0, 128, 128, (256,), 256, True, True, 2, (20, 24)),
+    (True, 5, 2, 2, 1, 256, 0, (), 128, True, False, 1, (30, 70)),
+    (True, 3, 1, 1, 0, 128, 0, (), 128, True, False, 0, (19, 130)),
+    (False, 3, 1, 1, 0, 96, 0, (96,), 128, False, False, 0, (8, 64)),
+]
+
+
+@pytest.mark.parametrize("case", RS_CASES, ids=[str(i) for i in range(len(RS_CASES))])
+def test_wide_rolling_loop_bitwise(case, monkeypatch):
+    from damvsnet_amd.frontend_hip import HipConv2d, planes
+    tr, k, s, p, op, c0, c1, geo, cout, relu, pre, post_up, (H, W) = case
+    g = torch.Generator().manual_seed(7)
+    B = 2
+    cin = c0 + c1 + len(geo)
+    conv = (nn.ConvTranspose2d(cin, cout, k, stride=s, padding=p, output_padding=op) if tr
+            else nn.Conv2d(cin, cout, k, stride=s, padding=p))
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.2)
+        conv.bias.copy_(torch.randn(conv.bias.shape, generator=g) * 0.1)
+    tensor_at = [c for c in range(cin) if c not in geo]
+    at = dict(c0=c0, c0_at=tensor_at[0])
+    if c1:
+        at.update(c1=c1, c1_at=tensor_at[c0])
+    L = HipConv2d(conv, torch.float32, relu, geo_at=geo, **at)
+    a = torch.randn(B, H, W, c0, generator=g).to(DEV)
+    b = torch.randn(B, H, W, c1, generator=g).to(DEV) if c1 else None
+    gp = planes(torch.randn(B, len(geo), H, W, generator=g).to(DEV)) if geo else ()
+    Ho, Wo = (H - 1) * s - 2 * p + k + op if tr else (H + 2 * p - k) // s + 1, \
+        (W - 1) * s - 2 * p + k + op if tr else (W + 2 * p - k) // s + 1
+    rp = torch.randn(B, Ho, Wo, L.cout_store, generator=g).to(DEV) if pre else None
+    rq = torch.randn(B, Ho // post_up, Wo // post_up, L.cout_store, generator=g).to(DEV) if post_up else None
+    run = lambda: L(B, H, W, a, b, geo=gp, res_pre=rp, res_post=rq, post_up=max(post_up, 1))  # noqa: E731
+    monkeypatch.delenv("DAMVS_WIDE_RS", raising=False)
+    y_rs = run()
+    monkeypatch.setenv("DAMVS_WIDE_RS", "0")
+    y_ag = run()
+    torch.cuda.synchronize()
+    assert torch.isfinite(y_rs).all()
+    assert torch.equal(y_rs, y_ag)

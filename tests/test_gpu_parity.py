@@ -487,6 +487,53 @@ def test_depthnet_errors():
         net.DepthNet(2, [cuda(f) for f in feats], cuda(P), cuda(hyps), 16, net.cost_regularization[2])
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_depthnet_range_status(dtype):
+    """The fp32 path's split-f16 products hold |x| < 65520 only (damvs_device.h mma_split32): features scaled so that
+    (ref - warp)^2 exceeds 65504 must raise DamvsRangeError (DAMVS_E_RANGE from damvs_stage_status), never return NaN
+    or finite-but-wrong maps. bf16 storage has the fp32 range: the same inputs give finite maps. The same features at
+    scale 1 pass on both paths, and a NaN input raises on both (ReLU keeps NaN, as torch.relu does)."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd._capi import DamvsRangeError
+    net = CascadeMVSNet(ndepths=[48, 32, 8], compute_dtype=dtype)
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"))
+    net = net.to(DEV).eval()
+    feats, P, hyps = depthnet_inputs()
+    run = lambda fs: net.DepthNet(2, [cuda(f) for f in fs], cuda(P), cuda(hyps), 8, net.cost_regularization[2])  # noqa
+    with torch.no_grad():
+        out = run(feats)
+        assert torch.isfinite(out["depth"]).all()
+        big = [f * 1000.0 for f in feats]
+        assert max(float((big[0] - f).abs().max()) for f in big[1:]) ** 2 > 65504.0
+        if dtype == torch.float32:
+            with pytest.raises(DamvsRangeError, match="DAMVS_E_RANGE"):
+                run(big)
+        else:
+            assert torch.isfinite(run(big)["depth"]).all()
+        nan = [f.clone() for f in feats]
+        nan[1][0, :, 100:104, 150:154] = float("nan")
+        with pytest.raises(DamvsRangeError):
+            run(nan)
+        out2 = run(feats)  # the status was read and cleared: a good forward passes again
+        assert torch.equal(out2["depth"], out["depth"])
+
+
+def test_cascade_range_status_fp32():
+    """CascadeMVSNet.forward reads every stage's range status once per forward (one and two sub-batch streams):
+    images scaled so that the fp32 front-end's activations leave the f16 range raise DamvsRangeError."""
+    from damvsnet_amd._capi import DamvsRangeError
+    net = make_model("forward_160x128_48_32_8", (48, 32, 8))
+    imgs, proj, dv, ins = forward_inputs(2, 5, 128, 160)
+    with torch.no_grad():
+        out = net(cuda(imgs), cuda(proj), cuda(dv), cuda(ins))
+        assert torch.isfinite(out["depth"]).all()
+        for streams in (1, 2):
+            with pytest.raises(DamvsRangeError):
+                net(cuda(imgs) * 1e5, cuda(proj), cuda(dv), cuda(ins), streams=streams)
+        out2 = net(cuda(imgs), cuda(proj), cuda(dv), cuda(ins), streams=2)
+        assert torch.equal(out2["depth"], out["depth"])
+
+
 # ----------------------------------------------------------------------------- full forward (A11)
 #
 # The cascade amplifies last-bit differences: with these random (BN-calibrated) weights, a

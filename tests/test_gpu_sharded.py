@@ -80,6 +80,25 @@ def test_sharded_stage_cfgD_8way_bitwise(s, D, H, W, warp):
             assert torch.equal(o[k], ref[k]), (r, k, (o[k] - ref[k]).abs().max().item())
 
 
+@pytest.mark.parametrize("warp", ["depth", "gather"])
+@pytest.mark.parametrize("s,D,H,W", [(0, 64, 264, 480), (1, 32, 528, 960)])
+def test_sharded_stage_cfgE_8way_bitwise(s, D, H, W, warp):
+    """BASELINE.json configs[4] (cfgE: Tanks&Temples 1920x1056, 11 views, 64/32/8, bf16 on 8 GPUs) at stages 1-2's real
+    sizes over 8 emulated ranks (stage 1: 264 rows = 33 groups of 8 over 8 slabs), both partitionings, bitwise the
+    unsharded stage on every rank."""
+    from damvsnet_amd.sharded import ThreadGroup, DepthShardedDepthNet
+    net, nhwc, proj, hyps = _stage_case(s, D, 1, H, W, torch.bfloat16, N=11)
+    cr = net.cost_regularization[s]
+    with torch.no_grad():
+        ref = net.DepthNet.forward_nhwc(s, nhwc, proj, hyps, cr)
+        outs = ThreadGroup(8).run(lambda comm: DepthShardedDepthNet(net, comm, warp=warp)(s, nhwc, proj, hyps, cr))
+    torch.cuda.synchronize()
+    assert len(outs) == 8
+    for r, o in enumerate(outs):
+        for k in ("depth", "photometric_confidence", "variance", "prob_volume"):
+            assert torch.equal(o[k], ref[k]), (r, k, (o[k] - ref[k]).abs().max().item())
+
+
 def test_sharded_cascade_bitwise():
     """The whole cascade (160x128, 5 views, 48/32/8, bf16) with every stage's DepthNet over 4 emulated ranks
     (stage-1 slabs of 8 rows) equals the single-GPU forward bitwise at every stage."""

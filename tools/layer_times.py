@@ -22,10 +22,16 @@ def main():
     ap.add_argument("--config", default="cfgC")
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--dtype", choices=["bf16", "f32"], default=None, help="override the config's dtype (f32: the parity path)")
     args = ap.parse_args()
     import bench
     from damvsnet_amd import frontend_hip as F
     H, W, N, nd, dtype, _ = bench.CONFIGS[args.config]
+    if args.dtype:
+        dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    es = 2.0 if dtype == torch.bfloat16 else 4.0
+    # fp32: every product as three split-f16 MFMAs, so the compute ceiling is a third of the dense f16 rate
+    peak = 2.5e15 if dtype == torch.bfloat16 else 2.5e15 / 3
     dev = torch.device("cuda")
     net, _ = bench.build_model(nd, dtype, dev)
     imgs, proj, dv, _ = bench.make_inputs(args.batch, N, H, W, dev)
@@ -69,8 +75,8 @@ def main():
         cin = c0 + c1 + ng
         px = B * Hi * Wi if L.transposed else B * oshape[1] * oshape[2]  # a transposed conv scatters k^2 taps per input
         flops = 2.0 * px * cin * L.cout * L.kernel * L.kernel
-        byts = 2.0 * B * Hi * Wi * (c0 + c1) + 4.0 * B * Hi * Wi * ng + 2.0 * B * oshape[1] * oshape[2] * oshape[3]
-        t_roof = max(flops / 2.5e15, byts / 8e12) * 1e3  # ms
+        byts = es * B * Hi * Wi * (c0 + c1) + 4.0 * B * Hi * Wi * ng + es * B * oshape[1] * oshape[2] * oshape[3]
+        t_roof = max(flops / peak, byts / 8e12) * 1e3  # ms
         rows.append((ms, lab, "%s %dx%d->%dx%d B%d cin %d+%d+g%d cout %d" % (L.desc, Hi, Wi, oshape[1], oshape[2], B, c0,
                                                                             c1, ng, L.cout),
                      flops / ms / 1e9, byts / ms / 1e6, t_roof / ms))
@@ -78,7 +84,7 @@ def main():
         ideal[lab] += t_roof
         flops_g[lab] += flops
     print("per group (ms):", {k: round(v, 3) for k, v in agg.items()}, "total %.3f" % sum(agg.values()))
-    print("per group roofline ms (max(FLOPs/2.5PF, bytes/8TB/s) per layer):", {k: round(v, 3) for k, v in ideal.items()},
+    print("per group roofline ms (max(FLOPs/%.2f PF, bytes/8TB/s) per layer):" % (peak / 1e15), {k: round(v, 3) for k, v in ideal.items()},
           "TFLOP/s:", {k: round(flops_g[k] / agg[k] / 1e9, 1) for k in agg})
     for ms, lab, desc, tf, gb, fr in sorted(rows, reverse=True)[:args.top]:
         print("%8.3f ms  %-14s %-58s %7.1f TFLOP/s %7.0f GB/s  roofline %.2f" % (ms, lab, desc, tf, gb, fr))
