@@ -1192,10 +1192,11 @@ int damvs_conv2d_create(const damvs_conv2d_desc* desc, const float* weight, cons
       const int kexp = split_exponent(pk);
       L->wscale = std::ldexp(1.f, -kexp);
       rc = upload_split(pk, kexp, &L->wpack);
-      // the 32-K split form of the wide kernel (conv2d_wide_kernel<float>) and of the narrow halo kernel
-      // (conv2d_halo_kernel<float, ..., W32>): phases and weights at 32 K per chunk
+      // the 32-K split form of the wide kernel (conv2d_wide_kernel<float>), of the narrow halo kernel
+      // (conv2d_halo_kernel<float, ..., W32>) and of the gather kernel (conv2d_mfma_kernel<float, ..., K32>: channel
+      // counts in multiples of 8): phases and weights at 32 K per chunk
       const int ctot = d.c0 + d.c1;
-      if (rc == DAMVS_OK && !L->xpair && d.c0 % 32 == 0 && d.c1 % 32 == 0 && ctot >= 32 && d.ngeo <= 1) {
+      if (rc == DAMVS_OK && !L->xpair && d.c0 % 8 == 0 && d.c1 % 8 == 0 && ctot >= 8 && d.ngeo <= 1) {
         damvs_conv2d T32 = *L;
         T32.wpack = nullptr;
         T32.kchunk_k = 32;

@@ -91,11 +91,17 @@ __device__ __forceinline__ void tail4(const Conv2dArgs& a, int b, int oy, int ox
 // XP (a.xpair layers: ConvTranspose stride 2, cout 8): MFMA row r = (x parity r >> 3, channel r & 7),
 // so lane group g holds channels (g & 1) * 4 of output x = 2 qx + (g >> 1); group g + 1 hands its 4
 // channels to group g (g even), which loads / stores the pixel's whole 8-channel record.
-template <typename T, int MT, bool TWO, bool XP = false>
-__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO ? 3 : 1)) void conv2d_mfma_kernel(const Conv2dArgs a, int nqblk) {
+// K32 (T = float, the fp32 path; a.wide32: the layer's 32-K split packing, channels in multiples of 8): K chunks of 32
+// (tap, channel) entries, 8 consecutive channels of one tap per lane (two 16-byte loads, split once into f16 hi / lo)
+// and mma_split32 (16x16x32, full f16 rate) instead of the 16-K form's three 16x16x16 per 4 channels: half the MFMA
+// issue for the same products (conv3d_mfma_kernel's K32 form, round 4).
+template <typename T, int MT, bool TWO, bool XP = false, bool K32 = false>
+__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO ? 3 : K32 && MT == 4 ? 2 : 1)) void conv2d_mfma_kernel(const Conv2dArgs a, int nqblk) {
   typedef BufIO<T> IO;
   typedef typename IO::raw raw;
-  constexpr int E = Stor<T>::E;
+  typedef typename std::conditional<K32, F16Pair, raw>::type frag;
+  static_assert(!K32 || (sizeof(T) == 4 && !XP), "32-K form: fp32 storage, no x-pair phases");
+  constexpr int E = K32 ? 8 : Stor<T>::E;  // K entries per lane and chunk
   constexpr int KC = 4 * E;
   constexpr uint32_t ES = sizeof(T);
   // logical block = (q-block, phase), phase fastest, XCD-contiguous (see conv3d_mfma_kernel)
@@ -140,6 +146,21 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
     for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + ((size_t)ph.w_off * a.MTtot + mt0) * 64 + lane;
+  // K32: [chunk][tile][hi: 64 lanes][lo: 64 lanes] (split_weights_blocked)
+  const uint4* __restrict__ wp32 =
+      reinterpret_cast<const uint4*>(a.wpack) + ((size_t)ph.w_off * a.MTtot + mt0) * 128 + lane;
+  auto wload = [&](int chunk, int m) -> frag {
+    if constexpr (K32) {
+      const uint4* q = wp32 + ((size_t)chunk * a.MTtot + m) * 128;
+      return F16Pair{q[0], q[64]};
+    } else {
+      return wp[(size_t)(chunk * a.MTtot + m) * 64];
+    }
+  };
+  auto mma = [&](const frag& w, const frag& x, f32x4_t& acc) {
+    if constexpr (K32) mma_split32(w, x, acc);
+    else Frag2<T>::mma(w, x, acc);
+  };
   const int npix = a.B * a.Hi * a.Wi;
   const int ctot = a.c0 + a.c1;
   const int nk = ph.kchunks;
@@ -149,9 +170,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
     int t = (g * E) / ctot, ci = g * E - t * ctot;  // this lane's (tap, channel) at k = s*KC + g*E
     const int qt = KC / ctot, rc = KC - qt * ctot;
     // fragments of chunk s (then advances the lane's (tap, channel) to chunk s+1)
-    auto fetch = [&](int s, raw* wf, raw* xf) {
+    auto fetch = [&](int s, frag* wf, frag* xf) {
 #pragma unroll
-      for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * a.MTtot + m) * 64];
+      for (int m = 0; m < MT; ++m) wf[m] = wload(s, m);
       const bool tv = t < ph.ntaps;
       const int code = s_tap[tv ? t : 0];
       const int dy = (code & 0xff) - 8, dx = ((code >> 8) & 0xff) - 8;
@@ -163,10 +184,15 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
         const int iy = ys[j] + dy, ix = xs[j] + dx;
         const bool ok = valid[j] && tv && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
         const uint32_t off = (uint32_t)((pin[j] + tapoff) * cs + cl) * ES;
-        if (TWO)
+        if constexpr (K32) {  // 8 channels of one tap (channel counts are multiples of 8): two loads, split once
+          const __amdgpu_buffer_rsrc_t r = (TWO && second) ? r1 : r0;
+          const uint32_t o = ok ? off : kOOB, o2 = ok ? off + 16u : kOOB;
+          xf[j] = split8(IO::frag(r, o), IO::frag(r, o2));
+        } else if (TWO) {
           xf[j] = IO::merge(IO::frag(r0, ok && !second ? off : kOOB), IO::frag(r1, ok && second ? off : kOOB));
-        else
+        } else {
           xf[j] = IO::frag(r0, ok ? off : kOOB);
+        }
       }
       ci += rc;
       t += qt;
@@ -174,7 +200,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
     };
     // software-pipelined one chunk ahead: chunk s+1's loads are in flight during chunk s's MFMAs
     // (the deep low-resolution layers run at 1-2 waves per SIMD, too few to hide load latency)
-    raw wf[MT], xf[kG2];
+    frag wf[MT], xf[kG2];
     if constexpr (MT <= 2) {  // thin layers: occupancy hides the latency, the registers buy nothing
 #pragma unroll 1
       for (int s = 0; s < nk; ++s) {
@@ -182,18 +208,18 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
 #pragma unroll
         for (int j = 0; j < kG2; ++j)
 #pragma unroll
-          for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf[j], acc[j][m]);
+          for (int m = 0; m < MT; ++m) mma(wf[m], xf[j], acc[j][m]);
       }
     } else {
       fetch(0, wf, xf);
       for (int s = 0; s < nk; ++s) {
-        raw wn[MT], xn[kG2];
+        frag wn[MT], xn[kG2];
         const bool more = s + 1 < nk;
         if (more) fetch(s + 1, wn, xn);
 #pragma unroll
         for (int j = 0; j < kG2; ++j)
 #pragma unroll
-          for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf[j], acc[j][m]);
+          for (int m = 0; m < MT; ++m) mma(wf[m], xf[j], acc[j][m]);
         if (more) {
 #pragma unroll
           for (int m = 0; m < MT; ++m) wf[m] = wn[m];
@@ -208,7 +234,6 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
   // tensor inputs) as extra K rows, one per tap, rounded to the compute type like the reference's
   // torch.cat(...).to(dtype)
   if (ph.gchunks > 0) {
-    const raw* __restrict__ wg = wp + (size_t)nk * a.MTtot * 64;
     const int plane = a.Hi * a.Wi;
     const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.geo[0], ((long long)(a.B - 1) * a.geo_bstride[0] + plane) * 4);
     int pg[kG2];  // plane offset of the pixel's tap-(0,0) input
@@ -218,9 +243,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
       pg[j] = b * (int)a.geo_bstride[0] + (pin[j] - b * plane);
     }
     for (int s = 0; s < ph.gchunks; ++s) {
-      raw wf[MT];
+      frag wf[MT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) wf[m] = wg[(size_t)(s * a.MTtot + m) * 64];
+      for (int m = 0; m < MT; ++m) wf[m] = wload(nk + s, m);
       float v[kG2][E];
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -237,13 +262,16 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
               __builtin_amdgcn_raw_buffer_load_b32(rg, ok ? (uint32_t)(pg[j] + tapoff) * 4u : kOOB, 0, 0));
         }
       }
-      raw xf[kG2];
+      frag xf[kG2];
 #pragma unroll
-      for (int j = 0; j < kG2; ++j) xf[j] = pack_vals<T>(v[j]);
+      for (int j = 0; j < kG2; ++j) {
+        if constexpr (K32) xf[j] = split8(v[j]);
+        else xf[j] = pack_vals<T>(v[j]);
+      }
 #pragma unroll
       for (int j = 0; j < kG2; ++j)
 #pragma unroll
-        for (int m = 0; m < MT; ++m) Frag2<T>::mma(wf[m], xf[j], acc[j][m]);
+        for (int m = 0; m < MT; ++m) mma(wf[m], xf[j], acc[j][m]);
     }
   }
 
@@ -732,7 +760,7 @@ hipError_t launch_halo_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span)
 
 // Returns hipErrorNotSupported when the halo kernel does not take the layer. W32: the fp32 layer's 32-K split form.
 template <typename T, bool W32 = false>
-hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a) {
+hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a, bool dry = false) {
   constexpr int KC = W32 ? 32 : 4 * Stor<T>::E;
   // largest cout tile count (MTtot) the halo kernel takes: its B reuse pays off for narrow outputs,
   // while wide outputs are bound by the A (weight) stream the gather kernel already amortises
@@ -761,6 +789,7 @@ hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a) {
   if ((HGR + span - 1) * (HGC + span - 1) > 512) return hipErrorNotSupported;  // PER = 8 fill pieces a thread
   // cout tile as wide as keeps about one wave per SIMD busy (the tile count is small for these layers)
   const long long tiles = (long long)((a.Wq + HGC - 1) / HGC) * ((a.Hq + HGR - 1) / HGR) * a.B * a.nphase;
+  if (dry) return (a.MTtot >= 8 ? a.MTtot % 8 == 0 : (W32 ? a.MTtot <= 2 : true)) ? hipSuccess : hipErrorNotSupported;
   if constexpr (W32) {  // fp32 32-K form: the narrow layers (cout <= 32)
     if (a.MTtot == 2) return launch_halo_t<T, 2, 1, true>(s, a, dmin, span);
     if (a.MTtot == 1) return launch_halo_t<T, 1, 1, true>(s, a, dmin, span);
@@ -1476,12 +1505,13 @@ hipError_t launch_lds2_t(hipStream_t s, const Conv2dArgs& a) {
 
 // Returns hipErrorNotSupported when the LDS variant does not take the layer.
 template <typename T>
-hipError_t launch_lds2(hipStream_t s, const Conv2dArgs& a) {
+hipError_t launch_lds2(hipStream_t s, const Conv2dArgs& a, bool dry = false) {
   static const bool off = [] {
     const char* v = getenv("DAMVS_CONV2D_NO_LDS");
     return v && v[0] == '1';
   }();
   if (off || !lds3_ok(a) || a.MTtot > 2 || (sizeof(T) == 4 && a.c0 > 16)) return hipErrorNotSupported;  // LDS <= 42 KB
+  if (dry) return a.c0 == 8 || a.c0 == 16 || (sizeof(T) == 2 && a.c0 == 32) ? hipSuccess : hipErrorNotSupported;
   const int MT = a.MTtot;
   switch (a.c0) {
     case 8: return MT == 1 ? launch_lds2_t<T, 8, 1>(s, a) : launch_lds2_t<T, 8, 2>(s, a);
@@ -1733,16 +1763,47 @@ hipError_t launch_planes(hipStream_t st, const Conv2dArgs& a) {
   return K == 3 ? launch_planes_k<T, 16, 3>(st, a) : launch_planes_k<T, 16, 5>(st, a);
 }
 
-template <typename T, int MT>
+template <typename T, int MT, bool K32 = false>
 hipError_t launch_mt(hipStream_t s, const Conv2dArgs& a) {
   const long long Qtot = (long long)a.B * a.Hq * a.Wq;
   const int nq = (int)((Qtot + 4LL * kG2 * 16 - 1) / (4LL * kG2 * 16));
   dim3 grid((unsigned)(nq * a.nphase), (unsigned)((a.MTtot + MT - 1) / MT));
   if (a.c1 > 0)
-    hipLaunchKernelGGL((conv2d_mfma_kernel<T, MT, true>), grid, dim3(256), 0, s, a, nq);
+    hipLaunchKernelGGL((conv2d_mfma_kernel<T, MT, true, false, K32>), grid, dim3(256), 0, s, a, nq);
   else
-    hipLaunchKernelGGL((conv2d_mfma_kernel<T, MT, false>), grid, dim3(256), 0, s, a, nq);
+    hipLaunchKernelGGL((conv2d_mfma_kernel<T, MT, false, false, K32>), grid, dim3(256), 0, s, a, nq);
   return hipGetLastError();
+}
+
+// The gather kernel's cout tile: the widest that still puts about one wave on every SIMD (the low-resolution
+// GeoFeatureFusion layers have few pixels and many channels); 0 when the tile count rules out every width.
+int gather_mt(const Conv2dArgs& a, bool bf16) {
+  const long long tiles = ((long long)a.B * a.Hq * a.Wq + 63) / 64 * a.nphase;
+  static const long long want = [] {
+    const char* v = getenv("DAMVS_CONV2D_WANT_TILES");
+    return v ? atoll(v) : 900LL;
+  }();
+  static const int maxmt = [] {
+    const char* v = getenv("DAMVS_CONV2D_MAXMT");
+    return v ? atoi(v) : 8;
+  }();
+  if (bf16 && maxmt >= 8 && a.MTtot % 8 == 0 && tiles * (a.MTtot / 8) >= want) return 8;
+  if (a.MTtot % 4 == 0 && tiles * (a.MTtot / 4) >= want) return 4;
+  if (a.MTtot % 2 == 0 && tiles * (a.MTtot / 2) >= want) return 2;
+  return 1;
+}
+
+// fp32 32-K gather form (conv2d_mfma_kernel K32) for the layers with a 32-K packing that neither the wide nor the halo
+// kernel takes; DAMVS_CONV2D_G32=0 (read per call: the parity test flips it) returns them to the 16-K form.
+template <typename T>
+hipError_t launch_gather32(hipStream_t s, const Conv2dArgs& a) {
+  const char* v = getenv("DAMVS_CONV2D_G32");
+  if ((v && v[0] == '0') || a.xpair || a.c0 % 8 || a.c1 % 8 || a.ngeo > 1) return hipErrorNotSupported;
+  switch (gather_mt(a, false)) {
+    case 4: return launch_mt<T, 4, true>(s, a);
+    case 2: return launch_mt<T, 2, true>(s, a);
+    default: return launch_mt<T, 1, true>(s, a);
+  }
 }
 
 
@@ -1764,12 +1825,19 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
     return hipGetLastError();
   }
   if (a.ngeo > 1) return hipErrorInvalidValue;  // the MFMA path takes at most one plane
-  if (a.wide32) {  // fp32 layer with its 32-K split packing: the wide kernel, else the narrow halo kernel, else
+  if (a.wide32) {  // fp32 layer with its 32-K split packing: the wide kernel, else the narrow halo kernel, else (unless
+                   // the thin-layer LDS kernel takes it on the 16-K packing) the 32-K gather kernel, else
                    // hipErrorNotSupported (damvs_conv2d_forward then runs the 16-K packing)
     if constexpr (sizeof(T) == 4) {
-      const hipError_t e = launch_wide<T>(s, a);
+      hipError_t e = launch_wide<T>(s, a);
       if (e != hipErrorNotSupported) return e;
-      return launch_halo<T, true>(s, a);
+      if (a.c0 % 32 == 0 && a.c1 % 32 == 0) {
+        e = launch_halo<T, true>(s, a);
+        if (e != hipErrorNotSupported) return e;
+      }
+      // the layers the 16-K route gives to the LDS-tiled kernels stay there (thin 3x3 layers, 16-channel slices)
+      if (launch_lds2<T>(s, a, true) == hipSuccess || launch_halo<T>(s, a, true) == hipSuccess) return hipErrorNotSupported;
+      return launch_gather32<T>(s, a);
     }
     return hipErrorInvalidValue;
   }
@@ -1796,18 +1864,10 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
   }
   // Widest cout tile (each loaded input fragment feeds MT MFMAs) that still puts about one wave on
   // every SIMD: the low-resolution GeoFeatureFusion layers have few pixels and many channels.
-  const long long tiles = ((long long)a.B * a.Hq * a.Wq + 63) / 64 * a.nphase;
-  static const long long want = [] {
-    const char* v = getenv("DAMVS_CONV2D_WANT_TILES");
-    return v ? atoll(v) : 900LL;
-  }();
-  static const int maxmt = [] {
-    const char* v = getenv("DAMVS_CONV2D_MAXMT");
-    return v ? atoi(v) : 8;
-  }();
-  if (T_is_bf16<T>::value && maxmt >= 8 && a.MTtot % 8 == 0 && tiles * (a.MTtot / 8) >= want) return launch_mt<T, 8>(s, a);
-  if (a.MTtot % 4 == 0 && tiles * (a.MTtot / 4) >= want) return launch_mt<T, 4>(s, a);
-  if (a.MTtot % 2 == 0 && tiles * (a.MTtot / 2) >= want) return launch_mt<T, 2>(s, a);
+  const int gmt = gather_mt(a, T_is_bf16<T>::value);
+  if (gmt == 8) return launch_mt<T, 8>(s, a);
+  if (gmt == 4) return launch_mt<T, 4>(s, a);
+  if (gmt == 2) return launch_mt<T, 2>(s, a);
   return launch_mt<T, 1>(s, a);
 }
 

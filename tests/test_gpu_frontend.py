@@ -395,3 +395,48 @@ def test_wide_rolling_loop_bitwise(case, monkeypatch):
     torch.cuda.synchronize()
     assert torch.isfinite(y_rs).all()
     assert torch.equal(y_rs, y_ag)
+
+
+# fp32 layers on the 32-K gather kernel (conv2d_mfma_kernel K32: 8 channels per lane and K step, 16x16x32 split-f16
+# MFMAs) against the 16-K form (DAMVS_CONV2D_G32=0): the same products summed in another order, so equal to fp32
+# rounding. FeatureNet's k5 s2 convs, the 1x1 GeoBlock downsamples (two inputs + plane, stride 2), the FPN inner conv
+# with the upsampled residual, GeoFF's full-resolution stride-2 conv with the depth plane.
+G32_CASES = [
+    (False, 5, 2, 2, 0, 8, 0, (), 16, True, False, 0, (60, 84)),
+    (False, 5, 2, 2, 0, 16, 0, (), 32, True, False, 0, (30, 44)),
+    (False, 1, 2, 0, 0, 128, 128, (256,), 256, True, False, 0, (20, 26)),
+    (False, 1, 1, 0, 0, 64, 0, (64,), 128, True, False, 0, (19, 30)),
+    (False, 1, 1, 0, 0, 16, 0, (), 32, False, False, 2, (24, 40)),
+    (False, 3, 2, 1, 0, 8, 0, (8,), 16, True, False, 0, (40, 72)),
+]
+
+
+@pytest.mark.parametrize("case", G32_CASES, ids=[str(i) for i in range(len(G32_CASES))])
+def test_gather_conv2d_k32_vs_k16_fp32(case, monkeypatch):
+    from damvsnet_amd.frontend_hip import HipConv2d, planes
+    tr, k, s, p, op, c0, c1, geo, cout, relu, pre, post_up, (H, W) = case
+    g = torch.Generator().manual_seed(11)
+    B = 2
+    cin = c0 + c1 + len(geo)
+    conv = nn.Conv2d(cin, cout, k, stride=s, padding=p)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.2)
+        conv.bias.copy_(torch.randn(conv.bias.shape, generator=g) * 0.1)
+    tensor_at = [c for c in range(cin) if c not in geo]
+    at = dict(c0=c0, c0_at=tensor_at[0])
+    if c1:
+        at.update(c1=c1, c1_at=tensor_at[c0])
+    L = HipConv2d(conv, torch.float32, relu, geo_at=geo, **at)
+    a = torch.randn(B, H, W, c0, generator=g).to(DEV)
+    b = torch.randn(B, H, W, c1, generator=g).to(DEV) if c1 else None
+    gp = planes(torch.randn(B, len(geo), H, W, generator=g).to(DEV)) if geo else ()
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    rq = torch.randn(B, Ho // post_up, Wo // post_up, L.cout_store, generator=g).to(DEV) if post_up else None
+    run = lambda: L(B, H, W, a, b, geo=gp, res_post=rq, post_up=max(post_up, 1))  # noqa: E731
+    monkeypatch.delenv("DAMVS_CONV2D_G32", raising=False)
+    y32 = run()
+    monkeypatch.setenv("DAMVS_CONV2D_G32", "0")
+    y16 = run()
+    torch.cuda.synchronize()
+    assert torch.isfinite(y32).all()
+    assert rel_max(y32.cpu().numpy(), y16.cpu().numpy()) < 2e-6
