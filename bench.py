@@ -126,7 +126,7 @@ def hot_path_roofline(per_stage_ms, H, W, N, nd, B, dtype_name):
     """Per stage and per map: algorithmic bytes / FLOPs (costmodel) against the in-pipeline times."""
     from damvsnet_amd import costmodel as CM
     e = 2 if dtype_name == "bf16" else 4
-    cost = CM.cascade_cost(H, W, N, nd, e, fused_head=CM.head_fused())
+    cost = CM.cascade_cost(H, W, N, nd, e)
     stages, t_meas, t_roof = {}, 0.0, 0.0
     for s, ms in per_stage_ms.items():
         groups = {}

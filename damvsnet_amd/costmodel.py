@@ -10,10 +10,6 @@ Per depth map and stage (V = D*h*w voxels, e = storage bytes: 2 bf16 / 4 fp32, h
   transposed convs)
 * prob conv + regression (models/module.py:541, models/cas_mvsnet.py:105-124): bytes = e*base*V (U-Net output)
   + 4*V (hypotheses) + 4*V (probability volume) + 12*h*w (three maps), FLOPs = 54*base*V + 12*V
-* fused head (fused_head=True, k_head.hip: conv11 + skip + prob conv + regression in one kernel, the default for
-  base 8): conv11 leaves the "unet" group for the "regress" group, and its full-resolution output is never
-  materialised: the group reads conv11's input (2*base channels at V/8) and the conv0 skip (base channels at V), so
-  the stage's algorithmic bytes drop by 2*e*base*V (that output's write and read back)
 """
 from __future__ import annotations
 
@@ -35,37 +31,23 @@ def unet_layers(C: int, base: int = 8):
             ("conv9", 4 * b, 2 * b, 2, 1, True, True), ("conv11", 2 * b, b, 1, 0, True, True))
 
 
-def stage_cost(N: int, C: int, D: int, h: int, w: int, e: int, base: int = 8, fused_head: bool = False):
+def stage_cost(N: int, C: int, D: int, h: int, w: int, e: int, base: int = 8):
     """{"warp" | "unet" | "regress": (bytes, flops)} for ONE depth map of one stage."""
     V = D * h * w
     hw = h * w
     warp = (e * (N * C * hw + C * V) + 4 * V, (N - 1) * V * (16 * C + 2))
     ub = uf = 0
-    hb = hf = 0  # conv11 inside the fused head
     for name, cin, cout, li, lo, tr, skip in unet_layers(C, base):
         vin, vout = V >> (3 * li), V >> (3 * lo)
-        f = 2 * 27 * cin * cout * (vin if tr else vout)
-        if fused_head and name == "conv11":
-            hb, hf = e * (cin * vin + cout * vout + 27 * cin * cout), f  # input + skip read, no output write
-            continue
         ub += e * (cin * vin + cout * vout * (2 if skip else 1) + 27 * cin * cout)
-        uf += f
-    feat = 0 if fused_head else e * base * V  # the prob conv's read of the U-Net output
-    regress = (hb + feat + 8 * V + 12 * hw + 4 * 27 * base, hf + 54 * base * V + 12 * V)
+        uf += 2 * 27 * cin * cout * (vin if tr else vout)
+    regress = (e * base * V + 8 * V + 12 * hw + 4 * 27 * base, 54 * base * V + 12 * V)
     return {"warp": warp, "unet": (ub, uf), "regress": regress}
 
 
-def cascade_cost(H: int, W: int, N: int, ndepths, e: int, channels=(32, 16, 8), fused_head: bool = False):
+def cascade_cost(H: int, W: int, N: int, ndepths, e: int, channels=(32, 16, 8)):
     """Per stage (list of stage_cost dicts) for one depth map of an H x W cascade (stages at 1/4, 1/2, 1)."""
-    return [stage_cost(N, channels[s], ndepths[s], H >> (2 - s), W >> (2 - s), e, fused_head=fused_head)
-            for s in range(3)]
-
-
-def head_fused() -> bool:
-    """Whether the library runs the fused head (damvs_stage_forward: only with DAMVS_HEAD_FUSE=1, capi.cpp
-    head_fusable)."""
-    import os
-    return os.environ.get("DAMVS_HEAD_FUSE", "0")[:1] == "1"
+    return [stage_cost(N, channels[s], ndepths[s], H >> (2 - s), W >> (2 - s), e) for s in range(3)]
 
 
 def roofline_time(nbytes: float, flops: float, dtype: str = "bf16") -> float:

@@ -471,49 +471,6 @@ int regress_tail(const damvs_stage* st, hipStream_t s, int B, int D, int h, int 
   return hip_check(launch_regress(s, B, D, h, w, logits, hyps, depth, conf, var, prob), "regress launch");
 }
 
-// The fused head (k_head.hip: conv11 + skip + prob conv + regression, the full-resolution U-Net output never in
-// HBM) for base 8 stages whose logit column fits LDS, with DAMVS_HEAD_FUSE=1 (read per call: tests flip it). Off by
-// default: measured slower than conv11's z-streamed kernel + prob_mfma / prob_regress (cfgC B=4: bf16 196.6 against
-// 202.7 maps/s, fp32 86.2 against 87.7; profiles/r04/ab_head_r04h.jsonl).
-bool head_fusable(const damvs_stage* st, int D, int h, int w) {
-  const char* v = getenv("DAMVS_HEAD_FUSE");
-  if (!(v && v[0] == '1')) return false;
-  const void* pk = st->dtype == DAMVS_BF16 ? st->prob_pack : st->prob_split;
-  if (!pk || st->base != 8 || prob_mfma_disabled()) return false;  // (pk: the head's prob A operand)
-  if (D % 2 || h % 2 || w % 2) return false;
-  return head_smem(st->dtype, D) <= 160 * 1024;
-}
-
-#ifdef DAMVS_DIAG
-float* g_head_diag = nullptr;  // diagnostic builds: damvs_head_diag_set
-#endif
-
-// conv11 + regression: x = conv9 output (level 1), c0 = conv0 output (level 0), the skip
-int run_head(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, const void* x, const void* c0,
-             const float* hyps, const float* prob_init, float* depth, float* conf, float* var, float* prob) {
-  const Shapes S = level_shapes(D, h, w);
-  const LayerPlan& P = st->L[9];
-  HeadArgs a;
-  std::memset(&a, 0, sizeof(a));
-  a.x = x;
-  a.skip = c0;
-  a.wdec = st->dtype == DAMVS_BF16 ? P.wpack_pair : P.wpack32;
-  a.bdec = P.bias;
-  a.wscale = P.wscale;
-  a.wprob = st->dtype == DAMVS_BF16 ? st->prob_pack : st->prob_split;
-  a.pscale = st->dtype == DAMVS_BF16 ? 1.f : st->prob_scale;
-  a.prob_init = prob_init;
-  a.hyps = hyps;
-  a.depth = depth; a.conf = conf; a.var = var; a.prob = prob;
-  a.B = B; a.D = S.D[0]; a.h = S.H[0]; a.w = S.W[0];
-  a.Di = S.D[1]; a.Hi = S.H[1]; a.Wi = S.W[1];
-#ifdef DAMVS_DIAG
-  a.diag = g_head_diag;
-#endif
-  if (!a.wdec) return fail(DAMVS_E_ARG, "conv11 has no x-pair packing");
-  return hip_check(launch_head(s, st->dtype, a), "head launch");
-}
-
 // U-Net layer i (conv0..conv6, conv7, conv9, conv11): (input level, output level)
 constexpr int kLayerLevels[10][2] = {{0, 0}, {0, 1}, {1, 1}, {1, 2}, {2, 2}, {2, 3}, {3, 3}, {3, 2}, {2, 1}, {1, 0}};
 
@@ -522,11 +479,6 @@ constexpr int kLayerLevels[10][2] = {{0, 0}, {0, 1}, {1, 1}, {1, 2}, {2, 2}, {2,
 extern "C" {
 
 int damvs_abi_version(void) { return DAMVS_ABI_VERSION; }
-
-#ifdef DAMVS_DIAG
-// diagnostic builds only: the fused head also writes its conv11 + skip outputs (fp32) to p ([B][D][h][w][8])
-void damvs_head_diag_set(float* p) { g_head_diag = p; }
-#endif
 
 #ifndef DAMVS_BUILD_ID
 #define DAMVS_BUILD_ID "unstamped"
@@ -684,7 +636,7 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
     rc = upload(pk.data(), pk.size() * 2, &st->prob_pack);
   }
   if (rc == DAMVS_OK && dtype == DAMVS_F32 && b == 8) {
-    // the rows of pack_prob_rows (above) with fp32 weights, split-f16 at 32 K per chunk: the fused head's fp32 form
+    // the rows of pack_prob_rows (above) with fp32 weights, split-f16 at 32 K per chunk: prob_mfma_kernel<float>
     std::vector<float> pf((size_t)kProbRowChunks * 64 * 8, 0.f), all(cr->prob_weight, cr->prob_weight + 27 * 8);
     for (int k = 0; k < kProbRowChunks; ++k)
       for (int lane = 0; lane < 64; ++lane)
@@ -790,16 +742,10 @@ int damvs_stage_forward_probed(const damvs_stage* st, void* stream, int B, int N
   DAMVS_TRY(mark(0));
   DAMVS_TRY(hip_check(launch_warp_aggregate(s, st->dtype, st->mode, wa, blk), "warp_aggregate launch"));
   DAMVS_TRY(mark(1));
-  if (head_fusable(st, D, h, w)) {  // conv11 inside the head kernel (mark 2 then sits before the head)
-    DAMVS_TRY(run_unet(st, s, B, D, h, w, ws + W.vol, ws, W, 9));
-    DAMVS_TRY(mark(2));
-    DAMVS_TRY(run_head(st, s, B, D, h, w, ws + W.c[2], ws + W.c[0], hyps, prob_init, depth, conf, var, prob));
-  } else {
-    DAMVS_TRY(run_unet(st, s, B, D, h, w, ws + W.vol, ws, W));
-    DAMVS_TRY(mark(2));
-    DAMVS_TRY(regress_tail(st, s, B, D, h, w, ws + W.c[0], hyps, prob_init, reinterpret_cast<float*>(ws + W.logits),
-                           depth, conf, var, prob));
-  }
+  DAMVS_TRY(run_unet(st, s, B, D, h, w, ws + W.vol, ws, W));
+  DAMVS_TRY(mark(2));
+  DAMVS_TRY(regress_tail(st, s, B, D, h, w, ws + W.c[0], hyps, prob_init, reinterpret_cast<float*>(ws + W.logits), depth,
+                         conf, var, prob));
   DAMVS_TRY(mark(3));
   // range check of the outputs (sticky status word, damvs_stage_status), after the last probe: not in the regression's time
   return hip_check(launch_finite_check(s, depth, conf, var, (long long)B * h * w, status), "finite check launch");

@@ -197,24 +197,5 @@ bool prob_mfma_enabled(int store);  // bf16 unless DAMVS_PROB_MFMA=0; fp32 only 
 hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float* logits, const float* hyps,
                           float* depth, float* conf, float* var, float* prob);
 
-// ---------------------------------------------------------------- fused head (k_head.hip)
-// conv11 (ConvTranspose3d 16 -> 8, k3 s2 p1 op1, BN folded, ReLU) + the conv0 skip + the prob conv + the softmax
-// regression in one pass: the 8-channel full-resolution U-Net output lives only in LDS.
-struct HeadArgs {
-  const void* x;       // conv9 output [B][Di][Hi][Wi][16] (T)
-  const void* skip;    // conv0 output [B][D][h][w][8] (T)
-  const void* wdec;    // conv11 x-pair A fragments: bf16 wpack_pair (32 K per chunk), fp32 wpack32 (split-f16)
-  const float* bdec;   // [8]
-  float wscale;        // fp32: 2^-k of the split conv11 weights; 1 for bf16
-  const void* wprob;   // prob A fragments: bf16 pack_prob_rows; fp32 the same rows split-f16 (32-K blocked)
-  float pscale;        // fp32: 2^-k of the split prob weights; 1 for bf16
-  const float* prob_init;
-  const float* hyps;
-  float *depth, *conf, *var, *prob;
-  int B, D, h, w, Di, Hi, Wi;
-  float* diag;  // diagnostic builds: conv11 + skip outputs (fp32, [B][D][h][w][8], tile interiors), else nullptr
-};
-size_t head_smem(int store, int D);
-hipError_t launch_head(hipStream_t s, int store, const HeadArgs& a);
 
 }  // namespace damvs

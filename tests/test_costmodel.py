@@ -28,24 +28,6 @@ def test_unet_flops_per_stage():
         assert (c[s]["unet"][1] + prob) / 1e9 == pytest.approx(ref, abs=0.1)
 
 
-def test_fused_head_moves_conv11_and_drops_its_output():
-    """The fused head: FLOPs unchanged (conv11 moves from "unet" to "regress"), bytes lower by 2*e*base*V per stage
-    (conv11's full-resolution output written and read back by the prob conv)."""
-    a = CM.cascade_cost(1184, 1600, 5, (48, 32, 8), 2)
-    f = CM.cascade_cost(1184, 1600, 5, (48, 32, 8), 2, fused_head=True)
-    for s in range(3):
-        D, h, w = (48, 32, 8)[s], 1184 >> (2 - s), 1600 >> (2 - s)
-        V = D * h * w
-        fa = sum(v[1] for v in a[s].values())
-        ff = sum(v[1] for v in f[s].values())
-        assert ff == fa
-        conv11 = 2 * 27 * 16 * 8 * (V // 8)
-        assert f[s]["unet"][1] == a[s]["unet"][1] - conv11
-        ba = sum(v[0] for v in a[s].values())
-        bf = sum(v[0] for v in f[s].values())
-        assert ba - bf == 2 * 2 * 8 * V
-
-
 def test_roofline_time_bound():
     assert CM.roofline_time(8e12, 1.0) == pytest.approx(1.0)
     assert CM.roofline_time(1.0, 2.5e15) == pytest.approx(1.0)

@@ -308,58 +308,6 @@ def test_prob_regress_fused_vs_split_path(D, W, dtype, monkeypatch):
     assert rel_max(np_(var), np_(v2)) < 1e-5
 
 
-HEAD_CASES = [(0, 48, 2, 32, 80), (1, 32, 2, 40, 72), (2, 8, 2, 48, 96), (1, 16, 1, 24, 56), (2, 8, 3, 56, 120)]
-
-
-def _head_pair(s, D, B, H, W, dtype, with_init, monkeypatch):
-    """(fused, unfused) stage outputs on the same inputs: DAMVS_HEAD_FUSE=1 / 0."""
-    from damvsnet_amd.cascade import CascadeMVSNet
-    from damvsnet_amd.engine import StageEngine
-    C = (32, 16, 8)[s]
-    net = CascadeMVSNet(ndepths=[48, 32, 8])
-    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
-    feats, P, hyps = depthnet_inputs(B=B, N=3, H=H, W=W, D=D, stage_idx=s, C=C)
-    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", dtype, torch.device(DEV))
-    nhwc = [cuda(f.permute(0, 2, 3, 1).contiguous().to(dtype)) for f in feats]
-    init = None
-    if with_init:
-        g = torch.Generator().manual_seed(D + W)
-        init = cuda(torch.randn((B, D, H, W), generator=g))
-    outs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("DAMVS_HEAD_FUSE", flag)
-        outs.append([t.clone() for t in eng.forward(nhwc, cuda(P), cuda(hyps), prob_init=init)])
-    torch.cuda.synchronize()
-    return outs
-
-
-@pytest.mark.parametrize("s,D,B,H,W", HEAD_CASES)
-@pytest.mark.parametrize("with_init", [False, True])
-def test_head_fused_bf16_bitwise(s, D, B, H, W, with_init, monkeypatch):
-    """The fused head (k_head.hip: conv11 + conv0 skip + prob conv + regression, the full-resolution U-Net output kept
-    in LDS) against conv11's z-streamed kernel + prob_mfma_kernel (DAMVS_HEAD_FUSE=0) on the same stage inputs: the
-    same products, bf16 rounding of the feature and summation order, so bitwise equal depth / confidence / variance /
-    probabilities. The 8 x 30 tiles start at row / column -1: every case leaves ragged tiles on both edges."""
-    fused, split = _head_pair(s, D, B, H, W, torch.bfloat16, with_init, monkeypatch)
-    for name, a, b in zip(("depth", "conf", "var", "prob"), fused, split):
-        assert torch.equal(a, b), (name, float((a - b).abs().max()))
-
-
-@pytest.mark.parametrize("s,D,B,H,W", HEAD_CASES)
-def test_head_fused_fp32_vs_split_path(s, D, B, H, W, monkeypatch):
-    """fp32: the fused head's split-f16 conv11 and prob conv (16x16x32 f16 MFMAs, the feature tile as f16 hi / lo
-    halves) against conv11's split-f16 z-streamed kernel + the fp32 VALU prob conv and regression: equal to fp32
-    rounding (measured below 1e-6 relative on depth)."""
-    fused, split = _head_pair(s, D, B, H, W, torch.float32, True, monkeypatch)
-    (d1, c1, v1, p1), (d2, c2, v2, p2) = fused, split
-    errs = (rel_max(np_(d1), np_(d2)), float(np.abs(np_(p1) - np_(p2)).max()), rel_max(np_(v1), np_(v2)))
-    print("head fused vs split fp32: depth rel %.2e, prob abs %.2e, var rel %.2e" % errs)
-    assert errs[0] < 5e-6 and errs[1] < 1e-5 and errs[2] < 1e-4
-    m = conf_mask_pair(np_(p1), np_(p2))
-    assert m.mean() > 0.99
-    assert np.abs(np_(c1) - np_(c2))[m].max() < 1e-5
-
-
 # ----------------------------------------------------------------------------- CostRegNet (A6)
 
 @pytest.mark.parametrize("s", [0, 1, 2])

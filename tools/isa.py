@@ -4,6 +4,9 @@
   python tools/isa.py [--lib PATH] --kernel SUBSTR [--out F] one kernel's instructions (addresses and encodings dropped)
   python tools/isa.py [--lib PATH] --hash SUBSTR             sha256 (16 hex) of each matching kernel's instruction text
   python tools/isa.py [--lib PATH] --mix SUBSTR              instruction-class counts of each matching kernel
+  python tools/isa.py --update-pins --validated-by LOG       rewrite tests/isa_pins.json from the built library
+                                                            (only after the GPU stream tests passed on this build:
+                                                            LOG is the committed pytest log that shows it)
 
 The instruction text is what tests/test_isa_pins.py hashes: branch targets are printed as offsets relative to the
 kernel (so the text does not depend on where the linker placed the kernel) and nothing else of the object enters it.
@@ -22,6 +25,7 @@ from codeobj_check import code_objects, LLVM  # noqa: E402
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(REPO, "damvsnet_amd", "libdamvs.so")
+PINS = os.path.join(REPO, "tests", "isa_pins.json")
 
 
 def demangle(names):
@@ -68,6 +72,19 @@ def isa_hash(instrs):
     return hashlib.sha256("\n".join(instrs).encode()).hexdigest()[:16]
 
 
+def hashes(lib=LIB):
+    """{demangled kernel name: instruction-text hash} of every kernel in lib."""
+    ks = disassemble(lib)
+    names = sorted(ks)
+    return {d: isa_hash(ks[k]) for k, d in zip(names, demangle(names))}
+
+
+def compiler():
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "--version"], capture_output=True, text=True)
+    line = [l for l in r.stdout.splitlines() if "clang version" in l]
+    return line[0].strip() if line else "unknown"
+
+
 def classify(t):
     op = t.split()[0]
     if op.startswith("v_mfma"):
@@ -95,8 +112,20 @@ def main():
     g.add_argument("--kernel")
     g.add_argument("--hash")
     g.add_argument("--mix")
+    g.add_argument("--update-pins", action="store_true")
+    ap.add_argument("--validated-by", default=None)
     ap.add_argument("--out")
     a = ap.parse_args()
+    if a.update_pins:
+        import json
+        if not a.validated_by or not os.path.exists(os.path.join(REPO, a.validated_by)):
+            sys.exit("--validated-by must name the committed GPU pytest log of tests/test_gpu_streams.py on this build")
+        with open(PINS, "w") as f:
+            json.dump({"compiler": compiler(), "validated_by": a.validated_by, "kernels": hashes(a.lib)}, f, indent=1,
+                      sort_keys=True)
+            f.write("\n")
+        print("wrote", PINS)
+        return
     ks = disassemble(a.lib)
     names = sorted(ks)
     dem = dict(zip(names, demangle(names)))
