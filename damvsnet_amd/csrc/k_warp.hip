@@ -105,8 +105,14 @@ struct Taps {
   float wt[4];
 };
 __device__ __forceinline__ Taps bilinear_taps(int h, int w, uint32_t rec, float ix, float iy) {
+#ifdef DAMVS_WARP_CLAMP
+  // (A/B build) each coordinate clamped into [-4, size + 4] by max / min (NaN -> -4): a sample outside the map keeps
+  // all four corners outside, so it still reads 0; no lane-dependent control flow or compare chain
+  const float cx = fminf(fmaxf(ix, -4.f), (float)w + 4.f), cy = fminf(fmaxf(iy, -4.f), (float)h + 4.f);
+#else
   const bool inside = ix > -2.f && ix < (float)w + 1.f && iy > -2.f && iy < (float)h + 1.f;  // false for NaN
   const float cx = inside ? ix : -4.f, cy = inside ? iy : -4.f;
+#endif
   const float x0f = floorf(cx), y0f = floorf(cy);
   const int x0 = (int)x0f, y0 = (int)y0f;
   const float wx1 = cx - x0f, wx0 = (x0f + 1.f) - cx;

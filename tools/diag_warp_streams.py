@@ -21,25 +21,30 @@ def main():
     ap.add_argument("--layout", default="cblock", choices=["cblock", "nhwc"])
     ap.add_argument("--layer", type=int, default=0)
     ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--stage", type=int, default=1, choices=[0, 1])
     a = ap.parse_args()
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     from common import model_state
     from test_gpu_streams import _perturb
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import hypotheses, block_channels, proj_prepare
     from damvsnet_amd import _capi, synth
     DEV = "cuda"
-    net = CascadeMVSNet(ndepths=[48, 32, 8], compute_dtype=torch.bfloat16)
+    net = CascadeMVSNet(ndepths=[48, 32, 8], compute_dtype=dt)
     net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
     net = net.to(DEV).eval()
-    B, N, H, W, s, C = 2, 5, 1184, 1600, 1, 16
-    h, w, D = H // 2, W // 2, 32
+    B, N, H, W, s = 2, 5, 1184, 1600, a.stage
+    C, D, scale = (32, 48, 4) if s == 0 else (16, 32, 2)
+    h, w = H // scale, W // scale
     proj, _, dv = synth.cameras(B, N, H, W)
-    P = _perturb(torch.from_numpy(proj["stage2"])).to(DEV)
+    P = _perturb(torch.from_numpy(proj["stage%d" % (s + 1)])).to(DEV)
     g = torch.Generator(device=DEV).manual_seed(0)
     pd = 600 + 100 * torch.rand(B, H // 4, W // 4, device=DEV, generator=g)
     pv = 5 + 20 * torch.rand(B, H // 4, W // 4, device=DEV, generator=g)
-    hyps = hypotheses(torch.from_numpy(dv).to(DEV), D, H, W, 2, pd, pv)
-    feats = [torch.randn(B, h, w, C, generator=g, device=DEV).to(torch.bfloat16) for _ in range(N)]
+    hyps = hypotheses(torch.from_numpy(dv).to(DEV), D, H, W, scale, pd, pv) if s else \
+        hypotheses(torch.from_numpy(dv).to(DEV), D, H, W, scale)
+    feats = [torch.randn(B, h, w, C, generator=g, device=DEV).to(dt) for _ in range(N)]
     eng = net.DepthNet.engine(s, net.cost_regularization[s], torch.device(DEV))
 
     def report(tag, outs, ref):

@@ -8,6 +8,12 @@ step timeout -k 10 700 python -u -m pytest -q --timeout 200 --timeout-method thr
   "tests/test_gpu_parity.py::test_depthnet_range_status" "tests/test_gpu_parity.py::test_cascade_range_status_fp32" \
   > gpurun_out/r05b_pytest.log 2>&1
 tail -3 gpurun_out/r05b_pytest.log
+# the warp beside conv0 on another stream: the default build and the clamp build (-DDAMVS_WARP_CLAMP, damvsnet_amd/ab)
+for dt in f32 bf16; do for st in 1 0; do
+  step timeout -k 10 120 python -u tools/diag_warp_streams.py --layout nhwc --dtype $dt --stage $st > gpurun_out/r05b_diag_${dt}_s$st.jsonl 2>&1
+  [ -f damvsnet_amd/ab/libdamvs_clamp.so ] && DAMVS_LIB=damvsnet_amd/ab/libdamvs_clamp.so step timeout -k 10 120 python -u tools/diag_warp_streams.py --layout nhwc --dtype $dt --stage $st > gpurun_out/r05b_diag_${dt}_s${st}_clamp.jsonl 2>&1
+done; done
+grep -c '"voxels": 0' gpurun_out/r05b_diag_*.jsonl
 step timeout -k 10 200 python -u tools/kbench2d.py --dtype f32 --only D,E,F,G,L,N > gpurun_out/r05b_k2d_f32.txt 2>&1
 tail -9 gpurun_out/r05b_k2d_f32.txt
 DAMVS_WIDE_RS=0 step timeout -k 10 200 python -u tools/kbench2d.py --dtype f32 --only D,F,L,N > gpurun_out/r05b_k2d_f32_ag.txt 2>&1
