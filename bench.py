@@ -151,11 +151,12 @@ def hot_path_roofline(per_stage_ms, H, W, N, nd, B, dtype_name):
                                               "roofline_frac": round(t_roof / t_meas, 4)}}
 
 
-def pmc_mfma(config, batch):
+def pmc_mfma(config, batch, dtype=None):
     """MFMA utilisation per kernel family from the committed rocprofv3 PMC summary
-    (profiles/<round>/pmc_mfma_<config>_b<batch>.json, tools/pmc_mfma.py), or None."""
+    (profiles/<round>/pmc_mfma_<config>_b<batch>[_f32].json, tools/pmc_mfma.py), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_mfma_%s_b%d.json" % (config, batch))))
+    sfx = "_f32" if dtype == "f32" else ""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_mfma_%s_b%d%s.json" % (config, batch, sfx))))
     if not files:
         return None
     with open(files[-1]) as f:
@@ -276,19 +277,18 @@ def warp_roofline(net, imgs, proj, dv, stage, dtype, iters=20):
     ms = e0.elapsed_time(e1) / iters
     D = net.ndepths[stage]
     h, w, C = fs[0].shape[1], fs[0].shape[2], fs[0].shape[3]
-    es = 2 if dtype == torch.bfloat16 else 4
-    alg = es * (N * C * h * w * B + C * D * h * w * B) + 4 * D * h * w * B + 4 * B * (N - 1) * 12
-    return ms, alg
+    return ms, warp_alg_bytes(B, N, C, D, h, w, 2 if dtype == torch.bfloat16 else 4)
 
 
-def pmc_traffic(config, batch, kernel_substr="warp_aggregate"):
+def pmc_traffic(config, batch, kernel_substr="warp_aggregate", dtype=None):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC summary
     (profiles/<round>/pmc_*.json, produced by tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE,
     the gfx950 correction of MI355X_MICROARCH.md), or None."""
     import glob
     # preferred: the kernel as the pipeline runs it (tools/pmc_warp_inpipe.py: FETCH_SIZE x2 + WRITE_SIZE of the
     # in-pipeline launches, whose per-pixel hypotheses scatter the gathers far more than kbench's)
-    inpipe = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_warp_inpipe_%s_b%d.json" % (config, batch))))
+    sfx = "_f32" if dtype == "f32" else ""
+    inpipe = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_warp_inpipe_%s_b%d%s.json" % (config, batch, sfx))))
     if inpipe and kernel_substr == "warp_aggregate":
         with open(inpipe[-1]) as f:
             p = json.load(f)["summary"]["pipeline"]
@@ -298,6 +298,8 @@ def pmc_traffic(config, batch, kernel_substr="warp_aggregate"):
                     "read_bytes_by_request_size": int(p["read_bytes_by_request_size"]) if "read_bytes_by_request_size" in p
                     else None,
                     "source": os.path.relpath(inpipe[-1], REPO) + " (in-pipeline launches)"}
+    if dtype == "f32":
+        return None
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_%s_%s_b%d.json" % (kernel_substr, config, batch))))
     if not files:
         return None
@@ -339,10 +341,18 @@ def cpu_baseline(cfg, budget_s=60.0):
                       % (len(times), cfg, t, min(times), max(times), t_warm)}
 
 
+def warp_alg_bytes(B, N, C, D, h, w, es):
+    """Algorithmic bytes of one warp + aggregation launch: features read once, the volume written
+    once, fp32 hypotheses, cameras."""
+    return es * (N * C * h * w * B + C * D * h * w * B) + 4 * D * h * w * B + 4 * B * (N - 1) * 12
+
+
 def parity_path(args, nd, device, imgs, proj, dv, ins, world, steps=20, warmup=3):
     """The fp32 path (fp32 storage and regression, conv products as split-f16 MFMAs) timed like the headline steps:
     the path that holds north_star's 1e-3 per-pixel depth gate and the fp32 parity suites (tests/test_gpu_parity.py
-    fp32 gates incl. the end-to-end conditioning gates, tests/test_gpu_fullsize.py fp32 at cfgC/D/E)."""
+    fp32 gates incl. the end-to-end conditioning gates, tests/test_gpu_fullsize.py fp32 at cfgC/D/E). Its own
+    rooflines come from a one-stream attribution pass after the timed steps (HIP events inside
+    damvs_stage_forward_probed), priced at the split-f16 ceiling (2.5 PFLOP/s / 3) for the MFMA-bound groups."""
     from damvsnet_amd.dist import max_over_ranks
     net, _ = build_model(nd, torch.float32, device, args.frontend)
     with torch.no_grad():
@@ -361,9 +371,41 @@ def parity_path(args, nd, device, imgs, proj, dv, ins, world, steps=20, warmup=3
         torch.cuda.synchronize()
         elapsed = max_over_ranks(time.perf_counter() - t0, device=coll_device(device))
         net.DepthNet.check_range()  # raises DamvsRangeError if any timed forward produced non-finite maps
+        probes = ProbeRecorder()
+        net.DepthNet.probe = probes
+        for _ in range(3):
+            net(imgs, proj, dv, ins, check_range=False)
+        torch.cuda.synchronize()
+        net.DepthNet.check_range()
+        net.DepthNet.probe = None
     del net
     torch.cuda.empty_cache()
     maps = steps * args.batch * world
+    H, W, N = imgs.shape[3], imgs.shape[4], imgs.shape[1]
+    per_stage = probes.per_stage_ms()
+    hp = hot_path_roofline(per_stage, H, W, N, nd, args.batch, "f32")
+    from damvsnet_amd import costmodel as CM
+    D2, h2, w2 = nd[1], H // 2, W // 2
+    warp_ms = per_stage[1]["warp"]
+    alg = warp_alg_bytes(args.batch, N, 16, D2, h2, w2, 4)
+    unet_ms = per_stage[1]["unet"]
+    unet_flops = args.batch * CM.stage_cost(N, 16, D2, h2, w2, 4)["unet"][1]
+    tr = pmc_traffic(args.config, args.batch, dtype="f32")
+    mf = pmc_mfma(args.config, args.batch, dtype="f32")
+    roof = {"kernel": "warp_split_kernel<float, 16> stage 2 (fused homography warp + adaptive aggregation, 4 lanes per "
+                      "voxel: 64-byte fp32 pixels), in-pipeline launch time (HIP events inside "
+                      "damvs_stage_forward_probed, one-stream attribution pass)",
+            "bound": "hbm", "achieved": round(alg / (warp_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(alg / (warp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms_per_launch": round(warp_ms, 4),
+            "algorithmic_bytes": int(alg), "traffic": tr["bytes"] if tr else None,
+            "traffic_raw": tr.get("raw_bytes") if tr else None,
+            "traffic_source": ("committed PMC profile " + tr["source"]) if tr else None}
+    mroof = {"kernel": "stage-2 CostRegNet (10 conv layers, split-f16 MFMAs), in-pipeline time",
+             "bound": "mfma", "achieved": round(unet_flops / (unet_ms * 1e-3) / 1e12, 2),
+             "peak": CM.MFMA_PEAK["f32"] / 1e12, "unit": "TFLOP/s",
+             "frac": round(unet_flops / (unet_ms * 1e-3) / CM.MFMA_PEAK["f32"], 4), "ms": round(unet_ms, 4),
+             "algorithmic_flops": int(unet_flops),
+             "peak_note": "split-f16 ceiling: every fp32 product is three f16 MFMAs, 2.5 PFLOP/s dense f16 / 3"}
     return {"value": round(maps / elapsed, 4), "unit": "depth maps/s", "ms_per_step": round(elapsed / steps * 1e3, 3),
             "steps": steps, "warmup": warmup, "dtype": "f32", "streams": args.streams, "batch_per_gpu": args.batch,
             "range_status": "ok: every stage of every timed forward finite (damvs_stage_status, read after the steps)",
@@ -371,7 +413,8 @@ def parity_path(args, nd, device, imgs, proj, dv, ins, world, steps=20, warmup=3
                        "(x = hi + lo, hi*hi + hi*lo + lo*hi, fp32 accumulation; damvsnet_amd/csrc/damvs_device.h)",
             "gates": "north_star: depth within 1e-3 relative at every pixel on identical inputs "
                      "(tests/test_gpu_fullsize.py fp32 at cfgC/D/E, tests/test_gpu_parity.py stage-isolated), and the "
-                     "end-to-end fp32-vs-fp64 conditioning gates (tests/test_gpu_parity.py _check_forward_e2e)"}
+                     "end-to-end fp32-vs-fp64 conditioning gates (tests/test_gpu_parity.py _check_forward_e2e)",
+            "roofline": roof, "mfma_roofline": mroof, "hot_path_roofline": hp, "mfma_utilisation": mf}
 
 
 def main():
@@ -488,8 +531,7 @@ def main():
         iso_ms, alg = warp_roofline(net, imgs, proj, dv, 1, dtype)
         pipe_ms = per_stage[1]["warp"]
         achieved = alg / (pipe_ms * 1e-3) / 1e9
-        native = dtype == CONFIGS[args.config][4]  # committed PMC profiles are of the config's own dtype
-        tr = pmc_traffic(args.config, args.batch) if native else None
+        tr = pmc_traffic(args.config, args.batch, dtype=dname)  # committed PMC profiles of this dtype
         result = {
             "metric": "depth maps/sec (full CascadeMVSNet forward)",
             "value": round(maps / elapsed, 4),
@@ -527,7 +569,7 @@ def main():
                          "isolated_frac": round(alg / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "hot_path_roofline": hp,
             "range_status": "ok: every stage of every timed forward finite (damvs_stage_status, read after the steps)",
-            "mfma_utilisation": pmc_mfma(args.config, args.batch) if native else None,
+            "mfma_utilisation": pmc_mfma(args.config, args.batch, dtype=dname),
         }
         if pp is not None:
             result["parity_path"] = pp

@@ -8,7 +8,8 @@ dropped. Per kernel family (U-Net conv3d, front-end conv2d, prob conv + regressi
   mfma_busy  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs)   (issued MFMA cycles per
                SIMD-cycle of the kernels' wall time, padding rows / zero taps included)
   valu_per_mfma = SQ_INSTS_VALU / SQ_INSTS_MFMA (when both exist)
-Writes <out>/pmc_mfma_<config>_b<batch>.json (bench.py reports it as "mfma_utilisation").
+Writes <out>/pmc_mfma_<config>_b<batch>[_f32].json (bench.py reports it as "mfma_utilisation"; --dtype f32: the
+fp32 parity path, whose mfma_busy counts the three split-f16 MFMAs of every product).
 """
 import argparse
 import collections
@@ -46,7 +47,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfgC")
     ap.add_argument("--batch", type=int, default=4)
-    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r02"))
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r05"))
     ap.add_argument("--tmp", default=os.path.join(REPO, "gpurun_out", "pmc_mfma"))
     args = ap.parse_args()
     os.makedirs(args.tmp, exist_ok=True)
@@ -57,6 +59,7 @@ def main():
     cmd = ["rocprofv3", "--pmc"] + counters + ["--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run", "--",
                                                sys.executable, os.path.join(REPO, "bench.py"), "--config", args.config,
                                                "--batch", str(args.batch), "--steps", "2", "--warmup", "1",
+                                               "--dtype", args.dtype, "--no-parity-path",
                                                "--no-cpu-baseline", "--no-shard-latency"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"))
     if r.returncode != 0:
@@ -85,12 +88,12 @@ def main():
         if a.get("SQ_INSTS_MFMA") and a.get("SQ_INSTS_VALU"):
             e["valu_per_mfma"] = round(a["SQ_INSTS_VALU"] / a["SQ_INSTS_MFMA"], 2)
         summary[fam] = e
-    res = {"config": args.config, "batch": args.batch, "counters": counters, "summary": summary,
+    res = {"config": args.config, "batch": args.batch, "dtype": args.dtype, "counters": counters, "summary": summary,
            "totals": {f: dict(a) for f, a in acc.items()},
            "formula": "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs); profiled pass "
                       "(3 forwards incl. warm-up and the B=1 latency block), clocks lower than unprofiled"}
     os.makedirs(args.out, exist_ok=True)
-    path = os.path.join(args.out, "pmc_mfma_%s_b%d.json" % (args.config, args.batch))
+    path = os.path.join(args.out, "pmc_mfma_%s_b%d%s.json" % (args.config, args.batch, "_f32" if args.dtype == "f32" else ""))
     with open(path, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(summary))

@@ -27,9 +27,12 @@ PASSES = [["GRBM_GUI_ACTIVE", "SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "S
           ["TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum"],
           ["WRITE_SIZE"]]
 # the stage-2 warp: the channel-split kernel (default) or the one-lane-per-voxel kernel (DAMVS_WARP_SPLIT=0)
-KERNEL = os.environ.get("PMC_WARP_KERNEL", "warp_split_kernel<unsigned short, 16"
+# PMC_DTYPE=f32: the fp32 parity path's stage-2 warp (warp_split_kernel<float, 16>: 4 lanes per voxel; the kernel name
+# identifies stage 2 there; 4 lanes per voxel: twice the bf16 kernel's grid)
+DTYPE = os.environ.get("PMC_DTYPE", "bf16")
+KERNEL = os.environ.get("PMC_WARP_KERNEL", ("warp_split_kernel<float, 16" if DTYPE == "f32" else "warp_split_kernel<unsigned short, 16")
                         if os.environ.get("DAMVS_WARP_SPLIT", "1") != "0" else "warp_aggregate_kernel<unsigned short, 16")
-GRID = int(os.environ.get("PMC_WARP_GRID", "3788800" if "split" in KERNEL else "1894400"))  # threads per launch
+GRID = int(os.environ.get("PMC_WARP_GRID", "7577600" if DTYPE == "f32" else "3788800" if "split" in KERNEL else "1894400"))
 N_PIPE = 5
 
 
@@ -37,14 +40,15 @@ def run_pass(i, counters, out):
     d = os.path.join(out, "p%d" % i)
     cmd = ["rocprofv3", "--pmc"] + counters + ["--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run", "--",
                                               sys.executable, os.path.join(REPO, "bench.py"), "--streams", "1",
-                                              "--warmup", "1", "--steps", "2", "--no-cpu-baseline"]
+                                              "--warmup", "1", "--steps", "2", "--no-cpu-baseline", "--no-parity-path",
+                                              "--dtype", DTYPE]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"))
     if r.returncode != 0:
         raise RuntimeError("pass %d failed:\n%s" % (i, r.stderr[-2000:]))
     disp = collections.OrderedDict()
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if KERNEL not in row["Kernel_Name"] or int(row.get("Grid_Size", 0) or 0) != GRID:
+            if KERNEL not in row["Kernel_Name"] or (GRID and int(row.get("Grid_Size", 0) or 0) != GRID):
                 continue
             k = int(row["Dispatch_Id"])
             e = disp.setdefault(k, {"start": int(row["Start_Timestamp"]),
