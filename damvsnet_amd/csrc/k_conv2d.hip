@@ -503,7 +503,10 @@ constexpr int HGR = 4, HGC = 64;  // q-tile rows (one per group) x columns (16 p
 // halo pixel keeps each 8-channel chunk as its f16 hi / lo halves in 8 slots, slot s at s ^ ((pixel >> 1) & 7) (the
 // 16 lanes of an N-group read 16 consecutive pixels); one halo buffer, rewritten between two barriers after a slice's
 // last tap (twice the bytes of the bf16 tile).
-template <typename T, int MT, int WM, bool TWO, bool W32 = false>
+// RS (W32 only): the rolling tap loop -- tap offsets by v_readlane, each N-group's B pair for the next tap read as soon
+// as that group's MFMAs are issued (pinned by sched_group_barrier), the next tap's A pairs loaded before the MFMAs; the
+// same MFMA sequence per accumulator as the plain W32 loop, so bitwise equal (DAMVS_HALO_RS=0 selects that loop).
+template <typename T, int MT, int WM, bool TWO, bool W32 = false, bool RS = false>
 __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int nsl,
                                                           int dmin, int span) {
   typedef BufIO<T> IO;
@@ -610,6 +613,55 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
   gfill(0);
   lstore(0);
   __syncthreads();
+  if constexpr (RS) {
+    static_assert(W32, "rolling tap loop: the 32-K form");
+    const int ltoff = lane < nt ? (ph.tap[lane][0] - dmin) * HC + (ph.tap[lane][1] - dmin) : 0;  // lane t: tap t
+    auto bread = [&](int t, frag (&xf)[GW]) DAMVS_INLINE {  // B pairs of tap t (one halo buffer)
+      const int to = __builtin_amdgcn_readlane(ltoff, t) + pcol;
+#pragma unroll
+      for (int j = 0; j < GW; ++j) {
+        const int pl = to + (j % HGR) * HC + (j / HGR) * 16;
+        const uint4* px = ubuf + pl * 8;
+        xf[j] = F16Pair{px[wslot(pl, g)], px[wslot(pl, g + 4)]};
+      }
+    };
+    for (int c = 0; c < nsl; ++c) {
+      if (c + 1 < nsl) gfill(c + 1);
+      frag wf[MT], xf[GW];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) wf[m] = wload(c, m);  // chunk (tap 0, slice c)
+      bread(0, xf);
+      for (int t = 0; t < nt; ++t) {
+        const int t1 = t + 1 < nt ? t + 1 : t;  // past the last tap: a harmless re-read
+        frag wn2[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) wn2[m] = wload(t1 * nsl + c, m);
+        const int to = __builtin_amdgcn_readlane(ltoff, t1) + pcol;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < GW; ++j) {
+#pragma unroll
+          for (int m = 0; m < MT; ++m) mma_split32(wf[m], xf[j], acc[j][m]);
+          const int pl = to + (j % HGR) * HC + (j / HGR) * 16;
+          const uint4* px = ubuf + pl * 8;
+          xf[j] = F16Pair{px[wslot(pl, g)], px[wslot(pl, g + 4)]};
+        }
+#pragma unroll
+        for (int j = 0; j < GW; ++j) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 3 * MT, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) wf[m] = wn2[m];
+      }
+      if (c + 1 < nsl) {
+        __syncthreads();  // every wave is done with slice c's halo
+        lstore(0);
+        __syncthreads();
+      }
+    }
+  } else
   for (int c = 0; c < nsl; ++c) {
     if (c + 1 < nsl) gfill(c + 1);
     const int bi = NHB == 2 ? (c & 1) : 0;
@@ -739,7 +791,7 @@ __global__ __launch_bounds__(256) void conv2d_halo_kernel(const Conv2dArgs a, in
   }
 }
 
-template <typename T, int MT, int WM, bool W32 = false>
+template <typename T, int MT, int WM, bool W32 = false, bool RS = false>
 hipError_t launch_halo_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span) {
   constexpr int KC = W32 ? 32 : 4 * Stor<T>::E;
   const int tx = (a.Wq + HGC - 1) / HGC, ty = (a.Hq + HGR - 1) / HGR;
@@ -748,7 +800,7 @@ hipError_t launch_halo_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span)
   const size_t smem = W32 ? hp * 8 * 16 : (nsl > 1 ? 2 : 1) * hp * 4 * 16;  // one slice (or W32): one buffer
   const long long nblk = (long long)tx * ty * a.B * a.nphase;
   const dim3 grid((unsigned)nblk, (unsigned)(a.MTtot / (MT * WM)));
-  auto k = a.c1 > 0 ? conv2d_halo_kernel<T, MT, WM, true, W32> : conv2d_halo_kernel<T, MT, WM, false, W32>;
+  auto k = a.c1 > 0 ? conv2d_halo_kernel<T, MT, WM, true, W32, RS> : conv2d_halo_kernel<T, MT, WM, false, W32, RS>;
   if (smem > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)smem);
@@ -790,9 +842,11 @@ hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a, bool dry = false) {
   // cout tile as wide as keeps about one wave per SIMD busy (the tile count is small for these layers)
   const long long tiles = (long long)((a.Wq + HGC - 1) / HGC) * ((a.Hq + HGR - 1) / HGR) * a.B * a.nphase;
   if (dry) return (a.MTtot >= 8 ? a.MTtot % 8 == 0 : (W32 ? a.MTtot <= 2 : true)) ? hipSuccess : hipErrorNotSupported;
-  if constexpr (W32) {  // fp32 32-K form: the narrow layers (cout <= 32)
-    if (a.MTtot == 2) return launch_halo_t<T, 2, 1, true>(s, a, dmin, span);
-    if (a.MTtot == 1) return launch_halo_t<T, 1, 1, true>(s, a, dmin, span);
+  if constexpr (W32) {  // fp32 32-K form: the narrow layers (cout <= 32); the rolling tap loop unless DAMVS_HALO_RS=0
+    const char* rv = getenv("DAMVS_HALO_RS");  // (read per call: the bitwise test flips it)
+    const bool rs = !(rv && rv[0] == '0');
+    if (a.MTtot == 2) return rs ? launch_halo_t<T, 2, 1, true, true>(s, a, dmin, span) : launch_halo_t<T, 2, 1, true>(s, a, dmin, span);
+    if (a.MTtot == 1) return rs ? launch_halo_t<T, 1, 1, true, true>(s, a, dmin, span) : launch_halo_t<T, 1, 1, true>(s, a, dmin, span);
     return hipErrorNotSupported;
   }
   if (a.MTtot >= 8) {  // wide: 2 x 2 wave grid, 4 cout tiles x 128 pixels a wave

@@ -440,3 +440,49 @@ def test_gather_conv2d_k32_vs_k16_fp32(case, monkeypatch):
     torch.cuda.synchronize()
     assert torch.isfinite(y32).all()
     assert rel_max(y32.cpu().numpy(), y16.cpu().numpy()) < 2e-6
+
+
+# fp32 narrow layers on the halo kernel's rolling tap loop (conv2d_halo_kernel RS) against its plain W32 loop
+# (DAMVS_HALO_RS=0): the same MFMA sequence per accumulator, so bitwise equal. One-slice layers with the plane (32+g ->
+# 32 and -> 16), the k5 s2 transposed decoders (4 phases, 4 slices), two inputs, ragged tiles.
+HALO_RS_CASES = [
+    (False, 3, 1, 1, 0, 32, 0, (32,), 32, True, True, 0, (37, 151)),
+    (False, 3, 1, 1, 0, 32, 0, (32,), 16, True, False, 0, (20, 70)),
+    (True, 5, 2, 2, 1, 128, 0, (), 32, True, False, 1, (30, 70)),
+    (True, 5, 2, 2, 1, 64, 0, (), 32, True, False, 1, (19, 40)),
+    (False, 3, 1, 1, 0, 32, 32, (), 32, True, False, 0, (24, 66)),
+]
+
+
+@pytest.mark.parametrize("case", HALO_RS_CASES, ids=[str(i) for i in range(len(HALO_RS_CASES))])
+def test_halo_rolling_loop_bitwise(case, monkeypatch):
+    from damvsnet_amd.frontend_hip import HipConv2d, planes
+    tr, k, s, p, op, c0, c1, geo, cout, relu, pre, post_up, (H, W) = case
+    g = torch.Generator().manual_seed(5)
+    B = 2
+    cin = c0 + c1 + len(geo)
+    conv = (nn.ConvTranspose2d(cin, cout, k, stride=s, padding=p, output_padding=op) if tr
+            else nn.Conv2d(cin, cout, k, stride=s, padding=p))
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.2)
+        conv.bias.copy_(torch.randn(conv.bias.shape, generator=g) * 0.1)
+    tensor_at = [c for c in range(cin) if c not in geo]
+    at = dict(c0=c0, c0_at=tensor_at[0])
+    if c1:
+        at.update(c1=c1, c1_at=tensor_at[c0])
+    L = HipConv2d(conv, torch.float32, relu, geo_at=geo, **at)
+    a = torch.randn(B, H, W, c0, generator=g).to(DEV)
+    b = torch.randn(B, H, W, c1, generator=g).to(DEV) if c1 else None
+    gp = planes(torch.randn(B, len(geo), H, W, generator=g).to(DEV)) if geo else ()
+    Ho, Wo = ((H - 1) * s - 2 * p + k + op, (W - 1) * s - 2 * p + k + op) if tr else \
+        ((H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1)
+    rp = torch.randn(B, Ho, Wo, L.cout_store, generator=g).to(DEV) if pre else None
+    rq = torch.randn(B, Ho // post_up, Wo // post_up, L.cout_store, generator=g).to(DEV) if post_up else None
+    run = lambda: L(B, H, W, a, b, geo=gp, res_pre=rp, res_post=rq, post_up=max(post_up, 1))  # noqa: E731
+    monkeypatch.delenv("DAMVS_HALO_RS", raising=False)
+    y_rs = run()
+    monkeypatch.setenv("DAMVS_HALO_RS", "0")
+    y_pl = run()
+    torch.cuda.synchronize()
+    assert torch.isfinite(y_rs).all()
+    assert torch.equal(y_rs, y_pl)

@@ -14,13 +14,13 @@ for dt in f32 bf16; do for st in 1 0; do
   [ -f damvsnet_amd/ab/libdamvs_clamp.so ] && DAMVS_LIB=damvsnet_amd/ab/libdamvs_clamp.so step timeout -k 10 120 python -u tools/diag_warp_streams.py --layout nhwc --dtype $dt --stage $st > gpurun_out/r05b_diag_${dt}_s${st}_clamp.jsonl 2>&1
 done; done
 grep -c '"voxels": 0' gpurun_out/r05b_diag_*.jsonl
-step timeout -k 10 200 python -u tools/kbench2d.py --dtype f32 --only D,E,F,G,L,N > gpurun_out/r05b_k2d_f32.txt 2>&1
+step timeout -k 10 200 python -u tools/kbench2d.py --dtype f32 --only D,E,F,G,L,M,N,O,Q > gpurun_out/r05b_k2d_f32.txt 2>&1
 tail -9 gpurun_out/r05b_k2d_f32.txt
-DAMVS_WIDE_RS=0 step timeout -k 10 200 python -u tools/kbench2d.py --dtype f32 --only D,F,L,N > gpurun_out/r05b_k2d_f32_ag.txt 2>&1
+DAMVS_WIDE_RS=0 DAMVS_HALO_RS=0 step timeout -k 10 200 python -u tools/kbench2d.py --dtype f32 --only D,F,G,L,M,N,O,Q > gpurun_out/r05b_k2d_f32_ag.txt 2>&1
 tail -6 gpurun_out/r05b_k2d_f32_ag.txt
 step timeout -k 10 240 python -u tools/layer_times.py --dtype f32 --top 70 > gpurun_out/r05b_layers_f32.txt 2>&1
 head -3 gpurun_out/r05b_layers_f32.txt
-DAMVS_CONV2D_G32=0 DAMVS_WIDE_RS=0 step timeout -k 10 240 python -u tools/layer_times.py --dtype f32 --top 70 > gpurun_out/r05b_layers_f32_base.txt 2>&1
+DAMVS_CONV2D_G32=0 DAMVS_WIDE_RS=0 DAMVS_HALO_RS=0 step timeout -k 10 240 python -u tools/layer_times.py --dtype f32 --top 70 > gpurun_out/r05b_layers_f32_base.txt 2>&1
 head -3 gpurun_out/r05b_layers_f32_base.txt
 step timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --dtype f32 --no-cpu-baseline > gpurun_out/r05b_bench_f32.json 2> gpurun_out/r05b_bench_f32.err
 python -c "import json;d=json.load(open('gpurun_out/r05b_bench_f32.json'));print(d['value'],d['ms_per_step'],d['ms_per_stage'])" || tail -5 gpurun_out/r05b_bench_f32.err
