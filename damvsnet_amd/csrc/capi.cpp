@@ -310,27 +310,16 @@ struct Workspace {
 };
 
 // c[i] holds conv_i's output for i = 0..6 (conv7/9/11 accumulate in place into c4/c2/c0).
-// Channel-blocked copies of the feature maps for the warp's gathers when a pixel is wider than 32 bytes (stage 1:
-// 32 bf16 channels). 32-byte pixels (stage 2: 16 bf16 channels) are gathered NHWC in place: with the pipeline's
-// per-pixel hypotheses a bilinear corner then costs one cache line instead of one per 16-byte chunk (in-pipeline
-// stage-2 warp 2.25 -> 2.08 ms, and no repack launch), while at 64 bytes the blocked form stays ahead (1.21 against
-// 1.65 ms). DAMVS_WARP_BLOCK32=1 (A/B) blocks 32-byte pixels too; read once per process. damvs_warp_feat_blocked
-// exports the decision (engine.warp_blocked asks it, so Python and the stage forward always agree).
+// Channel-blocked copies of the feature maps ([B][C/E][h][w][E], one 16-byte chunk per plane) for the one-lane warp
+// kernel's gathers when a pixel is wider than 32 bytes. 32-, 64- and 128-byte pixels (bf16 C 16 / 32, fp32 C 16 / 32)
+// go to the channel-split warp when the view pipeline takes the view count (odd N): S = 2 / 4 / 8 lanes read a corner's
+// whole pixel record in one instruction from the NHWC maps in place, no repack launch. With DAMVS_WARP_SPLIT=0 or an
+// even view count the one-lane kernel gathers them, also unblocked (its per-chunk loads of one pixel hit one or two
+// lines either way). damvs_warp_feat_blocked exports the decision (engine.warp_blocked asks it, so Python and the stage
+// forward always agree).
 bool feat_blocked(int dtype, int C) {
-  static const int limit = [] {
-    const char* v = getenv("DAMVS_WARP_BLOCK32");
-    return v && v[0] == '1' ? 16 : 32;
-  }();
-  static const bool split_off = [] {  // the launcher's switch (k_warp.hip split_lanes): read the same variable
-    const char* v = getenv("DAMVS_WARP_SPLIT");
-    return v && v[0] == '0';
-  }();
   const int bytes = C * (dtype == DAMVS_BF16 ? 2 : 4);
-  // 32-, 64- and 128-byte pixels go to the channel-split warp, which gathers the NHWC maps in place (a lane quad reads a
-  // 64-byte pixel in one instruction, where the blocked layout needs one line per 16-byte chunk); with an even view
-  // count (no view pipeline) the one-lane kernel gathers them unblocked
-  if (!split_off && limit == 32 && (bytes == 32 || bytes == 64 || bytes == 128)) return false;
-  return bytes > limit;
+  return bytes > 32 && bytes != 64 && bytes != 128;
 }
 bool feat_needs_blocking(const damvs_stage* st) { return feat_blocked(st->dtype, st->C); }
 

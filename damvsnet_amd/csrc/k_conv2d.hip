@@ -816,10 +816,7 @@ hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a, bool dry = false) {
   constexpr int KC = W32 ? 32 : 4 * Stor<T>::E;
   // largest cout tile count (MTtot) the halo kernel takes: its B reuse pays off for narrow outputs,
   // while wide outputs are bound by the A (weight) stream the gather kernel already amortises
-  static const int max_mt = [] {
-    const char* v = getenv("DAMVS_CONV2D_HALO");
-    return v ? atoi(v) : 2;
-  }();
+  constexpr int max_mt = 2;  // (8: the wide layers too, measured 192-194 against 203-204 maps/s in round 3)
   // one-slice inputs (Cin = KC) and single cout tiles as well: the half-resolution GeoBlock convs with a depth
   // plane (32+g -> 32: 173 -> 146 us, 32+g -> 16: 101 -> 79 us at B=4); DAMVS_CONV2D_HALO_THIN=0 restores the
   // gather kernel for them
@@ -1833,15 +1830,8 @@ hipError_t launch_mt(hipStream_t s, const Conv2dArgs& a) {
 // GeoFeatureFusion layers have few pixels and many channels); 0 when the tile count rules out every width.
 int gather_mt(const Conv2dArgs& a, bool bf16) {
   const long long tiles = ((long long)a.B * a.Hq * a.Wq + 63) / 64 * a.nphase;
-  static const long long want = [] {
-    const char* v = getenv("DAMVS_CONV2D_WANT_TILES");
-    return v ? atoll(v) : 900LL;
-  }();
-  static const int maxmt = [] {
-    const char* v = getenv("DAMVS_CONV2D_MAXMT");
-    return v ? atoi(v) : 8;
-  }();
-  if (bf16 && maxmt >= 8 && a.MTtot % 8 == 0 && tiles * (a.MTtot / 8) >= want) return 8;
+  constexpr long long want = 900;  // (600 / 1400 and a widest tile of 4 measured within the run-to-run spread)
+  if (bf16 && a.MTtot % 8 == 0 && tiles * (a.MTtot / 8) >= want) return 8;
   if (a.MTtot % 4 == 0 && tiles * (a.MTtot / 4) >= want) return 4;
   if (a.MTtot % 2 == 0 && tiles * (a.MTtot / 2) >= want) return 2;
   return 1;

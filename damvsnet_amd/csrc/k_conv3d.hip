@@ -917,11 +917,7 @@ template <typename T, int CIN, int TXG>
 hipError_t launch_zslide_pair_t(hipStream_t s, const ConvArgs& a) {
   constexpr int PLANE = (LTH + 2) * (16 * TXG + 2) * (CIN / 8) * ZForm<T>::PL;
   const size_t smem = 4 * PLANE * 16;
-  static const int zc = [] {
-    const char* v = getenv("DAMVS_ZSLIDE_ZC");
-    const int z = v ? atoi(v) : 16;  // measured: 16 beats 8 and 32 over stages 1-2 at B=4
-    return z > 0 ? z : 16;
-  }();
+  constexpr int zc = 16;  // z-planes per block; measured: 16 beats 8 and 32 over stages 1-2 at B=4
   const int tx = (a.Wo + 16 * TXG - 1) / (16 * TXG), ty = (a.Ho + LTH - 1) / LTH, nzc = (a.Do + zc - 1) / zc;
   const long long nt = (long long)tx * ty * nzc * a.B;
   auto k = conv3d_zslide_pair_kernel<T, CIN, TXG>;
@@ -1141,11 +1137,7 @@ template <typename T>
 hipError_t launch_lds(hipStream_t s, const ConvArgs& a) {
   if (a.nphase != 1 || a.in_stride != 1 || a.out_stride != 1 || a.ph[0].ntaps != 27) return hipErrorNotSupported;
   const int MT = a.MT;
-  static const bool no_pair = [] {
-    const char* v = getenv("DAMVS_CONV_NO_PAIR");
-    return v && v[0] == '1';
-  }();
-  if (a.wpack_pair && a.Cout <= 8 && !no_pair) {
+  if (a.wpack_pair && a.Cout <= 8) {
     if (a.Cin == 8) return launch_lds_pair_t<T, 8>(s, a);
     if (a.Cin == 16) return launch_lds_pair_t<T, 16>(s, a);
     if (a.Cin == 32) return launch_lds_pair_t<T, 32>(s, a);  // fp32: the 138 KB tile (one block per CU)

@@ -573,11 +573,6 @@ hipError_t launch_prob_regress(hipStream_t s, int store, int B, int Cb, int D, i
 }
 
 size_t prob_regress_smem_bytes(int store, int Cb, int D) {
-  static const bool two_pass = [] {  // measured slower at cfgC (A/B knob)
-    const char* v = getenv("DAMVS_PROBREG_TWOPASS");
-    return v && v[0] == '1';
-  }();
-  if (two_pass) return (size_t)-1;  // the caller takes the two-pass form
   if (Cb == 8) return store == ST_BF16 ? prob_regress_smem<bf16_t, 8>(D) : prob_regress_smem<float, 8>(D);
   return store == ST_BF16 ? prob_regress_smem<bf16_t, 16>(D) : prob_regress_smem<float, 16>(D);
 }

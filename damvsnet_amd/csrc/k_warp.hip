@@ -623,8 +623,8 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
 #endif
 }
 
-// Lanes per voxel the launcher uses for C-channel maps: the channel-split kernel for NHWC maps of 2 or 4 16-byte chunks
-// per pixel when the view pipeline takes the view count (odd N >= 3), else 1 (the one-lane kernel).
+// Lanes per voxel the launcher uses for C-channel maps: the channel-split kernel for NHWC maps of 2, 4 or 8 16-byte
+// chunks per pixel when the view pipeline takes the view count (odd N >= 3), else 1 (the one-lane kernel).
 // DAMVS_WARP_SPLIT=0 (one lane per voxel everywhere) and DAMVS_WARP_NO_PIPE=1 (no view pipeline) both give 1, so the
 // launcher's block geometry and launch_k's kernel choice follow one predicate.
 bool warp_no_pipe() {
@@ -655,27 +655,17 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
   }();
   if constexpr (!BLK && (C * sizeof(T) == 32 || C * sizeof(T) == 64 || C * sizeof(T) == 128)) {
     if (split_lanes<T, C, BLK>(a) > 1) {
-      // DAMVS_WARP_LDS_PAD (A/B): unused dynamic LDS per block, capping the blocks per CU (fewer pixels in flight
-      // per XCD, a smaller L2 working set)
-      static const size_t pad = [] {
-        const char* e = getenv("DAMVS_WARP_LDS_PAD");
-        return e ? (size_t)atoll(e) : (size_t)0;
-      }();
       if (a.N == 5 && !runtime_views)
-        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, 4>), grid, dim3(256), pad, s, a, a.rt, npb, dchunk, ndc);
+        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, 4>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
       else
-        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, -1>), grid, dim3(256), pad, s, a, a.rt, npb, dchunk, ndc);
+        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, -1>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
       return;
     }
   }
   // view pipeline: unrolled for N = 5 (the DTU default) at 16 channels (stage 2; A/B: 2.29 against 2.37 ms, while
   // stage 3 runs 1.47 against 1.50 ms on the runtime loop), a runtime view loop for any other odd
   // N (7, 11: the cfgD / cfgE benchmark configs; 3) and for 32 channels (the unrolled form needs 360 registers)
-  static const bool pipe32 = [] {  // DAMVS_WARP_PIPE32=0: 32-channel maps (stage 1) on the generic view loop
-    const char* v = getenv("DAMVS_WARP_PIPE32");
-    return !(v && v[0] == '0');
-  }();
-  const bool pipe = (C <= 16 || pipe32) && !no_pipe && a.N >= 3 && (a.N - 1) % 2 == 0;
+  const bool pipe = !no_pipe && a.N >= 3 && (a.N - 1) % 2 == 0;
   if constexpr (C == 16) {
     if (pipe && a.N == 5 && !runtime_views) {
       hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 4>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
@@ -726,10 +716,7 @@ hipError_t launch_c(hipStream_t s, const WarpArgs& a0) {
   }
   // depth chunk: as long as possible (locality) while keeping >= ~4 blocks per CU in flight
   int dchunk = a.D;
-  static const long long minblk = [] {
-    const char* e = getenv("DAMVS_WARP_MINBLK");
-    return e ? atoll(e) : 2048LL;
-  }();
+  constexpr long long minblk = 2048;  // (512 - 32768 measured flat within 3 %, 16384+ slower in the pipeline)
   while (dchunk > 2 && (long long)npb * a.B * ((a.D + dchunk - 1) / dchunk) < minblk) dchunk = (dchunk + 1) / 2;
   const int ndc = (a.D + dchunk - 1) / dchunk;
   dim3 grid((unsigned)(npb * ndc * a.B));

@@ -10,9 +10,8 @@ run() {  # run <label> [VAR=value ...]
     > gpurun_out/sw.log 2>&1 || { echo "$label failed"; tail -3 gpurun_out/sw.log; exit 1; }
   echo "$label $(tail -1 gpurun_out/sw.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
 }
-for cfg in "DAMVS_ZSLIDE_ZC=8" "DAMVS_ZSLIDE_ZC=32" "DAMVS_CONV2D_WANT_TILES=600" "DAMVS_CONV2D_WANT_TILES=1400" \
-           "DAMVS_WARP_MINBLK=1024" "DAMVS_CONV2D_HALO=8" "DAMVS_CONV2D_MAXMT=4" "DAMVS_PROB_MFMA=0" \
-           "DAMVS_CONV_XPAIR=0" "DAMVS_CONV2D_XPAIR=0" "DAMVS_CONV_NO_ZSLIDE=1" "DAMVS_DECONV_NO_ZSLIDE=1"; do
+for cfg in "DAMVS_PROB_MFMA=0" "DAMVS_CONV_XPAIR=0" "DAMVS_CONV2D_XPAIR=0" "DAMVS_CONV_NO_ZSLIDE=1" \
+           "DAMVS_DECONV_NO_ZSLIDE=1" "DAMVS_WIDE_RS=0" "DAMVS_HALO_RS=0" "DAMVS_CONV2D_G32=0"; do
   for rep in 1 2; do
     run "default" X=1
     run "$cfg" "$cfg"
