@@ -63,6 +63,7 @@ struct LayerPlan {
   float wscale = 1.f;  // fp32: 2^-k of the split-f16 weights (split_weights)
   void* wpack32 = nullptr;  // fp32: the z-streamed kernel's 32-K split packing (ConvArgs::wpack32)
   void* wgat32 = nullptr;   // fp32: the gather kernel's 32-K split packing (ConvArgs::wgat32; may alias wpack32)
+  int k32_chunks[kMaxPhases] = {0}, k32_off[kMaxPhases] = {0};  // its phases' K chunks / weight offsets (build_phases 32)
 };
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -369,6 +370,8 @@ ConvArgs conv_args(const damvs_stage* st, int li, int B, const Shapes& S, int li
   a.wpack_pair = P.wpack_pair;
   a.wpack32 = P.wpack32;
   a.wgat32 = P.wgat32;
+  std::memcpy(a.k32_chunks, P.k32_chunks, sizeof(a.k32_chunks));
+  std::memcpy(a.k32_off, P.k32_off, sizeof(a.k32_off));
   a.bias = P.bias;
   a.B = B;
   a.Cin = P.cin;
@@ -545,6 +548,7 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
       const std::vector<uint16_t> h = split_weights_blocked(p32, kexp);
       rc = upload(h.data(), h.size() * 2, &P.wpack32);
       P.wgat32 = P.wpack32;  // the same plain 32-K packing serves the gather kernel
+      for (int p = 0; p < P32.nphase; ++p) P.k32_chunks[p] = P32.ph[p].kchunks, P.k32_off[p] = P32.ph[p].w_off;
     } else if (rc == DAMVS_OK && dtype != DAMVS_BF16 && P.cout > 8) {
       // the gather kernel's 32-K form (conv3d_mfma_kernel<float, MT, false, true>: 16x16x32 f16 split products, twice the
       // 16-K form's MFMA rate) for the layers that run on it (conv3, conv5, conv6, conv7 and the tile kernels' fallbacks)
@@ -554,6 +558,7 @@ int damvs_stage_create(const damvs_costreg_params* cr, const damvs_aggweight_par
       pack_layer<float>(P32, wf, 8, p32, cvt_f32);
       const std::vector<uint16_t> h = split_weights_blocked(p32, kexp);
       rc = upload(h.data(), h.size() * 2, &P.wgat32);
+      for (int p = 0; p < P32.nphase; ++p) P.k32_chunks[p] = P32.ph[p].kchunks, P.k32_off[p] = P32.ph[p].w_off;
     }
     if (rc == DAMVS_OK && P.kind == DECONV_S2 && P.cout <= 8) {
       build_phases_xpair(P, 4 * E);

@@ -91,6 +91,9 @@ struct ConvArgs {
   float wscale;  // accumulator scale of the epilogue: 2^-k of the split-f16 fp32 weights (damvs_device.h), 1 for bf16
   FastDiv div_wq, div_hq, div_dq;  // set by launch_conv3d
   ConvPhase ph[kMaxPhases];
+  // fp32: the phases of wgat32 (build_phases(., 32) at layer creation): K chunks and weight offsets at 32 K per chunk
+  // (the taps are those of ph)
+  int k32_chunks[kMaxPhases], k32_off[kMaxPhases];
 };
 
 // ---------------------------------------------------------------- 2D front-end convolutions

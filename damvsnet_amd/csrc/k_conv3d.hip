@@ -1737,11 +1737,9 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
     const char* kv = getenv("DAMVS_CONV3D_K16");
     if (a.wgat32 && !(kv && kv[0] == '1')) {
       ConvArgs a2 = a;
-      int w = 0;
-      for (int p = 0; p < a.nphase; ++p) {  // the phases at 32 K per chunk (build_phases(., 32), pack_layer at E 8)
-        a2.ph[p].kchunks = (a.ph[p].ntaps * a.Cin + 31) / 32;
-        a2.ph[p].w_off = w;
-        w += a2.ph[p].kchunks * a.MT;
+      for (int p = 0; p < a.nphase; ++p) {  // the phases of the 32-K packing (LayerPlan, build_phases(., 32))
+        a2.ph[p].kchunks = a.k32_chunks[p];
+        a2.ph[p].w_off = a.k32_off[p];
       }
       switch (a.MT) {
         case 1: hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, false, true>), grid, dim3(256), 0, s, a2, nq); break;
