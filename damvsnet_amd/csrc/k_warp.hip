@@ -655,7 +655,11 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
   }();
   if constexpr (!BLK && (C * sizeof(T) == 32 || C * sizeof(T) == 64 || C * sizeof(T) == 128)) {
     if (split_lanes<T, C, BLK>(a) > 1) {
-      if (a.N == 5 && !runtime_views)
+      // fp32 storage: always the runtime view loop. The unrolled N = 5 form of the fp32 split kernel computes wrong
+      // voxels in lanes 48-63 while another stream's U-Net kernels share its CUs (round 5, tools/diag_warp_streams.py
+      // --dtype f32: 6-12 of 24 launches beside conv1 differ; the runtime loop and the one-lane kernel: 0 of 24 at
+      // stages 1 and 2; DESIGN.md section 4 "Concurrent streams"), while its bf16 form passes the same tests
+      if (a.N == 5 && !runtime_views && sizeof(T) == 2)
         hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, 4>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
       else
         hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, -1>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);

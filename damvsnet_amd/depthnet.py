@@ -67,8 +67,14 @@ class DepthNet(nn.Module):
         """Raise damvsnet_amd._capi.DamvsRangeError when a stage forward since the last check produced non-finite
         depth / confidence / variance (the fp32 path's split-f16 products are limited to |x| < 65520; the reference's
         fp32 convolutions are not). Synchronises the streams those forwards ran on."""
-        for eng in list(self._engines.values()):
-            eng.check_range()
+        err = None
+        for eng in list(self._engines.values()):  # every engine's status is read (and cleared) before raising
+            try:
+                eng.check_range()
+            except Exception as e:  # noqa: BLE001 (re-raised below)
+                err = err or e
+        if err is not None:
+            raise err
 
     def forward(self, stage_idx, features, proj_matrices, depth_values, num_depth, cost_regularization,
                 prob_volume_init=None, return_prob_volume=True):

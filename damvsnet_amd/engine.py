@@ -117,8 +117,14 @@ class StageEngine:
         """Raise DamvsRangeError if any forward since the last check wrote non-finite depth / confidence / variance
         (damvs_stage_status: sticky per workspace until read; synchronises the streams those forwards ran on)."""
         pending, self._unchecked = self._unchecked, {}
-        for stream, ws in pending.items():
-            check(self._lib.damvs_stage_status(self.handle, stream, ptr(ws), ws.numel()))
+        err = None
+        for stream, ws in pending.items():  # every status is read (and cleared) before the first error is raised
+            try:
+                check(self._lib.damvs_stage_status(self.handle, stream, ptr(ws), ws.numel()))
+            except _capi.DamvsError as e:
+                err = err or e
+        if err is not None:
+            raise err
 
     # ---- split entry points (parity tests / sharded execution)
     def warp_aggregate(self, feats, proj, hyps, rt=None, layout=_capi.DAMVS_LAYOUT_NHWC, out=None):
