@@ -194,6 +194,14 @@ __device__ __forceinline__ float relu(float x) { return x < 0.f ? 0.f : x; }
 // 5-7x the bf16 kernel's time instead of ~3x).
 #define DAMVS_INLINE __attribute__((always_inline))
 
+// compile-time bool for generic-lambda specialisation (step(BoolC<true>(), ...): decltype(arg)::value)
+template <bool B> struct BoolC {
+  static constexpr bool value = B;
+};
+template <int I> struct IntC {
+  static constexpr int value = I;
+};
+
 typedef unsigned int v4u32_t __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u32_t __attribute__((ext_vector_type(2)));
 

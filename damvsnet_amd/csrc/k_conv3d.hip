@@ -704,28 +704,70 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 && CIN <= 16 ? 2 : 
     f32x4_t acc[TXG];
 #pragma unroll
     for (int xg = 0; xg < TXG; ++xg) acc[xg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < KCHUNKS; ++s) {
-      const frag wf = wreg[s];
-      const int kt = (s * KC) / CIN, kc = ((s * KC) % CIN) / E;
+    auto coord = [&](int s, int& off, int& kc, int& dx) DAMVS_INLINE {  // K chunk s: slot offset, chunk, column
+      const int kt = (s * KC) / CIN;
+      kc = ((s * KC) % CIN) / E;
       const int dz = kt / 12;  // uniform over the chunk's taps (12 taps per dz, 1/2/4 taps per chunk)
       auto toff = [](int t) { return (((t / 3) % 4) * PW + t % 3) * (PL == 1 ? CH : S); };
-      int off = toff(kt), dx = kt % 3;
+      off = toff(kt), dx = kt % 3;
       if (KC > CIN) {
         off = gi == 1 ? toff(kt + 1) : off;
         off = gi == 2 ? toff(kt + 2) : off;
         off = gi == 3 ? toff(kt + 3) : off;
         if (PL == 2) dx = (kt + gi) % 3;
       }
-      if constexpr (PL == 1) {
+      off += (int)(pl[dz] - ring);
+    };
+    if constexpr (PL == 1) {
+#pragma unroll
+      for (int s = 0; s < KCHUNKS; ++s) {
+        const frag wf = wreg[s];
+        const int kt = (s * KC) / CIN, kc = ((s * KC) % CIN) / E;
+        const int dz = kt / 12;  // uniform over the chunk's taps (12 taps per dz, 1/2/4 taps per chunk)
+        auto toff = [](int t) { return (((t / 3) % 4) * PW + t % 3) * CH; };
+        int off = toff(kt);
+        if (KC > CIN) {
+          off = gi == 1 ? toff(kt + 1) : off;
+          off = gi == 2 ? toff(kt + 2) : off;
+          off = gi == 3 ? toff(kt + 3) : off;
+        }
         const uint4* src = pl[dz] + off + kc;
 #pragma unroll
         for (int xg = 0; xg < TXG; ++xg) Z::mma(wf, src[16 * xg * CH], acc[xg]);
-      } else {
-        const uint4* src = pl[dz] + off;
-        const int sw = dx == 0 ? sw0 : dx == 1 ? sw1 : sw2;  // +16 columns keep the swizzle
+      }
+    } else if constexpr (CIN != 8) {  // (fp32 CIN 16 / 32: the input-plane walk runs these layers; no prefetch, which
+                                      // spills at CIN 16)
 #pragma unroll
-        for (int xg = 0; xg < TXG; ++xg) Z::mma(wf, Z::bread(src + 16 * xg * S, kc + gc, CH, sw), acc[xg]);
+      for (int s = 0; s < KCHUNKS; ++s) {
+        int off, kc, dx;
+        coord(s, off, kc, dx);
+        const int sw = dx == 0 ? sw0 : dx == 1 ? sw1 : sw2;
+#pragma unroll
+        for (int xg = 0; xg < TXG; ++xg) Z::mma(wreg[s], Z::bread(ring + off + 16 * xg * S, kc + gc, CH, sw), acc[xg]);
+      }
+    } else {
+      // fp32 CIN 8 (stage-3 conv0): chunk s + 1's B pieces read while chunk s's MFMAs run (the sched_group_barriers
+      // hold that order; the compiler's own schedule read each piece pair just before its MFMAs and waited on it):
+      // stage 3 1.27 -> 1.24 ms at B = 4 (tools/unet_layers.py, profiles/r05/ab_conv0_r05j.txt)
+      frag b0[TXG], b1[TXG];
+#pragma unroll
+      for (int s = -1; s < KCHUNKS; ++s) {
+        if (s + 1 < KCHUNKS) {
+          int off, kc, dx;
+          coord(s + 1, off, kc, dx);
+          const int sw = dx == 0 ? sw0 : dx == 1 ? sw1 : sw2;  // +16 columns keep the swizzle
+#pragma unroll
+          for (int xg = 0; xg < TXG; ++xg) {
+            const frag f = Z::bread(ring + off + 16 * xg * S, kc + gc, CH, sw);
+            if ((s + 1) & 1) b1[xg] = f;
+            else b0[xg] = f;
+          }
+        }
+        if (s < 0) continue;
+#pragma unroll
+        for (int xg = 0; xg < TXG; ++xg) Z::mma(wreg[s], (s & 1) ? b1[xg] : b0[xg], acc[xg]);
+        if (s + 1 < KCHUNKS) __builtin_amdgcn_sched_group_barrier(0x100, 2 * TXG, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 3 * TXG, 0);
       }
     }
 #pragma unroll

@@ -581,9 +581,24 @@ __global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const
     __amdgpu_buffer_rsrc_t r;
     if constexpr (NVC > 0) r = rs[v];
     else r = make_rsrc(a.feats[v + 1], fbytes);
+#if defined(DAMVS_DIAG_WARP_SAMEX) || defined(DAMVS_DIAG_WARP_2TAP)
+    // diagnostic builds only (tools/gpu_ab_warp_ta.sh; wrong results): SAMEX reads the west corners twice (the same
+    // loads, half the distinct lines), 2TAP issues only the west corners (half the loads)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#ifdef DAMVS_DIAG_WARP_2TAP
+      if (k & 1) {
+        rv[k] = rv[k - 1];
+        continue;
+      }
+#endif
+      rv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, t.off[k & 2] + qoff, sb, 0));
+    }
+#else
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       rv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, t.off[k] + qoff, sb, 0));
+#endif
 #pragma unroll
     for (int k = 0; k < 4; ++k) wt[k] = t.wt[k];
   };

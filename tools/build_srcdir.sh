@@ -1,0 +1,18 @@
+#!/usr/bin/env bash
+# Build libdamvs from another source directory (its csrc/ and include/) into damvsnet_amd/ab/libdamvs_<name>.so, for
+# A/B runs through DAMVS_LIB of kernels that are not in the working tree (diagnostics).  tools/build_srcdir.sh <name> <dir>
+set -eu
+R=$(cd "$(dirname "$0")/.." && pwd)
+name=$1; S=$2
+T=$(mktemp -d)
+mkdir -p "$R/damvsnet_amd/ab"
+objs=""
+for f in "$S"/csrc/*.hip "$S"/csrc/*.cpp; do
+  o=$T/$(basename "$f").o
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I"$S/include" -I"$S/csrc" -x hip -c "$f" -o "$o" &
+  objs="$objs $o"
+done
+wait
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$R/damvsnet_amd/ab/libdamvs_$name.so" $objs
+rm -rf "$T"
+echo "$R/damvsnet_amd/ab/libdamvs_$name.so"

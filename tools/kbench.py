@@ -24,8 +24,11 @@ def main():
     ap.add_argument("--config", default="cfgC")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--dtype", default=None, choices=["f32", "bf16"], help="default: the config's")
     args = ap.parse_args()
     H, W, N, nd, dtype, _ = bench.CONFIGS[args.config]
+    if args.dtype:
+        dtype = torch.float32 if args.dtype == "f32" else torch.bfloat16
     dev = torch.device("cuda")
     net, _ = bench.build_model(nd, dtype, dev)
     s = args.stage - 1
@@ -74,7 +77,7 @@ def main():
             run()
         e1.record()
         torch.cuda.synchronize()
-    print("%s stage%d %s B=%d: %.3f ms per call" % (args.kernel, args.stage, args.config, B,
+    print("%s stage%d %s %s B=%d: %.3f ms per call" % (args.kernel, args.stage, args.config, str(dtype)[6:], B,
                                                    e0.elapsed_time(e1) / args.iters))
 
 
