@@ -96,6 +96,32 @@ template <> struct Rec16<bf16_t> {
   }
 };
 
+// CU-exclusive warp blocks (build option -DDAMVS_WARP_EXCLUSIVE, off in the product): every warp block holds the
+// whole register file of its CU -- R registers per wave reserved (an asm clobber of the last one makes the allocation
+// R), 512 / R waves per SIMD, i.e. 131072 / R threads per block: R = 128 (1024-thread blocks, 4 waves per SIMD) for the
+// product kernels, 256 / 512 for the one-lane kernels whose 16 / 32-channel vectors need more -- so no other kernel's
+// wave can be resident beside a warp block. Measured in round 5 against the concurrent-stream fault (DESIGN.md section
+// 4, "Concurrent streams"): it turned one failing instruction stream clean but not another, and costs 3-13 % of warp
+// time (profiles/r05/ab_warp_exclusive_r05m.txt), so the product keeps 256-thread blocks and the pinned kernels.
+template <typename T, int C, int MODE, bool SPLIT>
+constexpr int warp_regs() {
+  if (SPLIT) return MODE == AGG_VARIANCE && sizeof(T) == 2 ? 256 : 128;
+  const int rec = C * (int)sizeof(T);  // bytes per pixel, kept whole in registers by one lane
+  return rec <= 16 ? 128 : rec <= 32 ? 256 : 512;
+}
+#ifndef DAMVS_WARP_EXCLUSIVE
+template <int R> constexpr int warp_block() { return 256; }
+#define DAMVS_WARP_RESERVE(R)
+#else
+template <int R> constexpr int warp_block() { return 131072 / R; }  // (512 / R waves per SIMD) x 4 SIMDs x 64 lanes
+#define DAMVS_WARP_RESERVE(R)                                  \
+  do {                                                          \
+    if constexpr ((R) == 128) asm volatile("" ::: "v127");     \
+    else if constexpr ((R) == 256) asm volatile("" ::: "v255"); \
+    else asm volatile("" ::: "v255", "a255");                   \
+  } while (0)
+#endif
+
 // Bilinear footprint of one sample at (ix, iy): byte offsets of the nw, ne, sw, se pixel records inside one
 // batch element's map (rec bytes per record) and their weights. A corner outside the map gets the offset
 // kOOB, so its buffer load returns 0: grid_sample's zero padding without a weight select. Samples far
@@ -149,7 +175,7 @@ __device__ __forceinline__ int warp_pixel(const WarpArgs& a, int pb, int i, int 
   return (x < a.w && yl < a.rows) ? yl * a.w + x : -1;
 }
 
-// Work decomposition (locality): a block owns 256 consecutive pixels of one image row band and a
+// Work decomposition (locality): a block owns its block size of consecutive pixels of one image row band and a
 // chunk of `dchunk` consecutive depth planes, and each thread walks its pixel through those planes.
 // Consecutive hypotheses of one pixel sample along one epipolar segment, so a block's gathers stay
 // inside a narrow band of each source image; blocks are dealt so that each XCD gets a contiguous
@@ -165,8 +191,10 @@ __device__ __forceinline__ int warp_pixel(const WarpArgs& a, int pb, int i, int 
 // current view is reduced, and the loads are unconditional (the last plane re-reads its own last
 // view) so the vmcnt waits count exactly.
 template <typename T, int C, int MODE, bool BLK, int NVC>
-__global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC == 0 && MODE == AGG_ADAPTIVE ? 3 : 1)) void warp_aggregate_kernel(const WarpArgs a, const float* __restrict__ cams,
+__global__ __attribute__((amdgpu_flat_work_group_size(1, (warp_block<warp_regs<T, C, MODE, false>()>())))) DAMVS_WAVES((warp_block<warp_regs<T, C, MODE, false>()>() == 256 && sizeof(T) == 2 && C == 32 && NVC == 0 && MODE == AGG_ADAPTIVE ? 3 : 1)) void warp_aggregate_kernel(const WarpArgs a, const float* __restrict__ cams,
                                                              int npix_blocks, int dchunk, int ndchunks) {
+  constexpr int BLOCK = warp_block<warp_regs<T, C, MODE, false>()>();
+  DAMVS_WARP_RESERVE((warp_regs<T, C, MODE, false>()));
   constexpr int E = Stor<T>::E, NQ = C / E;
   static_assert(NVC % 2 == 0 || NVC < 0, "the view pipeline alternates two register sets");
   const int hw = a.h * a.w;  // feature-map plane (computed rows: y0 .. y0 + rows - 1)
@@ -205,7 +233,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC 
 #else
   const float* __restrict__ cam = cams + (size_t)b * (a.N - 1) * 12;
 #endif
-  const int p = warp_pixel(a, pb, threadIdx.x, 256);
+  const int p = warp_pixel(a, pb, threadIdx.x, BLOCK);
   if (p < 0) return;
   const int yl = p / a.w, x = p - yl * a.w;
   const int y = a.y0 + yl, pg = y * a.w + x;  // reference-image row and pixel
@@ -444,11 +472,12 @@ __device__ __forceinline__ float swz_xor4(float v) {
 }
 
 template <typename T, int C, int MODE, int NVC>
-__global__ __launch_bounds__(256) void warp_split_kernel(const WarpArgs a, const float* __restrict__ cams,
-                                                         int npix_blocks, int dchunk, int ndchunks) {
+__global__ __attribute__((amdgpu_flat_work_group_size(1, (warp_block<warp_regs<T, C, MODE, true>()>())))) void warp_split_kernel(const WarpArgs a, const float* __restrict__ cams,
+                                                                int npix_blocks, int dchunk, int ndchunks) {
+  DAMVS_WARP_RESERVE((warp_regs<T, C, MODE, true>()));
   constexpr int E = Stor<T>::E;  // channels per 16-byte chunk
   constexpr int S = C / E;       // lanes per voxel
-  constexpr int PPB = 256 / S;   // pixels per block
+  constexpr int PPB = warp_block<warp_regs<T, C, MODE, true>()>() / S;  // pixels per block
   static_assert(S == 2 || S == 4 || S == 8, "channel-split form: 2, 4 or 8 chunks per pixel");
   static_assert(NVC % 2 == 0 || NVC < 0, "the view pipeline alternates two register sets");
   const int hw = a.h * a.w;
@@ -675,9 +704,9 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
       // --dtype f32: 6-12 of 24 launches beside conv1 differ; the runtime loop and the one-lane kernel: 0 of 24 at
       // stages 1 and 2; DESIGN.md section 4 "Concurrent streams"), while its bf16 form passes the same tests
       if (a.N == 5 && !runtime_views && sizeof(T) == 2)
-        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, 4>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
+        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, 4>), grid, dim3(warp_block<warp_regs<T, C, MODE, true>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
       else
-        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, -1>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
+        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, -1>), grid, dim3(warp_block<warp_regs<T, C, MODE, true>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
       return;
     }
   }
@@ -687,14 +716,14 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
   const bool pipe = !no_pipe && a.N >= 3 && (a.N - 1) % 2 == 0;
   if constexpr (C == 16) {
     if (pipe && a.N == 5 && !runtime_views) {
-      hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 4>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
+      hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 4>), grid, dim3(warp_block<warp_regs<T, C, MODE, false>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
       return;
     }
   }
   if (pipe)
-    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, -1>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
+    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, -1>), grid, dim3(warp_block<warp_regs<T, C, MODE, false>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
   else
-    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 0>), grid, dim3(256), 0, s, a, a.rt, npb, dchunk, ndc);
+    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 0>), grid, dim3(warp_block<warp_regs<T, C, MODE, false>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
 }
 
 template <typename T, int MODE, bool BLK>
@@ -702,13 +731,19 @@ hipError_t launch_c(hipStream_t s, const WarpArgs& a0) {
   WarpArgs a = a0;
   // 32-bit buffer offsets: each view's feature tensor must stay below 2 GiB
   if ((long long)a.B * a.h * a.w * a.C * (long long)sizeof(T) >= (1LL << 31)) return hipErrorInvalidValue;
-  int lanes = 1;  // lanes per voxel of the kernel launch_k will pick (pixels per block = 256 / lanes)
+  // lanes per voxel and block size of the kernel launch_k will pick (pixels per block = block / lanes)
+  int lanes = 1, block = 256;
+  auto pick = [&](auto cc) {
+    constexpr int CC = decltype(cc)::value;
+    lanes = split_lanes<T, CC, BLK>(a);
+    block = lanes > 1 ? warp_block<warp_regs<T, CC, MODE, true>()>() : warp_block<warp_regs<T, CC, MODE, false>()>();
+  };
   switch (a.C) {
-    case 8: lanes = split_lanes<T, 8, BLK>(a); break;
-    case 16: lanes = split_lanes<T, 16, BLK>(a); break;
-    case 32: lanes = split_lanes<T, 32, BLK>(a); break;
+    case 8: pick(IntC<8>()); break;
+    case 16: pick(IntC<16>()); break;
+    case 32: pick(IntC<32>()); break;
   }
-  const int ppb = 256 / lanes;
+  const int ppb = block / lanes;
   // Pixel blocks as R-row tiles (R divides ppb) dealt across the full width, or in strips SW pixels wide:
   // DAMVS_WARP_TILE="R,SW", default R = 8; "0": ppb consecutive pixels of the row-major computed rows. The
   // 8-row tiles keep vertically adjacent pixels, whose bilinear footprints share source rows, on one CU: stage-2
@@ -735,7 +770,8 @@ hipError_t launch_c(hipStream_t s, const WarpArgs& a0) {
   }
   // depth chunk: as long as possible (locality) while keeping >= ~4 blocks per CU in flight
   int dchunk = a.D;
-  constexpr long long minblk = 2048;  // (512 - 32768 measured flat within 3 %, 16384+ slower in the pipeline)
+  // (in 256-thread blocks: 512 - 32768 measured flat within 3 %, 16384+ slower in the pipeline)
+  const long long minblk = 2048LL * 256 / block;
   while (dchunk > 2 && (long long)npb * a.B * ((a.D + dchunk - 1) / dchunk) < minblk) dchunk = (dchunk + 1) / 2;
   const int ndc = (a.D + dchunk - 1) / dchunk;
   dim3 grid((unsigned)(npb * ndc * a.B));
