@@ -77,6 +77,7 @@ SIGNATURES = (
     ("damvs_warp_aggregate", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_void_p),
                                      c_int, c_void_p, c_void_p, c_void_p)),
     ("damvs_warp_feat_blocked", c_int, (c_int, c_int)),
+    ("damvs_warp_feat_blocked_n", c_int, (c_int, c_int, c_int)),
     ("damvs_block_channels", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_void_p),
                                      ctypes.POINTER(c_void_p))),
     ("damvs_costreg_logits", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t,

@@ -312,17 +312,19 @@ struct Workspace {
 
 // c[i] holds conv_i's output for i = 0..6 (conv7/9/11 accumulate in place into c4/c2/c0).
 // Channel-blocked copies of the feature maps ([B][C/E][h][w][E], one 16-byte chunk per plane) for the one-lane warp
-// kernel's gathers when a pixel is wider than 32 bytes. 32-, 64- and 128-byte pixels (bf16 C 16 / 32, fp32 C 16 / 32)
-// go to the channel-split warp when the view pipeline takes the view count (odd N): S = 2 / 4 / 8 lanes read a corner's
-// whole pixel record in one instruction from the NHWC maps in place, no repack launch. With DAMVS_WARP_SPLIT=0 or an
-// even view count the one-lane kernel gathers them, also unblocked (its per-chunk loads of one pixel hit one or two
-// lines either way). damvs_warp_feat_blocked exports the decision (engine.warp_blocked asks it, so Python and the stage
-// forward always agree).
-bool feat_blocked(int dtype, int C) {
+// kernel's gathers when a pixel is wider than 32 bytes. 32-, 64- and 128-byte pixels (bf16 C 16 / 32, fp32 C 8 / 16 /
+// 32) go to the channel-split warp when the view pipeline takes the view count (odd N >= 3): S = 2 / 4 / 8 lanes read a
+// corner's whole pixel record in one instruction from the NHWC maps in place, no repack launch. Where the one-lane
+// kernel gathers them instead (even N, DAMVS_WARP_SPLIT=0) pixels wider than 32 bytes are blocked as well: stage 1 at
+// N = 6, cfgC B = 4, unblocked against blocked, fp32 (128-byte pixels) 8.44 against 3.62 ms, bf16 (64-byte) 2.04
+// against 1.58 ms; at N = 5 the split kernel on NHWC maps wins, fp32 2.05 against 2.38 ms (bf16 1.40 against 1.34 ms
+// before the 0.17 ms repack launch it saves; profiles/r05/ab_warp_layout_r05p.txt). damvs_warp_feat_blocked_n exports
+// the decision (engine.warp_blocked asks it, so Python and the stage forward always agree).
+bool feat_blocked(int dtype, int C, int N) {
   const int bytes = C * (dtype == DAMVS_BF16 ? 2 : 4);
-  return bytes > 32 && bytes != 64 && bytes != 128;
+  return bytes > 32 && !warp_split_for(bytes, N);
 }
-bool feat_needs_blocking(const damvs_stage* st) { return feat_blocked(st->dtype, st->C); }
+bool feat_needs_blocking(const damvs_stage* st, int N) { return feat_blocked(st->dtype, st->C, N); }
 
 Workspace plan_ws(const damvs_stage* st, int B, int N, int D, int h, int w) {
   const size_t es = st->dtype == DAMVS_BF16 ? 2 : 4;
@@ -337,7 +339,7 @@ Workspace plan_ws(const damvs_stage* st, int B, int N, int D, int h, int w) {
   ws.rt = o;
   o += align_up((size_t)B * (N > 1 ? N - 1 : 1) * 12 * 4);
   ws.feat = o;  // channel-blocked copies of the N feature maps (only when C spans several 16-B chunks)
-  if (feat_needs_blocking(st)) o += (size_t)N * align_up((size_t)B * h * w * st->C * es);
+  if (feat_needs_blocking(st, N)) o += (size_t)N * align_up((size_t)B * h * w * st->C * es);
   ws.vol = o;
   o += align_up(V * st->C * es);
   for (int i = 0; i < 7; ++i) {
@@ -715,7 +717,7 @@ int damvs_stage_forward_probed(const damvs_stage* st, void* stream, int B, int N
   float* rt = reinterpret_cast<float*>(ws + W.rt);
   int* status = reinterpret_cast<int*>(ws + W.status);
   DAMVS_TRY(hip_check(launch_proj_prepare(s, B, N, proj, rt), "proj_prepare launch"));
-  const bool blk = feat_needs_blocking(st);
+  const bool blk = feat_needs_blocking(st, N);
   const void* fv[kMaxViews];
   for (int v = 0; v < N; ++v) fv[v] = feats[v];
   if (blk) {  // repack to [B][C/E][h][w][E]: halves the cache lines each gather instruction touches
@@ -789,11 +791,14 @@ int damvs_warp_aggregate(const damvs_stage* st, void* stream, int B, int N, int 
                    "warp_aggregate launch");
 }
 
-int damvs_warp_feat_blocked(int dtype, int C) {
+int damvs_warp_feat_blocked_n(int dtype, int C, int N) {
   if (dtype != DAMVS_F32 && dtype != DAMVS_BF16) return fail(DAMVS_E_DTYPE, "dtype %d unsupported", dtype);
   if (C < 1) return fail(DAMVS_E_SHAPE, "C %d", C);
-  return feat_blocked(dtype, C) ? 1 : 0;
+  if (N < 2 || N > kMaxViews) return fail(DAMVS_E_SHAPE, "N %d", N);
+  return feat_blocked(dtype, C, N) ? 1 : 0;
 }
+
+int damvs_warp_feat_blocked(int dtype, int C) { return damvs_warp_feat_blocked_n(dtype, C, 5); }
 
 int damvs_block_channels(void* stream, int dtype, int N, int B, int h, int w, int C, const void* const* src,
                          void* const* dst) {

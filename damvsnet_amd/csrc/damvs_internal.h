@@ -144,6 +144,7 @@ struct FeatPtrs {
 };
 // blocked = features in channel-blocked layout [B][C/E][h][w][E] (E = 16 bytes of channels)
 hipError_t launch_warp_aggregate(hipStream_t s, int store, int mode, const WarpArgs& a, bool blocked);
+bool warp_split_for(int bytes, int N);  // the channel-split warp serves NHWC maps of these pixels at N views
 hipError_t launch_block_channels(hipStream_t s, int store, const FeatPtrs& src, const FeatPtrs& dst, int N, int B,
                                  int hw, int C);
 hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a);

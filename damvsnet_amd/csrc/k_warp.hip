@@ -678,16 +678,18 @@ bool warp_no_pipe() {
   }();
   return v;
 }
-template <typename T, int C, bool BLK>
-int split_lanes(const WarpArgs& a) {
+bool warp_split_enabled() {
   static const bool off = [] {
     const char* v = getenv("DAMVS_WARP_SPLIT");
     return v && v[0] == '0';
   }();
+  return !off && !warp_no_pipe();
+}
+
+template <typename T, int C, bool BLK>
+int split_lanes(const WarpArgs& a) {
   constexpr int S = C * (int)sizeof(T) / 16;
-  if (BLK || off || warp_no_pipe() || (S != 2 && S != 4 && S != 8)) return 1;
-  const bool pipe_ok = a.N >= 3 && (a.N - 1) % 2 == 0;
-  return pipe_ok ? S : 1;
+  return !BLK && warp_split_for(C * (int)sizeof(T), a.N) ? S : 1;
 }
 
 template <typename T, int C, int MODE, bool BLK>
@@ -827,6 +829,12 @@ __global__ __launch_bounds__(256) void block_channels_kernel(const FeatPtrs src,
 }
 
 }  // namespace
+
+// Whether launch_warp_aggregate runs the channel-split kernel for NHWC maps of `bytes`-byte pixels at N views (the
+// predicate split_lanes applies per launch; capi's feature-layout choice asks it before the maps are laid out).
+bool warp_split_for(int bytes, int N) {
+  return warp_split_enabled() && (bytes == 32 || bytes == 64 || bytes == 128) && N >= 3 && (N - 1) % 2 == 0;
+}
 
 hipError_t launch_warp_aggregate(hipStream_t s, int store, int mode, const WarpArgs& a, bool blocked) {
   if (blocked) return store == ST_BF16 ? launch_t<bf16_t, true>(s, mode, a) : launch_t<float, true>(s, mode, a);

@@ -208,11 +208,12 @@ def proj_prepare(proj):
     return rt
 
 
-def warp_blocked(C, element_size):
-    """Whether damvs_stage_forward gathers channel-blocked copies of C-channel feature maps: the library's own
-    decision (damvs_warp_feat_blocked), so split-entry callers lay the maps out exactly as the stage forward does."""
+def warp_blocked(C, element_size, N=5):
+    """Whether damvs_stage_forward gathers channel-blocked copies of C-channel feature maps at N views: the library's
+    own decision (damvs_warp_feat_blocked_n), so split-entry callers lay the maps out exactly as the stage forward
+    does."""
     lib = _capi.load_library()
-    r = lib.damvs_warp_feat_blocked(_capi.DAMVS_BF16 if element_size == 2 else _capi.DAMVS_F32, int(C))
+    r = lib.damvs_warp_feat_blocked_n(_capi.DAMVS_BF16 if element_size == 2 else _capi.DAMVS_F32, int(C), int(N))
     check(r if r < 0 else 0)
     return r == 1
 

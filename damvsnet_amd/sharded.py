@@ -385,7 +385,7 @@ class DepthShardedDepthNet:
                  for f in feats_nhwc]
         B, h, w, C = feats[0].shape
         layout = _capi.DAMVS_LAYOUT_NHWC
-        if warp_blocked(C, feats[0].element_size()):
+        if warp_blocked(C, feats[0].element_size(), len(feats)):
             feats, layout = block_channels(feats), _capi.DAMVS_LAYOUT_CBLOCK
         hyps = depth_values.float().contiguous()
         rt = proj_prepare(proj_matrices.float().contiguous())

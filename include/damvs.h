@@ -146,9 +146,12 @@ int damvs_warp_aggregate(const damvs_stage* st, void* stream, int B, int N, int 
                          const void* const* feats, int layout, const float* rt, const float* hyps, void* volume);
 
 /* NHWC [B][h][w][C] -> DAMVS_LAYOUT_CBLOCK for N maps (src[v] -> dst[v], device buffers). */
-/* 1 if the stage forward gathers C-channel maps of this dtype from channel-blocked copies (damvs_block_channels:
- * pixels wider than 32 bytes), 0 if it gathers the NHWC maps in place, negative on a bad argument. The split entry
- * point damvs_warp_aggregate takes either layout; callers that mirror damvs_stage_forward ask here. */
+/* 1 if the stage forward gathers C-channel maps of this dtype at N views from channel-blocked copies
+ * (damvs_block_channels: pixels wider than 32 bytes that the channel-split warp does not take -- it takes 32 / 64 /
+ * 128-byte pixels at odd N >= 3), 0 if it gathers the NHWC maps in place, negative on a bad argument. The split entry
+ * point damvs_warp_aggregate takes either layout; callers that mirror damvs_stage_forward ask here.
+ * damvs_warp_feat_blocked(dtype, C) is the N = 5 answer (the round-4 entry point, kept for existing callers). */
+int damvs_warp_feat_blocked_n(int dtype, int C, int N);
 int damvs_warp_feat_blocked(int dtype, int C);
 int damvs_block_channels(void* stream, int dtype, int N, int B, int h, int w, int C, const void* const* src,
                          void* const* dst);

@@ -25,8 +25,13 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--dtype", default=None, choices=["f32", "bf16"], help="default: the config's")
+    ap.add_argument("--views", type=int, default=0, help="override the config's view count N")
+    ap.add_argument("--layout", default="auto", choices=["auto", "nhwc", "cblock"],
+                    help="warp feature layout (auto: the library's choice, damvs_warp_feat_blocked)")
     args = ap.parse_args()
     H, W, N, nd, dtype, _ = bench.CONFIGS[args.config]
+    if args.views:
+        N = args.views
     if args.dtype:
         dtype = torch.float32 if args.dtype == "f32" else torch.bfloat16
     dev = torch.device("cuda")
@@ -52,7 +57,7 @@ def main():
     eng = net.DepthNet.engine(s, net.cost_regularization[s], dev)
     P = proj["stage%d" % (s + 1)]
     rt = proj_prepare(P)
-    blocked = warp_blocked(C, feats[0].element_size())
+    blocked = warp_blocked(C, feats[0].element_size(), N) if args.layout == "auto" else args.layout == "cblock"
     fb = block_channels(feats) if blocked else feats
     layout = _capi.DAMVS_LAYOUT_CBLOCK if blocked else _capi.DAMVS_LAYOUT_NHWC
     vol = eng.warp_aggregate(fb, None, hyps, rt=rt, layout=layout)
@@ -77,7 +82,8 @@ def main():
             run()
         e1.record()
         torch.cuda.synchronize()
-    print("%s stage%d %s %s B=%d: %.3f ms per call" % (args.kernel, args.stage, args.config, str(dtype)[6:], B,
+    print("%s stage%d %s %s N=%d %s B=%d: %.3f ms per call" % (args.kernel, args.stage, args.config, str(dtype)[6:], N,
+                                                         "cblock" if blocked else "nhwc", B,
                                                    e0.elapsed_time(e1) / args.iters))
 
 

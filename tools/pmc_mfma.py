@@ -74,6 +74,10 @@ def main():
             key = (row.get("Dispatch_Id") or row.get("Correlation_Id"), fam)
             per_dispatch[key][row["Counter_Name"]] = float(row["Counter_Value"])
             per_dispatch[key]["_ns"] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+    if not per_dispatch:  # say what the pass produced instead of writing an empty summary
+        files = glob.glob(os.path.join(d, "**", "*"), recursive=True)
+        raise SystemExit("no counter rows for any kernel family; files: %s\nstdout tail:\n%s\nstderr tail:\n%s"
+                         % (files[:20], r.stdout[-1500:], r.stderr[-1500:]))
     for (_, fam), cs in per_dispatch.items():
         a = acc[fam]
         a["dispatches"] += 1
