@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r05"))
     ap.add_argument("--tmp", default=os.path.join(REPO, "gpurun_out", "pmc_mfma"))
     args = ap.parse_args()
+    args.tmp, args.out = os.path.abspath(args.tmp), os.path.abspath(args.out)  # rocprofv3 runs with cwd /tmp
     os.makedirs(args.tmp, exist_ok=True)
     counters = available(args.tmp)
     if "SQ_VALU_MFMA_BUSY_CYCLES" not in counters or "GRBM_GUI_ACTIVE" not in counters:
