@@ -223,11 +223,23 @@ class HipFeatureNet:
             if self.num_stage == 3:
                 self.out3 = L(fnet.out3, False, c0=fnet.out3.in_channels)
 
+    # the kernels' 32-bit buffer offsets keep every operand below 2 GiB; the widest FeatureNet tensors are the
+    # full-resolution 8-channel ones, so view groups are sized to keep those under this bound
+    MAX_ACT_BYTES = 3 << 29  # 1.5 GiB
+
     def __call__(self, x):
         """x: (B, 3, H, W), or (B, N, 3, H, W) views batched view-major (row v*B + b) with no copy of the
-        images: the first layer reads each view's planes in place, one launch per view."""
+        images: the first layer reads each view's planes in place, one launch per view. Views run in groups when one
+        batch of all of them would pass the 32-bit offset bound (cfgE's 11 views x B=4 at 1920 x 1056 in fp32: 2.85 GB per
+        8-channel activation); the groups' outputs are concatenated in view order."""
         if x.dim() == 5:
             Bv, N, _, H, W = x.shape
+            es = torch.tensor([], dtype=self.c0[0].dtype).element_size()
+            per_view = Bv * H * W * 8 * es
+            if N > 1 and N * per_view > self.MAX_ACT_BYTES:
+                g = max(1, self.MAX_ACT_BYTES // per_view)
+                parts = [self(x[:, v:v + g]) for v in range(0, N, g)]
+                return {k: torch.cat([p[k] for p in parts], 0) for k in parts[0]}
             B = N * Bv
             L = self.c0[0]
             t = torch.empty(L.out_shape(B, H, W), device=x.device, dtype=L.dtype)

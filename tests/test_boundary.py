@@ -87,3 +87,22 @@ def test_cpu_inputs_fail_loudly():
     from damvsnet_amd.depthnet import homo_warping
     with pytest.raises(ValueError, match="HIP device"):
         homo_warping(torch.zeros(1, 8, 8, 8), torch.eye(4)[None], torch.eye(4)[None], torch.ones(1, 2))
+
+
+def test_warp_feature_layout_by_view_count():
+    """damvs_warp_feat_blocked_n (host logic, no device work): NHWC in place wherever the channel-split warp takes the
+    pixel (32 / 64 / 128 bytes at odd N >= 3), channel-blocked for wider pixels the one-lane warp gathers (even N:
+    profiles/r05/ab_warp_layout_r05p.txt), NHWC for 16-byte pixels; the N-less entry point answers for N = 5."""
+    from damvsnet_amd import _capi
+    lib = _capi.load_library()
+    F32, BF16 = _capi.DAMVS_F32, _capi.DAMVS_BF16
+    for dt, C in ((F32, 32), (F32, 16), (BF16, 32)):  # 128 / 64 / 64-byte pixels
+        assert lib.damvs_warp_feat_blocked_n(dt, C, 5) == 0 and lib.damvs_warp_feat_blocked_n(dt, C, 11) == 0
+        assert lib.damvs_warp_feat_blocked_n(dt, C, 4) == 1 and lib.damvs_warp_feat_blocked_n(dt, C, 2) == 1
+        assert lib.damvs_warp_feat_blocked(dt, C) == 0
+    for dt, C in ((F32, 8), (BF16, 16), (BF16, 8)):  # 32 / 32 / 16-byte pixels: never blocked
+        for n in (2, 4, 5):
+            assert lib.damvs_warp_feat_blocked_n(dt, C, n) == 0
+    assert lib.damvs_warp_feat_blocked_n(F32, 24, 5) == 1  # 96-byte pixels: no split form
+    assert lib.damvs_warp_feat_blocked_n(F32, 32, 1) < 0 and lib.damvs_warp_feat_blocked_n(7, 32, 5) < 0
+

@@ -209,6 +209,33 @@ def test_warp_aggregate_channel_blocked_layout(C, dtype):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("s", [0, 1])
+def test_stage_forward_even_views_vs_oracle(s, dtype):
+    """The stage forward at an even view count (N = 4: the one-lane warp, so 64 / 128-byte pixels are channel-blocked
+    inside damvs_stage_forward since round 5) against the oracle stage (models/cas_mvsnet.py:18-134) on the same
+    inputs: fp32 at the north-star gate (1e-3 per pixel), bf16 at the stated bf16 gate of the isolated stages."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import warp_blocked
+    C = (32, 16)[s]
+    net = CascadeMVSNet(ndepths=[48, 32, 8], compute_dtype=dtype)
+    sd = model_state("depthnet_cfgA_adaptive")
+    net.load_state_dict(sd, strict=True)
+    net = net.to(DEV).eval()
+    feats, P, hyps = depthnet_inputs(B=2, N=4, H=24, W=40, D=8, stage_idx=s, C=C)
+    if dtype == torch.bfloat16:
+        feats = [f.to(torch.bfloat16).float() for f in feats]
+    assert warp_blocked(C, 2 if dtype == torch.bfloat16 else 4, 4) == (C * (2 if dtype == torch.bfloat16 else 4) > 32)
+    ref = O.depthnet_stage(s, feats, P, hyps, sd, "adaptive")
+    with torch.no_grad():
+        got = net.DepthNet(s, [cuda(f) for f in feats], cuda(P), cuda(hyps), 8, net.cost_regularization[s])
+    pr = pixel_rel(np_(got["depth"]), ref["depth"].numpy())
+    if dtype == torch.float32:
+        assert pr.max() < 1e-3, pr.max()
+    else:  # the stated bf16 gate (test_stage_isolated_bf16_stated_gate)
+        assert pr.mean() < 3e-3 and np.quantile(pr, 0.99) < 1.2e-2, (pr.mean(), np.quantile(pr, 0.99))
+
+
 @pytest.mark.parametrize("C,dtype", [(32, torch.bfloat16), (16, torch.bfloat16), (8, torch.bfloat16),
                                      (24, torch.bfloat16), (32, torch.float32), (4, torch.float32)])
 def test_block_channels_is_the_blocked_permutation(C, dtype):
