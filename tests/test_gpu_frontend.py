@@ -282,6 +282,26 @@ def test_featurenet_views_read_in_place():
         assert torch.equal(a[k], b[k]), k
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_featurenet_view_groups_bitwise(dtype, monkeypatch):
+    """Views in groups (HipFeatureNet.MAX_ACT_BYTES: the 2 GiB operand bound at cfgE's fp32 B=4) give the one-call
+    result bitwise: every layer is per-image, and the groups' outputs are concatenated in view order. The bound is
+    lowered here so that 5 views run as groups of 2, 2, 1."""
+    from damvsnet_amd.frontend_hip import HipFeatureNet
+    sd = model_state("forward_160x128_48_32_8")
+    fnet, _ = _folded(sd, dtype)
+    net = HipFeatureNet(fnet, dtype)
+    imgs, _, _, _ = forward_inputs(2, 5, 64, 96)
+    imgs = imgs.to(DEV)
+    a = net(imgs)
+    per_view = 2 * 64 * 96 * 8 * torch.tensor([], dtype=dtype).element_size()
+    monkeypatch.setattr(HipFeatureNet, "MAX_ACT_BYTES", 2 * per_view + 1)
+    b = net(imgs)
+    assert a.keys() == b.keys()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
 @pytest.mark.parametrize("dt,tol", [(torch.bfloat16, 3e-2), (torch.float32, 2e-5)])
 @pytest.mark.parametrize("B,H,W", [(2, 12, 20), (1, 40, 260), (3, 18, 134)])
 def test_fpn_top_fused_vs_torch(B, H, W, dt, tol):
