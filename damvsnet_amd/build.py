@@ -30,6 +30,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-I" + INCLUDE, "-I" + CSRC,
           "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 
+# Per-file extra flags. k_warp.hip is built without the SLP vectorizer so that its kernels carry no packed-FP32 VALU
+# ops (v_pk_fma/mul/add_f32): with those, the warp kernels' lanes 48-63 computed wrong tap coordinates while MFMA
+# kernels of another stream shared the CU (DESIGN.md §4 "Concurrent streams"; profiles/r05/pytest_streams_diag_r05w.txt).
+FILE_FLAGS = {"k_warp.hip": ["-fno-slp-vectorize"]}
+
 
 def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
@@ -53,6 +58,8 @@ def source_hash(arch: str | None = None) -> str:
     if arch is not None:
         flags = ["--offload-arch=" + arch if f.startswith("--offload-arch=") else f for f in flags]
     h.update(" ".join(flags).encode())
+    for name in sorted(FILE_FLAGS):
+        h.update(("\0%s:%s" % (name, " ".join(FILE_FLAGS[name]))).encode())
     return h.hexdigest()[:16]
 
 
@@ -70,7 +77,8 @@ def _stale(want: str) -> bool:
 
 def _compile(src, build_id):
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
-    cmd = [HIPCC] + CFLAGS + ['-DDAMVS_BUILD_ID="%s"' % build_id, "-x", "hip", "-c", src, "-o", obj]
+    cmd = [HIPCC] + CFLAGS + FILE_FLAGS.get(os.path.basename(src), []) + \
+        ['-DDAMVS_BUILD_ID="%s"' % build_id, "-x", "hip", "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (src, " ".join(cmd), r.stderr))

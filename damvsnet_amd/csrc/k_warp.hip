@@ -701,11 +701,12 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
   }();
   if constexpr (!BLK && (C * sizeof(T) == 32 || C * sizeof(T) == 64 || C * sizeof(T) == 128)) {
     if (split_lanes<T, C, BLK>(a) > 1) {
-      // fp32 storage: always the runtime view loop. The unrolled N = 5 form of the fp32 split kernel computes wrong
-      // voxels in lanes 48-63 while another stream's U-Net kernels share its CUs (round 5, tools/diag_warp_streams.py
-      // --dtype f32: 6-12 of 24 launches beside conv1 differ; the runtime loop and the one-lane kernel: 0 of 24 at
-      // stages 1 and 2; DESIGN.md section 4 "Concurrent streams"), while its bf16 form passes the same tests
-      if (a.N == 5 && !runtime_views && sizeof(T) == 2)
+      // N = 5: the unrolled view loop at both storage types. Its fp32 form computed wrong voxels in lanes 48-63 beside
+      // another stream's U-Net kernels while the warp unit was built with packed-FP32 VALU ops; built without them
+      // (build.py FILE_FLAGS) it passes every stream case and runs 2 % faster than the runtime loop (stages 1-3: 0.520 /
+      // 0.749 / 0.535 against 0.532 / 0.766 / 0.548 ms, profiles/r05/diag_streams/r05y; DESIGN.md section 4
+      // "Concurrent streams")
+      if (a.N == 5 && !runtime_views)
         hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, 4>), grid, dim3(warp_block<warp_regs<T, C, MODE, true>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
       else
         hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, -1>), grid, dim3(warp_block<warp_regs<T, C, MODE, true>()>()), 0, s, a, a.rt, npb, dchunk, ndc);

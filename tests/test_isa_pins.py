@@ -42,3 +42,22 @@ def test_kernel_instruction_streams_are_the_validated_ones():
         "instruction streams differ from the stream-test-validated build (%d changed, %d removed): run "
         "tests/test_gpu_streams.py on the GPU, commit the log, then tools/isa.py --update-pins --validated-by <log>.\n"
         "changed: %s\nremoved: %s" % (len(changed), len(gone), changed[:20], gone[:20]))
+
+
+@pytest.mark.skipif(not _llvm_ok(), reason="no llvm-objdump")
+def test_warp_kernels_carry_no_packed_fp32_ops():
+    """Round 5 located the concurrent-stream fault in the warp's packed-FP32 VALU ops: a warp build whose sampling
+    path used v_pk_fma_f32 / v_pk_mul_f32 computed wrong sample coordinates in lanes 48-63 beside MFMA kernels of
+    another stream, and the same source built without them (-fno-slp-vectorize) passed every stream case
+    (profiles/r05/diag_streams/r05w). build.py compiles k_warp.hip that way (FILE_FLAGS); this keeps it so."""
+    import re
+    import isa
+    from damvsnet_amd import build
+    assert "-fno-slp-vectorize" in build.FILE_FLAGS.get("k_warp.hip", [])
+    build.build()
+    ks = isa.disassemble()
+    warp = {k: b for k, b in ks.items() if "warp_split_kernel" in k or "warp_aggregate_kernel" in k}
+    assert len(warp) >= 40, sorted(ks)[:10]
+    pk = re.compile(r"v_pk_(fma|mul|add|mov)_f32\b")
+    bad = sorted(k for k, b in warp.items() if any(pk.match(t) for t in b))
+    assert not bad, "warp kernels with packed-FP32 VALU ops: %s" % bad[:10]

@@ -9,7 +9,8 @@ mkdir -p "$R/damvsnet_amd/ab"
 objs=""
 for f in "$R"/damvsnet_amd/csrc/*.hip "$R"/damvsnet_amd/csrc/*.cpp; do
   o=$T/$(basename "$f").o
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I"$R/include" -I"$R/damvsnet_amd/csrc" "$@" -x hip -c "$f" -o "$o" &
+  fl=""; [ "$(basename "$f")" = k_warp.hip ] && fl="-fno-slp-vectorize"   # as damvsnet_amd/build.py FILE_FLAGS
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $fl -I"$R/include" -I"$R/damvsnet_amd/csrc" "$@" -x hip -c "$f" -o "$o" &
   objs="$objs $o"
 done
 wait

@@ -10,7 +10,8 @@ objs=""
 for f in "$S"/csrc/*.hip "$S"/csrc/*.cpp; do
   o=$T/$(basename "$f").o
   extra=""; [ "$(basename "$f")" = k_warp.hip ] && extra="$*"
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I"$S/include" -I"$S/csrc" $extra -x hip -c "$f" -o "$o" &
+  fl=""; [ "$(basename "$f")" = k_warp.hip ] && fl="-fno-slp-vectorize"   # as damvsnet_amd/build.py FILE_FLAGS
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $fl -I"$S/include" -I"$S/csrc" $extra -x hip -c "$f" -o "$o" &
   objs="$objs $o"
 done
 wait

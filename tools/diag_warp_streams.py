@@ -47,12 +47,66 @@ def main():
     feats = [torch.randn(B, h, w, C, generator=g, device=DEV).to(dt) for _ in range(N)]
     eng = net.DepthNet.engine(s, net.cost_regularization[s], torch.device(DEV))
 
+    es = feats[0].element_size()
+    S = C * es // 16 if (C * es) in (32, 64, 128) else 1  # lanes per voxel of the split kernel (NHWC maps, odd N)
+    ppb = 256 // S
+    tc = ppb // 8  # 8-row pixel tiles (warp_pixel, DAMVS_WARP_TILE default)
+
+    def waves(d):
+        """Per wave instance (batch, tile, wave) whose voxels differ: planes hit, pixels per (wave, plane), lanes."""
+        badc = (d > 0)  # [B][D][h][w][C]
+        idx = badc.any(-1).nonzero()
+        if not len(idx):
+            return {}
+        b, z, y, x = idx[:, 0], idx[:, 1], idx[:, 2], idx[:, 3]
+        i = (y % 8) * tc + (x % tc)
+        t = i * S
+        wave = t // 64
+        lane0 = t % 64
+        key = ((b * 1000 + y // 8) * 1000 + x // tc) * 8 + wave
+        chunks = badc[b, z, y, x].reshape(len(idx), S, -1).any(-1).sum(-1)  # bad 16-byte chunks per bad voxel
+        per = {}
+        for k, zz, ln in zip(key.tolist(), z.tolist(), lane0.tolist()):
+            e = per.setdefault(k, {"planes": {}, "lanes": set()})
+            e["planes"][zz] = e["planes"].get(zz, 0) + 1
+            e["lanes"].add(ln)
+        nplanes = [len(e["planes"]) for e in per.values()]
+        suffix = sum(1 for e in per.values() if sorted(e["planes"]) == list(range(min(e["planes"]), D)))
+        full_q = sum(1 for e in per.values() for c in e["planes"].values() if c == 16 // S)
+        events = sum(len(e["planes"]) for e in per.values())
+        return {"waves": len(per), "planes_per_wave_hist": torch.bincount(torch.tensor(nplanes), minlength=D + 1).tolist(),
+                "suffix_shaped": suffix, "wave_plane_events": events, "events_whole_quarter": full_q,
+                "min_lane": min(min(e["lanes"]) for e in per.values()),
+                "bad_chunks_per_voxel_hist": torch.bincount(chunks.cpu(), minlength=S + 1).tolist()}
+
+    lib = _capi.load_library()
+
+    def take():
+        """Diagnostic builds (-DDAMVS_DIAG): the records the warp kernels appended since the last take, by kind."""
+        if not hasattr(lib, "damvs_diag_take_warp"):
+            return None
+        import ctypes
+        buf = (ctypes.c_uint * (8 + 8 * 64))()
+        lib.damvs_diag_take_warp(buf, len(buf))
+        kinds = {}
+        for r in range(min(buf[0], 64)):
+            k = buf[8 + 8 * r]
+            kinds[k] = kinds.get(k, 0) + 1
+        first = [{"kind": buf[8 + 8 * r], "lane": buf[10 + 8 * r] >> 8, "view": buf[10 + 8 * r] & 255,
+                  "seen": "0x%08x" % buf[11 + 8 * r], "want": "0x%08x" % buf[12 + 8 * r]} for r in range(min(buf[0], 4))]
+        return {"count": int(buf[0]), "kinds_in_first_64": kinds, "first": first}
+
     def report(tag, outs, ref):
+        rec_diag = take()
+        if rec_diag is not None:
+            print(json.dumps({"case": tag, "diag_records": rec_diag}), flush=True)
         for i, o in enumerate(outs):
             d = (o.float() - ref.float()).abs()
             bad = (d > 0).any(-1)  # [B][D][h][w]
             nb = int(bad.sum())
             rec = {"case": tag, "rep": i, "voxels": nb}
+            if nb and S > 1 and a.layout == "nhwc":
+                rec["wave_analysis"] = waves(d)
             if nb:
                 idx = bad.nonzero()
                 rec["batch"] = sorted(set(idx[:, 0].tolist()))
