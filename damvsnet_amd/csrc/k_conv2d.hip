@@ -955,8 +955,11 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
   raw* abuf = reinterpret_cast<raw*>(smem);  // 2 x AR slots
   const WideHalo<IS, WRT> hg(span);
   const int HP = hg.hp;
-  // fp32 (AG, below): A fragments from L1 / L2 per wave, no A buffer in LDS
-  constexpr bool AG = SP;
+  // AG (below): A fragments from L1 / L2 per wave, no A buffer in LDS -- fp32, and bf16 except the 32-column waves of
+  // the stride-2 64-channel block (A/B, bf16 GeoFF layers at B=4, profiles/r05/ab_wide_ag_bf16: cout-64 stride-1
+  // layers 0.207 -> 0.170 and 0.123 -> 0.103 ms, stride-2 128-channel 0.299 -> 0.282 ms, the stride-2 64-channel block
+  // 0.120 -> 0.130 ms)
+  constexpr bool AG = SP || !HALFW;
   // stride 1: the next slice's halo goes to the other of two buffers; stride 2 (2.5x the pixels) and the fp32 64-channel
   // block: one buffer, rewritten between two barriers after the slice's last tap
   constexpr int NHB = IS == 1 && !(SP && WM == 1) ? 2 : 1;  // fp32 64-channel block: its 4-row halo twice = 1 block / CU
@@ -1047,7 +1050,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
     for (int j = 0; j < NGW; ++j) acc[m][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   // the fp32 depth plane's halo (zero outside the image) for the trailing plane chunk, staged once
-  float* gbuf = reinterpret_cast<float*>(hbuf + NHB * HP * SLOTS);  // HP floats
+  // (bf16 AG: at least the epilogue's 4 x 32 x 68-float staging tiles below it)
+  const int gofs = SP || !AG ? NHB * HP * SLOTS : max(NHB * HP * SLOTS, 4 * 32 * 68 / 4);
+  float* gbuf = reinterpret_cast<float*>(hbuf + gofs);  // HP floats
   if (ph.gchunks > 0) {
     const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.geo[0], ((long long)(a.B - 1) * a.geo_bstride[0] + a.Hi * a.Wi) * 4);
     const int pg0 = b * (int)a.geo_bstride[0];
@@ -1267,6 +1272,46 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
       }
     }
     __syncthreads();  // the epilogue's staging tiles overwrite the halo region other waves may still read
+  } else if constexpr (AG && !SP) {
+    // bf16 AG: the fp32 AG loop below with one 16-byte A fragment per cout tile (tile m of the wave's cout half at
+    // m * 64 slots of the chunk) and one MFMA per product
+    const raw* wa = wsrc + wm * 256 + lane;
+    auto aload = [&](raw (&x)[4], int cc, int tt) DAMVS_INLINE {
+      const raw* q = wa + (size_t)(tt * nsl + cc) * cstride;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) x[m] = q[m * 64];
+    };
+    auto gstep = [&](const raw (&cur)[4], raw (&nxt)[4]) DAMVS_INLINE {
+      int c1 = c, t1 = t + 1;
+      if (t1 == nt) {
+        c1 = c + 1 < nsl ? c + 1 : c;
+        t1 = c + 1 < nsl ? 0 : nt - 1;
+      }
+      aload(nxt, c1, t1);
+      const int p0x = s_toff[t] + lanepix;
+      const raw* hbs = hbuf + (NHB == 2 ? (c & 1) * HP * SLOTS : 0) + p0x * SLOTS + Fm::slot(p0x, g);
+      raw bf[NGW];
+#pragma unroll
+      for (int j = 0; j < NGW; ++j) bf[j] = hbs[j * 64];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int j = 0; j < NGW; ++j) Frag2<bf16_t>::mma(cur[m], bf[j], acc[m][j]);
+      if (t == 0 && c + 1 < nsl) hload(c + 1);
+      if (t == nt - 1 && c + 1 < nsl) {
+        if (NHB == 1) __syncthreads();
+        hstore(NHB == 2 ? (c + 1) & 1 : 0);
+        __syncthreads();
+      }
+      if (++t == nt) { t = 0; ++c; }
+    };
+    raw a0[4], a1[4];
+    aload(a0, 0, 0);
+    for (int kk = 0; kk < nk; kk += 2) {
+      gstep(a0, a1);
+      if (kk + 1 < nk) gstep(a1, a0);
+    }
+    __syncthreads();
   } else if constexpr (AG) {
     const raw* wa = wsrc + wm * 512 + lane;  // the wave's cout half: tile m's hi at m * 128, lo at m * 128 + 64
     auto aload = [&](F16Pair (&x)[4], int cc, int tt) DAMVS_INLINE {
@@ -1463,9 +1508,10 @@ hipError_t launch_wide_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span)
   constexpr int WRT = WM == 1 && IS == 2 ? 2 : 4 / WM, AR = WM * 256 * WideForm<T>::PL, SLOTS = WideForm<T>::SLOTS;
   const WideHalo<IS, WRT> hg(span);
   constexpr int NHB = IS == 1 && !(SP && WM == 1) ? 2 : 1, WPER = RS ? 5 : IS == 1 ? 7 : 11;
-  constexpr bool AG = SP;  // fp32: A fragments from L1 / L2, no A buffers in LDS
+  constexpr bool AG = SP || !(WM == 1 && IS == 2);  // A fragments from L1 / L2, no A buffers in LDS (the kernel's AG)
   if (hg.hp * 4 > WPER * 256) return hipErrorNotSupported;
-  const size_t below_plane = (AG ? 0 : 2 * (size_t)AR * 16) + NHB * (size_t)hg.hp * SLOTS * 16;
+  size_t below_plane = (AG ? 0 : 2 * (size_t)AR * 16) + NHB * (size_t)hg.hp * SLOTS * 16;
+  if (!SP && AG && below_plane < 4 * 32 * 68 * 4) below_plane = 4 * 32 * 68 * 4;  // as gofs in the kernel
   if (below_plane < 4 * 32 * 68 * 4) return hipErrorNotSupported;  // the epilogue's staging tiles stay below the plane halo
   const int tx = (a.Wq + WC - 1) / WC, ty = (a.Hq + WRT - 1) / WRT;
   const int nsl = (a.c0 + a.c1) / 32;
