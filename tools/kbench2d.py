@@ -43,6 +43,9 @@ CASES = {
     "W conv0.0 planes g3->8 k3 x20": (False, 3, 1, 1, 0, 0, 0, 3, 8, True, 20, 1184, 1600, False, 0),
     "X rgb init g4->8 k5 B=4": (False, 5, 1, 2, 0, 0, 0, 4, 8, True, 4, 1184, 1600, False, 0),
     "Y depth init g2->8 k5 B=4": (False, 5, 1, 2, 0, 0, 0, 2, 8, True, 4, 1184, 1600, False, 0),
+    "G4 deconv 128->32 k5s2 B=4": (True, 5, 2, 2, 1, 128, 0, 0, 32, True, 4, 296, 400, False, 1),
+    "M4 dec5 64->32 k5s2 B=4": (True, 5, 2, 2, 1, 64, 0, 0, 32, True, 4, 296, 400, False, 1),
+    "Z4 dec 16->8 k5s2 full B=4": (True, 5, 2, 2, 1, 16, 0, 0, 8, True, 4, 592, 800, False, 1),
 }
 
 
