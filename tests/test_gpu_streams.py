@@ -39,12 +39,15 @@ def _perturb(P):
 # (dtype, stage, layout): the product's own warp kernel for each stage and dtype (layout None: the library's choice,
 # damvs_warp_feat_blocked, as damvs_stage_forward makes it) -- bf16 stage 2 (2 lanes per voxel), stage 1 (4 lanes); fp32
 # stage 2 (4 lanes), stage 1 (8 lanes: 128-byte pixels); plus the one-lane kernel on channel-blocked maps (bf16 stage 2)
+# and stage 3 (full resolution, 8 channels: the one-lane kernel at bf16, 2 lanes at fp32 on the unrolled view loop the
+# packed-FP32 fix brought back)
 WARP_CASES = [(torch.bfloat16, 1, None), (torch.bfloat16, 1, "cblock"), (torch.bfloat16, 0, None),
-              (torch.float32, 1, None), (torch.float32, 0, None)]
+              (torch.float32, 1, None), (torch.float32, 0, None), (torch.bfloat16, 2, None), (torch.float32, 2, None)]
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("dtype,s,layout", WARP_CASES, ids=["bf16-s2", "bf16-s2-cblock", "bf16-s1", "f32-s2", "f32-s1"])
+@pytest.mark.parametrize("dtype,s,layout", WARP_CASES,
+                         ids=["bf16-s2", "bf16-s2-cblock", "bf16-s1", "f32-s2", "f32-s1", "bf16-s3", "f32-s3"])
 def test_warp_beside_unet_layers_on_another_stream(dtype, s, layout):
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import hypotheses, block_channels, proj_prepare, warp_blocked
@@ -53,16 +56,16 @@ def test_warp_beside_unet_layers_on_another_stream(dtype, s, layout):
     net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
     net = net.to(DEV).eval()
     B, N, H, W = 2, 5, 1184, 1600
-    C, D, scale = (32, 48, 4) if s == 0 else (16, 32, 2)
+    C, D, scale = {0: (32, 48, 4), 1: (16, 32, 2), 2: (8, 8, 1)}[s]
     h, w = H // scale, W // scale
     proj, _, dv = synth.cameras(B, N, H, W)
     P = _perturb(torch.from_numpy(proj["stage%d" % (s + 1)])).to(DEV)
     g = torch.Generator(device=DEV).manual_seed(0)
     if s == 0:
         hyps = hypotheses(torch.from_numpy(dv).to(DEV), D, H, W, scale)
-    else:  # refined per-pixel hypotheses, as the pipeline's stage 2 has them
-        pd = 600 + 100 * torch.rand(B, H // 4, W // 4, device=DEV, generator=g)
-        pv = 5 + 20 * torch.rand(B, H // 4, W // 4, device=DEV, generator=g)
+    else:  # refined per-pixel hypotheses from the previous stage's maps, as the pipeline has them
+        pd = 600 + 100 * torch.rand(B, H // (2 * scale), W // (2 * scale), device=DEV, generator=g)
+        pv = 5 + 20 * torch.rand(B, H // (2 * scale), W // (2 * scale), device=DEV, generator=g)
         hyps = hypotheses(torch.from_numpy(dv).to(DEV), D, H, W, scale, pd, pv)
     feats = [torch.randn(B, h, w, C, generator=g, device=DEV).to(dtype) for _ in range(N)]
     eng = net.DepthNet.engine(s, net.cost_regularization[s], torch.device(DEV))
