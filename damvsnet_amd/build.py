@@ -32,7 +32,7 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-I" + INCLUDE
 
 # Per-file extra flags. k_warp.hip is built without the SLP vectorizer so that its kernels carry no packed-FP32 VALU
 # ops (v_pk_fma/mul/add_f32): with those, the warp kernels' lanes 48-63 computed wrong tap coordinates while MFMA
-# kernels of another stream shared the CU (DESIGN.md §4 "Concurrent streams"; profiles/r05/pytest_streams_diag_r05w.txt).
+# kernels of another stream shared the CU (DESIGN.md §4 "Concurrent streams"; profiles/r05/diag_streams/r05w).
 FILE_FLAGS = {"k_warp.hip": ["-fno-slp-vectorize"]}
 
 
