@@ -708,6 +708,11 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
       // "Concurrent streams")
       if (a.N == 5 && !runtime_views)
         hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, 4>), grid, dim3(warp_block<warp_regs<T, C, MODE, true>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
+      // N = 7 (cfgD) unrolled too, except the fp32 8-channel maps: cfgD B=4 stages 1 / 2 bf16 2.392 / 2.462 -> 2.293 /
+      // 2.393 ms, fp32 3.525 / 4.240 -> 3.438 / 4.041 ms; fp32 stage 3 3.174 -> 3.233 ms stays on the runtime loop
+      // (profiles/r05/ab_warp_n7)
+      else if (a.N == 7 && !runtime_views && !(sizeof(T) == 4 && C == 8))
+        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, (sizeof(T) == 4 && C == 8) ? 4 : 6>), grid, dim3(warp_block<warp_regs<T, C, MODE, true>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
       else
         hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, -1>), grid, dim3(warp_block<warp_regs<T, C, MODE, true>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
       return;

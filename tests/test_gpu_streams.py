@@ -41,21 +41,24 @@ def _perturb(P):
 # stage 2 (4 lanes), stage 1 (8 lanes: 128-byte pixels); plus the one-lane kernel on channel-blocked maps (bf16 stage 2)
 # and stage 3 (full resolution, 8 channels: the one-lane kernel at bf16, 2 lanes at fp32 on the unrolled view loop the
 # packed-FP32 fix brought back)
-WARP_CASES = [(torch.bfloat16, 1, None), (torch.bfloat16, 1, "cblock"), (torch.bfloat16, 0, None),
-              (torch.float32, 1, None), (torch.float32, 0, None), (torch.bfloat16, 2, None), (torch.float32, 2, None)]
+# and the N = 7 (cfgD) unrolled split kernels at stage 2
+WARP_CASES = [(torch.bfloat16, 1, None, 5), (torch.bfloat16, 1, "cblock", 5), (torch.bfloat16, 0, None, 5),
+              (torch.float32, 1, None, 5), (torch.float32, 0, None, 5), (torch.bfloat16, 2, None, 5),
+              (torch.float32, 2, None, 5), (torch.bfloat16, 1, None, 7), (torch.float32, 1, None, 7)]
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("dtype,s,layout", WARP_CASES,
-                         ids=["bf16-s2", "bf16-s2-cblock", "bf16-s1", "f32-s2", "f32-s1", "bf16-s3", "f32-s3"])
-def test_warp_beside_unet_layers_on_another_stream(dtype, s, layout):
+@pytest.mark.parametrize("dtype,s,layout,N", WARP_CASES,
+                         ids=["bf16-s2", "bf16-s2-cblock", "bf16-s1", "f32-s2", "f32-s1", "bf16-s3", "f32-s3",
+                              "bf16-s2-n7", "f32-s2-n7"])
+def test_warp_beside_unet_layers_on_another_stream(dtype, s, layout, N):
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import hypotheses, block_channels, proj_prepare, warp_blocked
     from damvsnet_amd import _capi, synth
     net = CascadeMVSNet(ndepths=[48, 32, 8], compute_dtype=dtype)
     net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
     net = net.to(DEV).eval()
-    B, N, H, W = 2, 5, 1184, 1600
+    B, H, W = 2, 1184, 1600
     C, D, scale = {0: (32, 48, 4), 1: (16, 32, 2), 2: (8, 8, 1)}[s]
     h, w = H // scale, W // scale
     proj, _, dv = synth.cameras(B, N, H, W)
@@ -69,7 +72,7 @@ def test_warp_beside_unet_layers_on_another_stream(dtype, s, layout):
         hyps = hypotheses(torch.from_numpy(dv).to(DEV), D, H, W, scale, pd, pv)
     feats = [torch.randn(B, h, w, C, generator=g, device=DEV).to(dtype) for _ in range(N)]
     eng = net.DepthNet.engine(s, net.cost_regularization[s], torch.device(DEV))
-    blocked = warp_blocked(C, feats[0].element_size()) if layout is None else layout == "cblock"
+    blocked = warp_blocked(C, feats[0].element_size(), N) if layout is None else layout == "cblock"
     with torch.no_grad():
         rt = proj_prepare(P)
         fb = block_channels(feats) if blocked else feats
