@@ -186,7 +186,9 @@ class CascadeMVSNet(nn.Module):
         ``streams`` > 1 runs the batch as that many sub-batches on concurrent streams (_forward_streams; not with
         a stage hook or a custom stage runner). ``check_range``: after the last stage, read every stage's range
         status (damvs_stage_status, one host sync per forward) and raise damvsnet_amd._capi.DamvsRangeError if any
-        depth / confidence / variance is non-finite -- the fp32 path's split-f16 products hold |x| < 65520 only."""
+        depth / confidence / variance is non-finite. With a custom ``depthnet`` runner the range status is that
+        runner's business: sharded.DepthShardedDepthNet runs the stage as split layer calls, which do not write a
+        status word, so no DamvsRangeError is raised on that path."""
         if streams > 1 and imgs.shape[0] > 1 and stage_hook is None and depthnet is None and imgs.is_cuda \
                 and not self.refine:
             return self._forward_streams(imgs, proj_matrices, depth_values, intrinsics_matrices,
@@ -230,7 +232,7 @@ class CascadeMVSNet(nn.Module):
             elif self.frontend_impl == "hip":
                 out = self.DepthNet.forward_nhwc(s, fs, proj_matrices[name], hyps, cr)
             else:
-                out = self.DepthNet(s, fs, proj_matrices[name], hyps, self.ndepths[s], cr)
+                out = self.DepthNet(s, fs, proj_matrices[name], hyps, self.ndepths[s], cr, check_range=False)
             depth, conf, exp_var = out["depth"], out["photometric_confidence"], out["variance"]
             outputs[name] = out
             outputs.update(out)

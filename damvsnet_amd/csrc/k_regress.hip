@@ -579,7 +579,8 @@ size_t prob_regress_smem_bytes(int store, int Cb, int D) {
 
 // The range check at the end of damvs_stage_forward: depth, confidence and variance maps read once (a grid-stride loop
 // over ~2 blocks per CU, coalesced 4-byte loads: any alignment); any non-finite value sets status[0] = 1 by a vector
-// store (the status word was cleared by the stage's first kernel). 12 bytes per pixel: ~15 us at stage 3 of cfgC.
+// store. The status word is sticky: nothing in a forward clears it; only damvs_stage_status reads and clears it, and the
+// caller zeroes it when it allocates the workspace (include/damvs.h). 12 bytes per pixel: ~15 us at stage 3 of cfgC.
 __global__ __launch_bounds__(256) void finite_check_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                            const float* __restrict__ c, long long n, int* __restrict__ status) {
   bool bad = false;

@@ -20,63 +20,11 @@
 
 #include "damvs_device.h"
 
-
-// Diagnostic variants (DIAGNOSTIC builds only, tools/diag_streams.py; the product is always 0 / 0):
-// DAMVS_DIAG_WARP_LDS_CAMS = 1 stages the cameras in LDS as round 2 first did and, with -DDAMVS_DIAG, records every
-// camera word whose LDS copy differs from the global cameras right after the barrier and again after the depth walk;
-// DAMVS_DIAG_WARP_NT = 1 writes the volume with nontemporal stores; DAMVS_DIAG_WARP_NT_RELEASE = 1 adds an agent-scope
-// release (buffer_wbl2 sc1: the XCD L2's dirty lines written back) at the end of every wave of the warp kernels.
-#ifndef DAMVS_DIAG_WARP_NT_RELEASE
-#define DAMVS_DIAG_WARP_NT_RELEASE 0
-#endif
-#ifndef DAMVS_DIAG_WARP_LDS_CAMS
-#define DAMVS_DIAG_WARP_LDS_CAMS 0
-#endif
-#ifndef DAMVS_DIAG_WARP_NT
-#define DAMVS_DIAG_WARP_NT 0
-#endif
-// DAMVS_DIAG_WARP_FULLWAIT = 1: s_waitcnt vmcnt(0) before every view reduction of the pipelined loop (every load in
-// flight has landed before any sample register is read)
-#ifndef DAMVS_DIAG_WARP_FULLWAIT
-#define DAMVS_DIAG_WARP_FULLWAIT 0
-#endif
-
 namespace damvs {
 
 namespace {
 
-#if DAMVS_DIAG_WARP_LDS_CAMS && defined(DAMVS_DIAG)
-// every thread compares all n camera words of the LDS copy with global memory; one record per mismatching thread
-__device__ __forceinline__ void diag_check_cams(const float* s_cam, const float* gcam, int n, unsigned kind) {
-  unsigned bad = 0, first = 0, seen0 = 0, want0 = 0;
-  for (int i = 0; i < n; ++i) {
-    const unsigned seen = __float_as_uint(reinterpret_cast<const volatile float*>(s_cam)[i]);
-    const unsigned want = __float_as_uint(gcam[i]);
-    if (seen != want && !bad++) { first = i; seen0 = seen; want0 = want; }
-  }
-  if (bad) diag_record(kind, (threadIdx.x << 8) | first, seen0, want0);
-}
-#endif
-
-template <typename T, int C>
-__device__ __forceinline__ void store_vol(T* p, const float* v) {
-#if DAMVS_DIAG_WARP_NT
-#pragma unroll
-  for (int i = 0; i < C; i += Stor<T>::E) {
-    uint32_t w[4];
-    if constexpr (sizeof(T) == 2) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) w[k] = (uint32_t)f2bf(v[i + 2 * k]) | ((uint32_t)f2bf(v[i + 2 * k + 1]) << 16);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) w[k] = __float_as_uint(v[i + k]);
-    }
-    __builtin_nontemporal_store((v4u32_t){w[0], w[1], w[2], w[3]}, reinterpret_cast<v4u32_t*>(p + i));
-  }
-#else
-  store_vec<T, C>(p, v);
-#endif
-}
+constexpr int kWarpBlock = 256;  // threads per warp block
 
 // One 16-byte storage record -> E floats.
 template <typename T> struct Rec16;
@@ -96,32 +44,6 @@ template <> struct Rec16<bf16_t> {
   }
 };
 
-// CU-exclusive warp blocks (build option -DDAMVS_WARP_EXCLUSIVE, off in the product): every warp block holds the
-// whole register file of its CU -- R registers per wave reserved (an asm clobber of the last one makes the allocation
-// R), 512 / R waves per SIMD, i.e. 131072 / R threads per block: R = 128 (1024-thread blocks, 4 waves per SIMD) for the
-// product kernels, 256 / 512 for the one-lane kernels whose 16 / 32-channel vectors need more -- so no other kernel's
-// wave can be resident beside a warp block. Measured in round 5 against the concurrent-stream fault (DESIGN.md section
-// 4, "Concurrent streams"): it turned one failing instruction stream clean but not another, and costs 3-13 % of warp
-// time (profiles/r05/ab_warp_exclusive_r05m.txt), so the product keeps 256-thread blocks and the pinned kernels.
-template <typename T, int C, int MODE, bool SPLIT>
-constexpr int warp_regs() {
-  if (SPLIT) return MODE == AGG_VARIANCE && sizeof(T) == 2 ? 256 : 128;
-  const int rec = C * (int)sizeof(T);  // bytes per pixel, kept whole in registers by one lane
-  return rec <= 16 ? 128 : rec <= 32 ? 256 : 512;
-}
-#ifndef DAMVS_WARP_EXCLUSIVE
-template <int R> constexpr int warp_block() { return 256; }
-#define DAMVS_WARP_RESERVE(R)
-#else
-template <int R> constexpr int warp_block() { return 131072 / R; }  // (512 / R waves per SIMD) x 4 SIMDs x 64 lanes
-#define DAMVS_WARP_RESERVE(R)                                  \
-  do {                                                          \
-    if constexpr ((R) == 128) asm volatile("" ::: "v127");     \
-    else if constexpr ((R) == 256) asm volatile("" ::: "v255"); \
-    else asm volatile("" ::: "v255", "a255");                   \
-  } while (0)
-#endif
-
 // Bilinear footprint of one sample at (ix, iy): byte offsets of the nw, ne, sw, se pixel records inside one
 // batch element's map (rec bytes per record) and their weights. A corner outside the map gets the offset
 // kOOB, so its buffer load returns 0: grid_sample's zero padding without a weight select. Samples far
@@ -131,14 +53,8 @@ struct Taps {
   float wt[4];
 };
 __device__ __forceinline__ Taps bilinear_taps(int h, int w, uint32_t rec, float ix, float iy) {
-#ifdef DAMVS_WARP_CLAMP
-  // (A/B build) each coordinate clamped into [-4, size + 4] by max / min (NaN -> -4): a sample outside the map keeps
-  // all four corners outside, so it still reads 0; no lane-dependent control flow or compare chain
-  const float cx = fminf(fmaxf(ix, -4.f), (float)w + 4.f), cy = fminf(fmaxf(iy, -4.f), (float)h + 4.f);
-#else
   const bool inside = ix > -2.f && ix < (float)w + 1.f && iy > -2.f && iy < (float)h + 1.f;  // false for NaN
   const float cx = inside ? ix : -4.f, cy = inside ? iy : -4.f;
-#endif
   const float x0f = floorf(cx), y0f = floorf(cy);
   const int x0 = (int)x0f, y0 = (int)y0f;
   const float wx1 = cx - x0f, wx0 = (x0f + 1.f) - cx;
@@ -191,10 +107,9 @@ __device__ __forceinline__ int warp_pixel(const WarpArgs& a, int pb, int i, int 
 // current view is reduced, and the loads are unconditional (the last plane re-reads its own last
 // view) so the vmcnt waits count exactly.
 template <typename T, int C, int MODE, bool BLK, int NVC>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, (warp_block<warp_regs<T, C, MODE, false>()>())))) DAMVS_WAVES((warp_block<warp_regs<T, C, MODE, false>()>() == 256 && sizeof(T) == 2 && C == 32 && NVC == 0 && MODE == AGG_ADAPTIVE ? 3 : 1)) void warp_aggregate_kernel(const WarpArgs a, const float* __restrict__ cams,
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kWarpBlock))) DAMVS_WAVES((sizeof(T) == 2 && C == 32 && NVC == 0 && MODE == AGG_ADAPTIVE ? 3 : 1)) void warp_aggregate_kernel(const WarpArgs a, const float* __restrict__ cams,
                                                              int npix_blocks, int dchunk, int ndchunks) {
-  constexpr int BLOCK = warp_block<warp_regs<T, C, MODE, false>()>();
-  DAMVS_WARP_RESERVE((warp_regs<T, C, MODE, false>()));
+  constexpr int BLOCK = kWarpBlock;
   constexpr int E = Stor<T>::E, NQ = C / E;
   static_assert(NVC % 2 == 0 || NVC < 0, "the view pipeline alternates two register sets");
   const int hw = a.h * a.w;  // feature-map plane (computed rows: y0 .. y0 + rows - 1)
@@ -208,31 +123,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, (warp_block<warp_regs<T
   // kernel argument, i.e. scalar loads into SGPRs. (Staged in LDS and read back by the compiler's wide broadcast
   // ds_read_b128 / ds_read2_b64, lanes 48-63 of some waves got wrong cameras beside U-Net kernels on another
   // stream, while ds_read_b32 reads of the same copy were always right: DESIGN.md section 4, "Concurrent streams".)
-#if DAMVS_DIAG_WARP_LDS_CAMS
-  __shared__ __attribute__((aligned(16))) float s_cam[(kMaxViews - 1) * 12];
-  const float* gcam = cams + (size_t)b * (a.N - 1) * 12;
-  if ((int)threadIdx.x < (a.N - 1) * 12) s_cam[threadIdx.x] = gcam[threadIdx.x];
-  __syncthreads();
-#ifdef DAMVS_DIAG
-  diag_check_cams(s_cam, gcam, (a.N - 1) * 12, 1);
-#endif
-#if DAMVS_DIAG_WARP_LDS_CAMS == 2
-  // the cameras read back one word at a time (ds_read_b32: an opaque per-read index keeps the load-store optimiser
-  // from merging them into ds_read_b64 / b128) into a private copy
-  float cam_w[(kMaxViews - 1) * 12];
-#pragma unroll
-  for (int i = 0; i < 4 * 12; ++i) {
-    int j = i;
-    asm volatile("" : "+v"(j));
-    cam_w[i] = s_cam[j];
-  }
-  const float* cam = cam_w;
-#else
-  const float* cam = s_cam;
-#endif
-#else
   const float* __restrict__ cam = cams + (size_t)b * (a.N - 1) * 12;
-#endif
   const int p = warp_pixel(a, pb, threadIdx.x, BLOCK);
   if (p < 0) return;
   const int yl = p / a.w, x = p - yl * a.w;
@@ -308,7 +199,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, (warp_block<warp_regs<T
 #pragma unroll
       for (int c = 0; c < C; ++c) o[c] = acc[c];
     }
-    store_vol<T, C>(reinterpret_cast<T*>(a.out) + vox_of(d) * C, o);
+    store_vec<T, C>(reinterpret_cast<T*>(a.out) + vox_of(d) * C, o);
   };
   auto init = [&](float* acc, float* sq) {
 #pragma unroll
@@ -339,21 +230,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, (warp_block<warp_regs<T
         tz[v] = m[11];
         rs[v] = make_rsrc(a.feats[v + 1], fbytes);
       }
-#if DAMVS_DIAG_WARP_LDS_CAMS && defined(DAMVS_DIAG)
-      // the hoisted rays / translations against the same expressions on the global cameras (kind 4: record word =
-      // lane << 8 | view * 8 + component)
-#pragma unroll
-      for (int v = 0; v < NVC; ++v) {
-        const float* g = gcam + v * 12;
-        const float e[6] = {g[0] * fx + g[1] * fy + g[2], g[3] * fx + g[4] * fy + g[5], g[6] * fx + g[7] * fy + g[8],
-                            g[9], g[10], g[11]};
-        const float h[6] = {rx[v], ry[v], rz[v], tx[v], ty[v], tz[v]};
-#pragma unroll
-        for (int k = 0; k < 6; ++k)
-          if (__float_as_uint(e[k]) != __float_as_uint(h[k]))
-            diag_record(4, ((threadIdx.x & 63) << 8) | (v * 8 + k), __float_as_uint(h[k]), __float_as_uint(e[k]));
-      }
-#endif
     }
     auto taps = [&](int v, float hyp) {
       float qx, qy, qz;
@@ -396,9 +272,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, (warp_block<warp_regs<T
       auto step = [&](int v, const uint4* cur, const float* wcur, uint4* nxt, float* wnxt) {
         if (v + 1 < nv) issue(v + 1, taps(v + 1, hyp), nxt, wnxt);
         else issue(0, taps(0, hyp_n), nxt, wnxt);  // next plane's first view (the last plane: a re-read)
-#if DAMVS_DIAG_WARP_FULLWAIT
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-#endif
         reduce(cur, wcur, acc, sq);
       };
       if constexpr (NVC > 0) {
@@ -444,12 +317,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, (warp_block<warp_regs<T
       finish(d, acc, sq);
     }
   }
-#if DAMVS_DIAG_WARP_LDS_CAMS && defined(DAMVS_DIAG)
-  diag_check_cams(s_cam, gcam, (a.N - 1) * 12, 2);
-#endif
-#if DAMVS_DIAG_WARP_NT_RELEASE
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
 }
 
 // Channel-split form (NHWC maps whose pixel is S = C * sizeof(T) / 16 chunks of 16 bytes, S = 2, 4 or 8 -- 8: the
@@ -472,12 +339,11 @@ __device__ __forceinline__ float swz_xor4(float v) {
 }
 
 template <typename T, int C, int MODE, int NVC>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, (warp_block<warp_regs<T, C, MODE, true>()>())))) void warp_split_kernel(const WarpArgs a, const float* __restrict__ cams,
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kWarpBlock))) void warp_split_kernel(const WarpArgs a, const float* __restrict__ cams,
                                                                 int npix_blocks, int dchunk, int ndchunks) {
-  DAMVS_WARP_RESERVE((warp_regs<T, C, MODE, true>()));
   constexpr int E = Stor<T>::E;  // channels per 16-byte chunk
   constexpr int S = C / E;       // lanes per voxel
-  constexpr int PPB = warp_block<warp_regs<T, C, MODE, true>()>() / S;  // pixels per block
+  constexpr int PPB = kWarpBlock / S;  // pixels per block
   static_assert(S == 2 || S == 4 || S == 8, "channel-split form: 2, 4 or 8 chunks per pixel");
   static_assert(NVC % 2 == 0 || NVC < 0, "the view pipeline alternates two register sets");
   const int hw = a.h * a.w;
@@ -565,7 +431,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, (warp_block<warp_regs<T
         o[e] = acc[e];
       }
     }
-    store_vol<T, E>(reinterpret_cast<T*>(a.out) + vox_of(d) * C + q * E, o);
+    store_vec<T, E>(reinterpret_cast<T*>(a.out) + vox_of(d) * C + q * E, o);
   };
   auto init = [&](float* acc, float* sq) {
 #pragma unroll
@@ -610,24 +476,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, (warp_block<warp_regs<T
     __amdgpu_buffer_rsrc_t r;
     if constexpr (NVC > 0) r = rs[v];
     else r = make_rsrc(a.feats[v + 1], fbytes);
-#if defined(DAMVS_DIAG_WARP_SAMEX) || defined(DAMVS_DIAG_WARP_2TAP)
-    // diagnostic builds only (tools/gpu_ab_warp_ta.sh; wrong results): SAMEX reads the west corners twice (the same
-    // loads, half the distinct lines), 2TAP issues only the west corners (half the loads)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-#ifdef DAMVS_DIAG_WARP_2TAP
-      if (k & 1) {
-        rv[k] = rv[k - 1];
-        continue;
-      }
-#endif
-      rv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, t.off[k & 2] + qoff, sb, 0));
-    }
-#else
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       rv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, t.off[k] + qoff, sb, 0));
-#endif
 #pragma unroll
     for (int k = 0; k < 4; ++k) wt[k] = t.wt[k];
   };
@@ -662,9 +513,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, (warp_block<warp_regs<T
     hyp_n = hyp_nn;
     finish(d, acc, sq);
   }
-#if DAMVS_DIAG_WARP_NT_RELEASE
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
 }
 
 // Lanes per voxel the launcher uses for C-channel maps: the channel-split kernel for NHWC maps of 2, 4 or 8 16-byte
@@ -707,14 +555,14 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
       // 0.749 / 0.535 against 0.532 / 0.766 / 0.548 ms, profiles/r05/diag_streams/r05y; DESIGN.md section 4
       // "Concurrent streams")
       if (a.N == 5 && !runtime_views)
-        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, 4>), grid, dim3(warp_block<warp_regs<T, C, MODE, true>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
+        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, 4>), grid, dim3(kWarpBlock), 0, s, a, a.rt, npb, dchunk, ndc);
       // N = 7 (cfgD) unrolled too, except the fp32 8-channel maps: cfgD B=4 stages 1 / 2 bf16 2.392 / 2.462 -> 2.293 /
       // 2.393 ms, fp32 3.525 / 4.240 -> 3.438 / 4.041 ms; fp32 stage 3 3.174 -> 3.233 ms stays on the runtime loop
       // (profiles/r05/ab_warp_n7)
       else if (a.N == 7 && !runtime_views && !(sizeof(T) == 4 && C == 8))
-        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, (sizeof(T) == 4 && C == 8) ? 4 : 6>), grid, dim3(warp_block<warp_regs<T, C, MODE, true>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
+        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, (sizeof(T) == 4 && C == 8) ? 4 : 6>), grid, dim3(kWarpBlock), 0, s, a, a.rt, npb, dchunk, ndc);
       else
-        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, -1>), grid, dim3(warp_block<warp_regs<T, C, MODE, true>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
+        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, -1>), grid, dim3(kWarpBlock), 0, s, a, a.rt, npb, dchunk, ndc);
       return;
     }
   }
@@ -724,14 +572,14 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
   const bool pipe = !no_pipe && a.N >= 3 && (a.N - 1) % 2 == 0;
   if constexpr (C == 16) {
     if (pipe && a.N == 5 && !runtime_views) {
-      hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 4>), grid, dim3(warp_block<warp_regs<T, C, MODE, false>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
+      hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 4>), grid, dim3(kWarpBlock), 0, s, a, a.rt, npb, dchunk, ndc);
       return;
     }
   }
   if (pipe)
-    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, -1>), grid, dim3(warp_block<warp_regs<T, C, MODE, false>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
+    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, -1>), grid, dim3(kWarpBlock), 0, s, a, a.rt, npb, dchunk, ndc);
   else
-    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 0>), grid, dim3(warp_block<warp_regs<T, C, MODE, false>()>()), 0, s, a, a.rt, npb, dchunk, ndc);
+    hipLaunchKernelGGL((warp_aggregate_kernel<T, C, MODE, BLK, 0>), grid, dim3(kWarpBlock), 0, s, a, a.rt, npb, dchunk, ndc);
 }
 
 template <typename T, int MODE, bool BLK>
@@ -744,7 +592,7 @@ hipError_t launch_c(hipStream_t s, const WarpArgs& a0) {
   auto pick = [&](auto cc) {
     constexpr int CC = decltype(cc)::value;
     lanes = split_lanes<T, CC, BLK>(a);
-    block = lanes > 1 ? warp_block<warp_regs<T, CC, MODE, true>()>() : warp_block<warp_regs<T, CC, MODE, false>()>();
+    block = kWarpBlock;
   };
   switch (a.C) {
     case 8: pick(IntC<8>()); break;
@@ -866,7 +714,3 @@ hipError_t launch_block_channels(hipStream_t s, int store, const FeatPtrs& src, 
 }
 
 }  // namespace damvs
-
-#ifdef DAMVS_DIAG
-DAMVS_DIAG_EXPORT(warp)
-#endif

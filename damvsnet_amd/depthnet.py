@@ -77,7 +77,10 @@ class DepthNet(nn.Module):
             raise err
 
     def forward(self, stage_idx, features, proj_matrices, depth_values, num_depth, cost_regularization,
-                prob_volume_init=None, return_prob_volume=True):
+                prob_volume_init=None, return_prob_volume=True, check_range=True):
+        """The reference's per-stage call (models/cas_mvsnet.py:18). ``check_range`` (default on, one host sync):
+        raise DamvsRangeError right away on non-finite outputs; CascadeMVSNet passes False and checks once per
+        forward."""
         assert len(features) == proj_matrices.shape[1], "Different number of images and projection matrices"
         assert depth_values.shape[1] == num_depth, "depth_values.shape[1]:{}  num_depth:{}".format(
             depth_values.shape[1], num_depth)
@@ -86,7 +89,7 @@ class DepthNet(nn.Module):
         _require_gpu(depth_values, proj_matrices, *features)
         feats = [to_nhwc(f, self.compute_dtype) for f in features]
         return self.forward_nhwc(stage_idx, feats, proj_matrices, depth_values, cost_regularization,
-                                 prob_volume_init, return_prob_volume, check_range=True)
+                                 prob_volume_init, return_prob_volume, check_range=check_range)
 
     def forward_nhwc(self, stage_idx, feats_nhwc, proj_matrices, depth_values, cost_regularization,
                      prob_volume_init=None, return_prob_volume=True, check_range=False):

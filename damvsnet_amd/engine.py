@@ -61,7 +61,7 @@ class StageEngine:
         self.handle = handle
         self._lib = lib
         self._ws = None
-        self._unchecked = {}  # stream pointer -> workspace of a forward whose range status was not read yet
+        self._unchecked = {}  # stream pointer -> {data_ptr: workspace} of forwards whose range status was not read yet
         self.version = _param_version(costreg) + (_param_version(aggw) if aggw is not None else ())
 
     def __del__(self):
@@ -99,7 +99,8 @@ class StageEngine:
         var = torch.empty_like(depth)
         prob = torch.empty(B, D, h, w, device=dev, dtype=torch.float32) if want_prob else None
         fptrs = (ctypes.c_void_p * N)(*[f.data_ptr() for f in feats_nhwc])
-        self._unchecked[_capi.stream_ptr(dev)] = ws
+        # a workspace replaced by a larger one (shape change between checks) stays pending until check_range()
+        self._unchecked.setdefault(_capi.stream_ptr(dev), {})[ws.data_ptr()] = ws
         if probe is None:
             check(self._lib.damvs_stage_forward(self.handle, _capi.stream_ptr(dev), B, N, D, h, w, fptrs, ptr(proj),
                                                 ptr(hyps), ptr(prob_init), ptr(ws), ws.numel(), ptr(depth), ptr(conf),
@@ -118,11 +119,12 @@ class StageEngine:
         (damvs_stage_status: sticky per workspace until read; synchronises the streams those forwards ran on)."""
         pending, self._unchecked = self._unchecked, {}
         err = None
-        for stream, ws in pending.items():  # every status is read (and cleared) before the first error is raised
-            try:
-                check(self._lib.damvs_stage_status(self.handle, stream, ptr(ws), ws.numel()))
-            except _capi.DamvsError as e:
-                err = err or e
+        for stream, wss in pending.items():  # every status is read (and cleared) before the first error is raised
+            for ws in wss.values():
+                try:
+                    check(self._lib.damvs_stage_status(self.handle, stream, ptr(ws), ws.numel()))
+                except _capi.DamvsError as e:
+                    err = err or e
         if err is not None:
             raise err
 

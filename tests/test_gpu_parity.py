@@ -509,6 +509,27 @@ def test_cascade_range_status_fp32():
         assert torch.equal(out2["depth"], out["depth"])
 
 
+def test_cascade_range_status_torch_frontend():
+    """The torch front-end branch of CascadeMVSNet.forward honours check_range: with check_range=False
+    no stage reads its status (no per-stage host sync) and the pending status is reported by the next check."""
+    from damvsnet_amd._capi import DamvsRangeError
+    from damvsnet_amd.cascade import CascadeMVSNet
+    net = CascadeMVSNet(ndepths=[48, 32, 8], frontend_impl="torch")
+    net.load_state_dict(model_state("forward_160x128_48_32_8"), strict=True)
+    net = net.to(DEV).eval()
+    imgs, proj, dv, ins = forward_inputs(1, 3, 128, 160)
+    bad = cuda(imgs).clone()
+    bad[0, 1, :, 40:60, 50:90] = float("nan")  # a source view: NaN features reach the cost volume
+    with torch.no_grad():
+        with pytest.raises(DamvsRangeError):
+            net(bad, cuda(proj), cuda(dv), cuda(ins))
+        net(bad, cuda(proj), cuda(dv), cuda(ins), check_range=False)  # deferred: nothing raised here
+        with pytest.raises(DamvsRangeError):
+            net.DepthNet.check_range()
+        out = net(cuda(imgs), cuda(proj), cuda(dv), cuda(ins))
+        assert torch.isfinite(out["depth"]).all()
+
+
 # ----------------------------------------------------------------------------- full forward (A11)
 #
 # The cascade amplifies last-bit differences: with these random (BN-calibrated) weights, a

@@ -44,13 +44,14 @@ def _perturb(P):
 # and the N = 7 (cfgD) unrolled split kernels at stage 2
 WARP_CASES = [(torch.bfloat16, 1, None, 5), (torch.bfloat16, 1, "cblock", 5), (torch.bfloat16, 0, None, 5),
               (torch.float32, 1, None, 5), (torch.float32, 0, None, 5), (torch.bfloat16, 2, None, 5),
-              (torch.float32, 2, None, 5), (torch.bfloat16, 1, None, 7), (torch.float32, 1, None, 7)]
+              (torch.float32, 2, None, 5), (torch.bfloat16, 1, None, 7), (torch.float32, 1, None, 7),
+              (torch.bfloat16, 0, None, 7), (torch.float32, 0, None, 7)]
 
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("dtype,s,layout,N", WARP_CASES,
                          ids=["bf16-s2", "bf16-s2-cblock", "bf16-s1", "f32-s2", "f32-s1", "bf16-s3", "f32-s3",
-                              "bf16-s2-n7", "f32-s2-n7"])
+                              "bf16-s2-n7", "f32-s2-n7", "bf16-s1-n7", "f32-s1-n7"])
 def test_warp_beside_unet_layers_on_another_stream(dtype, s, layout, N):
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd.engine import hypotheses, block_channels, proj_prepare, warp_blocked
