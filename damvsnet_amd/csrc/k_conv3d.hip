@@ -18,6 +18,7 @@
 // with 1..8 taps (sub-pixel decomposition): no MFMA work on the structural zeros a
 // zero-inserted transposed conv would carry.
 #include <cstdlib>
+#include <cstring>
 
 #include "damvs_device.h"
 
@@ -950,6 +951,202 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (CIN == 32 ? 1 : 
   }
 }
 
+// fp32 conv0 with the kernel depths on different waves (round 6). The input-plane walk above keeps all 36 / 18 A pairs
+// (CIN 32 / 16) of a layer in every wave: 288 / 144 registers, one / two waves per SIMD, MFMA busy 0.30 (stage 1 conv0
+// 1.76 ms against a 0.57 ms MFMA floor). Here a block of 3 RP waves walks the input planes of an (2 RP) x (16 TXG)
+// output window: wave (rp, dz) holds only kernel depth dz's NJ = KCHUNKS / 3 A pairs (96 / 48 / 24 registers) and, at
+// input plane p, runs depth dz's MFMAs for output plane o = p + 1 - dz of row pair rp. The three partial sums of an
+// output plane are chained through LDS in the walk order: depth 0's wave starts the accumulator at step o - 1 and
+// leaves it in chain01, depth 1's wave continues it at step o (MFMAs into the loaded accumulator) and leaves it in
+// chain12, depth 2's wave finishes it at step o + 1 and runs the epilogue. Per output plane and column group that is
+// the input-plane walk's MFMA chain (depth 0's chunks, then depth 1's, then depth 2's, chunks ascending, fp32
+// accumulator stored and reloaded exactly): bitwise the same results (test_conv0_dz_fp32_bitwise). The three depth
+// waves read the same B fragments (3 ds_read_b128 pairs per plane where the walk read one), which the LDS carries at
+// 2 / 3 of its rate beside the MFMAs at full rate. Ring: 2 slots as in the walk; chain buffers double-buffered by the
+// output plane's parity.
+template <int CIN, int RP, int TXG>
+__global__ __launch_bounds__(192 * RP) DAMVS_WAVES(CIN == 32 ? 3 : 4) void conv0_dz_kernel(
+    const ConvArgs a, int tiles_x, int tiles_y, int nzc, int zc, int ntiles) {
+  typedef ZForm<float> Z;
+  typedef Z::frag frag;
+  constexpr int PL = 2, ES = 4, NT = 192 * RP;
+  constexpr int E = 8, KC = 32, CH = CIN / E, S = CH * PL;
+  constexpr int LR = 2 * RP;  // output rows per block
+  constexpr int TX = 16 * TXG, PW = TX + 2, PH = LR + 2;
+  constexpr int PLANE = PH * PW * S;             // 16-byte slots per halo plane
+  constexpr int NLD = (PH * PW * CH + NT - 1) / NT;  // 8-channel chunks per thread per plane
+  constexpr int KCHUNKS = 36 * CIN / KC;
+  constexpr int NJ = KCHUNKS / 3;  // K chunks per kernel depth
+  constexpr int CHAIN = RP * TXG * 64;  // float4 per chain buffer (one per lane, row pair and column group)
+  static_assert(KC % CIN == 0 || CIN % KC == 0, "chunking");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint4* ring = reinterpret_cast<uint4*>(smem);
+  f32x4_t* chain = reinterpret_cast<f32x4_t*>(smem + 2 * PLANE * 16);  // [2 chains][2 parities][CHAIN]
+
+  const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
+  int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tx = tt % tiles_x; tt /= tiles_x;
+  const int ty = tt % tiles_y; tt /= tiles_y;
+  const int tz = tt % nzc;
+  const int b = tt / nzc;
+  const int x0 = tx * TX, y0 = ty * LR, zb = tz * zc;
+  const int zend = min(zb + zc, a.Do);
+
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * ES);
+  auto load_plane = [&](int iz, uint4 (*v)[PL]) DAMVS_INLINE {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * NT;
+      const int row = c / (PW * CH), col = c - row * (PW * CH);
+      const int iy = y0 - 1 + row, ix = x0 - 1 + col / CH;
+      const bool ok = c < PH * PW * CH && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
+                      (unsigned)ix < (unsigned)a.Wi;
+      const uint32_t off = (uint32_t)((((b * a.Di + iz) * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * (16u * PL);
+#pragma unroll
+      for (int h = 0; h < PL; ++h) v[i][h] = BufIO<bf16_t>::frag(rin, ok ? off + 16u * h : kOOB);
+    }
+  };
+  auto store_plane = [&](int iz, const uint4 (*v)[PL]) DAMVS_INLINE {
+    uint4* dst = ring + ((iz + 2) & 1) * PLANE;  // two slots: plane p + 1 goes where plane p - 1 was
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = threadIdx.x + i * NT;
+      if (c >= PH * PW * CH) continue;
+      const int vox = c / CH, q = c - vox * CH, sw = Z::template zsw<S>(vox % PW);
+      const F16Pair pr = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+      dst[vox * S + (q ^ sw)] = pr.h;
+      dst[vox * S + ((CH + q) ^ sw)] = pr.l;
+    }
+  };
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rp = wave % RP, dz = wave / RP;  // wave-uniform
+  frag wreg[NJ];
+  {
+    const uint4* __restrict__ wsrc = reinterpret_cast<const uint4*>(a.wpack32) + lane;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) wreg[j] = Z::wload(wsrc, dz * NJ + j, 0);
+  }
+  uint4 pa[NLD][PL], pb[NLD][PL];
+  load_plane(zb - 1, pa);
+  store_plane(zb - 1, pa);
+  load_plane(zb, pa);  // stored at the end of step zb - 1; from there on planes are fetched two steps ahead
+  __syncthreads();
+
+  const int n = lane & 15, g = lane >> 4;
+  const int gi = (g * E) / CIN, gc = (g * E) % CIN / E;
+  const int lbase = (2 * rp * PW + n) * S;
+  const int sw0 = Z::template zsw<S>(n), sw1 = Z::template zsw<S>(n + 1), sw2 = Z::template zsw<S>(n + 2);
+  const long long nout = (long long)a.B * a.Do * a.Ho * a.Wo * a.Cout * ES;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout);
+  const int co = (g & 1) * 4, r = g >> 1;
+  float bias[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias[i] = co < a.Cout ? a.bias[co + i] : 0.f;
+  const int oy = y0 + 2 * rp + r;
+  f32x4_t* const ch_in = chain + (dz == 2 ? 2 * CHAIN : 0);   // dz 1 reads chain01, dz 2 chain12
+  f32x4_t* const ch_out = chain + (dz == 0 ? 0 : 2 * CHAIN);  // dz 0 writes chain01, dz 1 chain12
+  const int cslot = rp * TXG * 64 + lane;
+
+  // step p: input plane p (ring slot p & 1); plane p + 1 (in `cur`) goes to the ring after the MFMAs, plane p + 2 is
+  // fetched into `nxt` before them
+  auto step = [&](int p, uint4 (*cur)[PL], uint4 (*nxt)[PL]) DAMVS_INLINE {
+    if (p + 2 <= zend) load_plane(p + 2, nxt);
+    const int o = p + 1 - dz;  // this wave's output plane at this step
+    if (o >= zb && o < zend) {
+      f32x4_t acc[TXG];
+      const int par = (o & 1) * CHAIN + cslot;
+#pragma unroll
+      for (int xg = 0; xg < TXG; ++xg)
+        acc[xg] = dz == 0 ? (f32x4_t){0.f, 0.f, 0.f, 0.f} : ch_in[par + xg * 64];
+      const uint4* src = ring + (p & 1) * PLANE + lbase;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int kt = (j * KC) / CIN, kc = ((j * KC) % CIN) / E;
+        auto toff = [](int t) { return (((t / 3) % 4) * PW + t % 3) * S; };
+        int off = toff(kt), dx = kt % 3;
+        if (KC > CIN) {
+          off = gi == 1 ? toff(kt + 1) : off;
+          off = gi == 2 ? toff(kt + 2) : off;
+          off = gi == 3 ? toff(kt + 3) : off;
+          dx = (kt + gi) % 3;
+        }
+        const int sw = dx == 0 ? sw0 : dx == 1 ? sw1 : sw2;  // +16 columns keep the swizzle
+#pragma unroll
+        for (int xg = 0; xg < TXG; ++xg) Z::mma(wreg[j], Z::bread(src + off + 16 * xg * S, kc + gc, CH, sw), acc[xg]);
+      }
+      if (dz < 2) {
+#pragma unroll
+        for (int xg = 0; xg < TXG; ++xg) ch_out[par + xg * 64] = acc[xg];
+      } else {
+#pragma unroll
+        for (int xg = 0; xg < TXG; ++xg) {
+          const int ox = x0 + 16 * xg + n;
+          const bool vok = oy < a.Ho && ox < a.Wo && co < a.Cout;
+          const uint32_t off = (uint32_t)((((b * a.Do + o) * a.Ho + oy) * a.Wo + ox) * a.Cout + co) * (uint32_t)ES;
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[i] = acc[xg][i] * a.wscale + bias[i];  // 2^-k: exact
+            if (a.relu) v[i] = relu(v[i]);
+          }
+          BufIO<float>::stq(ro, vok ? off : kOOB, v);
+        }
+      }
+    }
+    if (p + 1 <= zend) store_plane(p + 1, cur);  // slot of plane p - 1, last read before the previous barrier
+    __syncthreads();
+  };
+  for (int p = zb - 1; p <= zend; p += 2) {
+    step(p, pa, pb);
+    if (p + 1 <= zend) step(p + 1, pb, pa);
+  }
+}
+
+template <int CIN, int RP, int TXG>
+hipError_t launch_dz_t(hipStream_t s, const ConvArgs& a) {
+  constexpr int PLANE = (2 * RP + 2) * (16 * TXG + 2) * (CIN / 8) * 2;
+  const size_t smem = 2 * PLANE * 16 + 4 * (size_t)RP * TXG * 64 * 16;
+  constexpr int zc = 16;
+  const int tx = (a.Wo + 16 * TXG - 1) / (16 * TXG), ty = (a.Ho + 2 * RP - 1) / (2 * RP), nzc = (a.Do + zc - 1) / zc;
+  const long long nt = (long long)tx * ty * nzc * a.B;
+  auto k = conv0_dz_kernel<CIN, RP, TXG>;
+  if (smem > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)smem);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3((unsigned)nt), dim3(192 * RP), smem, s, a, tx, ty, nzc, zc, (int)nt);
+  return hipGetLastError();
+}
+
+// DAMVS_CONV0_DZ (read per call): "0" = off (the input-plane walk / output-plane walk as DAMVS_CONV0_REUSE says), else
+// "RP,TXG" overrides the default block shape of conv0_dz_kernel
+bool conv0_dz_shape(int CIN, int& rp, int& txg) {
+  const char* v = getenv("DAMVS_CONV0_DZ");
+  rp = 4;
+  txg = CIN == 8 ? 2 : 1;
+  if (!v) return true;
+  if (v[0] == '0') return false;
+  const char* c = strchr(v, ',');
+  rp = atoi(v);
+  txg = c ? atoi(c + 1) : txg;
+  return true;
+}
+
+template <int CIN>
+hipError_t launch_dz(hipStream_t s, const ConvArgs& a, int rp, int txg) {
+  // the shapes that build without spills (tests/test_codeobj.py): CIN 32 (4, 1); CIN 16 (4, 1), (2, 1); CIN 8 all four
+  if (rp == 4 && txg == 1) return launch_dz_t<CIN, 4, 1>(s, a);
+  if constexpr (CIN <= 16) {
+    if (rp == 2 && txg == 1) return launch_dz_t<CIN, 2, 1>(s, a);
+  }
+  if constexpr (CIN == 8) {
+    if (rp == 4 && txg == 2) return launch_dz_t<CIN, 4, 2>(s, a);
+    if (rp == 2 && txg == 2) return launch_dz_t<CIN, 2, 2>(s, a);
+  }
+  return hipErrorInvalidValue;
+}
+
 bool zslide_disabled() {  // read per call: tests flip it between launches
   const char* v = getenv("DAMVS_CONV_NO_ZSLIDE");
   return v && v[0] == '1';
@@ -1001,6 +1198,8 @@ hipError_t launch_lds_pair_t(hipStream_t s, const ConvArgs& a) {
     // fp32: the split-f16 z-streamed kernel on the 32-K row-pair packing, A fragments in registers (CIN 32: 36 pairs,
     // 288 VGPRs, with the 92 KB ring one block and one wave per SIMD)
     if (!a.resid && a.wpack32 && !zslide_disabled()) {
+      int rp, txg;
+      if (conv0_dz_shape(CIN, rp, txg)) return launch_dz<CIN>(s, a, rp, txg);
       // DAMVS_CONV0_REUSE (read per call): 1 = the input-plane walk, 0 = the output-plane walk; default: the walk at CIN
       // 16 / 32 (bitwise equal, test_conv0_reuse_fp32_bitwise)
       const char* rv = getenv("DAMVS_CONV0_REUSE");

@@ -13,6 +13,13 @@ path against the float64 depths at a fixed multiple of these numbers.
 
 Writes ``tests/golden/conditioning.npz``: ``<case>::s<k>_depth64`` (float64 depth, stage k) and
 ``<case>::s<k>_stats`` = [mean, p99, max] of the fp32-vs-fp64 per-pixel relative difference.
+
+``--cfgC`` writes ``tests/golden/conditioning_cfgC.npz`` instead: the config of record (BASELINE.json configs[2],
+1600x1184, 5 views, 48/32/8) with the weights whose BN statistics were calibrated on the reference at cfgB. To keep
+the fixture small, each float64 depth map is stored as its float32 rounding ``s<k>_hi`` plus the float16 remainder
+``s<k>_lo`` (hi + lo reproduces the float64 depth to ~1e-10 relative, far below every gate), and stage 3 on the
+even rows and columns only (``s3`` = depth[::2, ::2]; the stats are taken over the same pixels). Each case's run
+time is ~2 min of CPU (fp32 + fp64 forwards).
 """
 from __future__ import annotations
 
@@ -48,7 +55,34 @@ def run(sd, inputs, ndepths, mode, dtype):
     return [out["stage%d" % s]["depth"].double().numpy() for s in (1, 2, 3)]
 
 
+CFGC = ("cfgC_1600x1184", "forward_cfgB_640x512", 1184, 1600, 5, (48, 32, 8), "adaptive")
+
+
+def main_cfgC():
+    torch.set_num_threads(os.cpu_count() or 8)
+    case, fixture, H, W, N, nd, mode = CFGC
+    t0 = time.time()
+    sd = model_state(fixture)
+    inputs = forward_inputs(1, N, H, W)
+    d32 = run(sd, inputs, nd, mode, torch.float32)
+    d64 = run(sd, inputs, nd, mode, torch.float64)
+    res = {}
+    for s in range(3):
+        a, b = (d32[s], d64[s]) if s < 2 else (d32[s][:, ::2, ::2], d64[s][:, ::2, ::2])
+        pr = np.abs(a - b) / np.maximum(np.abs(b), 1e-12)
+        st = np.array([pr.mean(), np.quantile(pr, 0.99), pr.max()])
+        hi = b.astype(np.float32)
+        lo = (b - hi.astype(np.float64)).astype(np.float16)
+        assert np.abs(hi.astype(np.float64) + lo.astype(np.float64) - b).max() / np.abs(b).min() < 1e-9
+        res["s%d_hi" % (s + 1)], res["s%d_lo" % (s + 1)], res["s%d_stats" % (s + 1)] = hi, lo, st
+        print("%-26s stage%d fp32 vs fp64: mean %.3e p99 %.3e max %.3e" % (case, s + 1, *st))
+    print("  (%.1f s)" % (time.time() - t0))
+    np.savez_compressed(os.path.join(HERE, "conditioning_cfgC.npz"), **res)
+
+
 def main():
+    if "--cfgC" in sys.argv:
+        return main_cfgC()
     torch.set_num_threads(os.cpu_count() or 8)
     res = {}
     for case, fixture, H, W, N, nd, mode in CASES:

@@ -639,6 +639,33 @@ def test_forward_cfgB_golden_fp32():
     assert pixel_rel(np_(out["stage1"]["depth"]), g["s1_depth"]).max() < 1e-3
 
 
+def test_forward_cfgC_e2e_fp32():
+    """The config of record end to end (BASELINE.json configs[2]: 1600x1184, 5 views, 48/32/8) on the fp32 parity path:
+    per stage, the HIP depth against the float64 oracle depth on identical inputs (weights BN-calibrated on the
+    reference at cfgB) within COND_K x the oracle's own fp32-vs-fp64 mean / p99 / max per-pixel relative difference
+    (tests/golden/make_conditioning.py --cfgC: stage 1 3.7e-5 max, stage 2 6.2e-3 max, stage 3 mean 3.3e-2 -- the
+    cascade amplifies last-bit differences); stage 3 on the even rows and columns the fixture keeps. Stage 1 also holds
+    the north-star 1e-3 per pixel end to end."""
+    net = make_model("forward_cfgB_640x512", (48, 32, 8))
+    imgs, proj, dv, ins = forward_inputs(1, 5, 1184, 1600)
+    with torch.no_grad():
+        out = net(cuda(imgs), cuda(proj), cuda(dv), cuda(ins))
+    g = golden("conditioning_cfgC")
+    for s in (1, 2, 3):
+        ref = g["s%d_hi" % s].astype(np.float64) + g["s%d_lo" % s].astype(np.float64)
+        d = np_(out["stage%d" % s]["depth"])
+        if s == 3:
+            d = d[:, ::2, ::2]
+        rm, rp, rx = g["s%d_stats" % s]
+        pr = pixel_rel(d, ref)
+        m, p, x = pr.mean(), np.quantile(pr, 0.99), pr.max()
+        print("e2e cfgC stage%d vs fp64: mean %.3e (%.2fx ref) p99 %.3e (%.2fx) max %.3e (%.2fx)"
+              % (s, m, m / rm, p, p / rp, x, x / rx))
+        assert m <= COND_K * rm and p <= COND_K * rp and x <= COND_K * rx, (s, m / rm, p / rp, x / rx)
+        if s == 1:
+            assert x < 1e-3
+
+
 def test_depthnet_deterministic():
     """The HIP path has no atomics: repeated stage runs are bitwise identical."""
     from damvsnet_amd.cascade import CascadeMVSNet
@@ -743,9 +770,34 @@ def test_conv0_reuse_fp32_bitwise(s, D, H, W, monkeypatch):
     eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.float32,
                       torch.device(DEV))
     vol = eng.warp_aggregate([cuda(f.permute(0, 2, 3, 1).contiguous()) for f in feats], cuda(P), cuda(hyps))
+    monkeypatch.setenv("DAMVS_CONV0_DZ", "0")
     monkeypatch.setenv("DAMVS_CONV0_REUSE", "1")
     a = eng.costreg_logits(vol).clone()
     monkeypatch.setenv("DAMVS_CONV0_REUSE", "0")
+    b = eng.costreg_logits(vol).clone()
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("s,D,H,W,shape", [(0, 48, 40, 72, "4,1"), (0, 20, 36, 88, "4,1"), (1, 24, 40, 72, "4,1"),
+                                             (1, 32, 44, 80, "2,1"), (2, 8, 48, 96, "4,2"), (2, 8, 44, 80, "4,1"),
+                                             (2, 16, 40, 72, "2,2"), (2, 8, 40, 72, "2,1")])
+def test_conv0_dz_fp32_bitwise(s, D, H, W, shape, monkeypatch):
+    """fp32 conv0 with the kernel depths on different waves (conv0_dz_kernel, partial sums chained through LDS in the
+    walk order) against the input-plane walk: the same MFMA chain per output plane, so the logits agree bitwise; every
+    block shape the launcher offers, D not a multiple of the 16-plane chunk, ragged row and column tiles."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import StageEngine
+    C = (32, 16, 8)[s]
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    feats, P, hyps = depthnet_inputs(B=2, N=3, H=H, W=W, D=D, stage_idx=s, C=C)
+    eng = StageEngine(net.cost_regularization[s], net.DepthNet.weight_net[s], "adaptive", torch.float32,
+                      torch.device(DEV))
+    vol = eng.warp_aggregate([cuda(f.permute(0, 2, 3, 1).contiguous()) for f in feats], cuda(P), cuda(hyps))
+    monkeypatch.setenv("DAMVS_CONV0_DZ", shape)
+    a = eng.costreg_logits(vol).clone()
+    monkeypatch.setenv("DAMVS_CONV0_DZ", "0")
+    monkeypatch.setenv("DAMVS_CONV0_REUSE", "1")
     b = eng.costreg_logits(vol).clone()
     assert torch.equal(a, b)
 
