@@ -85,6 +85,9 @@ SIGNATURES = (
     ("damvs_warp_aggregate_rows", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                           c_int, ctypes.POINTER(c_void_p), c_int, c_void_p, c_void_p, c_void_p)),
     ("damvs_costreg_layer", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p)),
+    ("damvs_costreg_layer_scaled", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                           c_void_p, c_void_p)),
+    ("damvs_tensor_amax", c_int, (c_void_p, c_void_p, ctypes.c_longlong, c_void_p)),
     ("damvs_stage_regress", c_int, (c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p)),
     ("damvs_regress", c_int, (c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -53,3 +53,63 @@ def cascade_cost(H: int, W: int, N: int, ndepths, e: int, channels=(32, 16, 8)):
 def roofline_time(nbytes: float, flops: float, dtype: str = "bf16") -> float:
     """Seconds at the roofline: max(bytes / HBM peak, FLOPs / MFMA peak)."""
     return max(nbytes / HBM_PEAK, flops / MFMA_PEAK[dtype])
+
+
+# ------------------------------------------------------------------------------- multi-GPU latency model (DESIGN §7)
+# One depth map over P GPUs (damvsnet_amd/sharded.py), predicted from measured one-GPU kernel times and the xGMI
+# figures of SURVEY.md section 5 (8 fully connected MI355X, 7 links x ~153 GB/s per GPU; all-gather / all-to-all can
+# use all 7 links, ~1 TB/s per GPU; ring collectives per-link bound). Nothing here is measured on several GPUs: the
+# model is the prediction a SCALE record would test.
+XGMI_LINK = 153e9       # B/s per link and direction
+XGMI_ALL = 7 * XGMI_LINK  # B/s per GPU when every link carries traffic (all-gather / all-to-all)
+P2P_LATENCY = 15e-6     # s per RCCL point-to-point group (one halo exchange of a batch half)
+COLL_LATENCY = 25e-6    # s per collective (all-gather / all-to-all launch and ring start)
+LAUNCH_FLOOR = 6e-6     # s: no kernel finishes faster, however small its share of the work
+
+
+def slab_factor(h: int, P: int, halo: int = 8) -> float:
+    """Rows a rank's U-Net layer computes (its tallest slab, multiple of 8, plus 2 x 8 halo rows) over h / P."""
+    n8 = h // 8
+    tallest = 8 * (n8 // P + (1 if n8 % P else 0))
+    return (tallest + 2 * halo) / (h / P)
+
+
+def sharded_latency(t1: dict, P: int, mode: str, stages, es: int = 2, link=XGMI_LINK, all_bw=XGMI_ALL):
+    """Predicted ms per depth map (B = 1) of the cascade on P GPUs.
+
+    t1      measured one-GPU times in ms at B = 1: t1["replicated"] (front end + hypotheses + GeoFF: every rank
+            runs them whole) and per stage s t1["stages"][s] = {"warp", "unet", "regress"} (ms)
+    stages  per stage (D, h, w, C) of the volume
+    mode    "gather" (north_star's literal form: D-sharded warp, one all-gather of the volume, U-Net and
+            regression replicated) or "depth" (D-sharded warp, all-to-all to H-slabs, U-Net on slabs with a halo
+            exchange after each of its 10 layers, regression on slabs, one all-gather of the output rows)
+    Returns {"total", "per_stage": [...], "comm": ms of communication on the critical path}."""
+    if P == 1:
+        tot = t1["replicated"] + sum(sum(st.values()) for st in t1["stages"])
+        return {"total": tot, "per_stage": [sum(st.values()) for st in t1["stages"]], "comm": 0.0}
+    per, comm = [], 0.0
+    for (D, h, w, C), st in zip(stages, t1["stages"]):
+        vol = D * h * w * C * es
+        warp = max(st["warp"] / P, LAUNCH_FLOOR * 1e3)
+        if mode == "gather":
+            c = (COLL_LATENCY + vol * (P - 1) / P / all_bw) * 1e3
+            t = warp + c + st["unet"] + st["regress"]
+        elif mode == "depth":
+            f = slab_factor(h, P)
+            a2a = (COLL_LATENCY + vol * 1.4 * (P - 1) / P / P / all_bw) * 1e3  # x1.4: the slab's halo rows
+            # 10 layers, two batch halves each: a P2P group per half and layer; the exchange of one half overlaps
+            # the other half's layer, so per layer the exposed cost is one group's latency + its bytes on one link
+            halo_bytes = 0.0
+            for l, cl in ((0, 8), (1, 16), (1, 16), (2, 32), (2, 32), (3, 64), (3, 64), (2, 32), (1, 16), (0, 8)):
+                halo_bytes += 2 * (8 >> l) * (w >> l) * (D >> l) * cl * es
+            halos = (10 * P2P_LATENCY + halo_bytes / link) * 1e3
+            unet = max(st["unet"] * f / P, 10 * LAUNCH_FLOOR * 1e3)
+            reg = max(st["regress"] * f / P, LAUNCH_FLOOR * 1e3)
+            rows = (COLL_LATENCY + 3 * h * w * 4 * (P - 1) / P / all_bw) * 1e3  # depth / conf / var rows
+            c = a2a + halos + rows
+            t = warp + unet + reg + c
+        else:
+            raise ValueError(mode)
+        per.append(t)
+        comm += c
+    return {"total": t1["replicated"] + sum(per), "per_stage": per, "comm": comm}

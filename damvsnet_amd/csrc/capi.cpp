@@ -307,8 +307,15 @@ Shapes level_shapes(int D, int h, int w) {
 }
 
 struct Workspace {
-  size_t status, rt, feat, vol, c[7], logits, total;
+  size_t status, amax, rt, feat, vol, c[7], logits, total;
 };
+
+// Magnitude slots of the fp32 stage's activation tensors (damvs_device.h prescale_of): the volume, conv0..conv6
+// outputs, conv7 / conv9 outputs after their in-place skip adds (c4', c2'). conv11's output feeds the exact-fp32 VALU
+// prob conv and needs none. kAmaxSlotBytes each, zeroed at the start of every stage forward.
+enum { AM_VOL = 0, AM_C0 = 1, AM_C4S = 8, AM_C2S = 9, AM_SLOTS = 10 };
+constexpr size_t kAmaxSlotBytes = (size_t)kAmaxSlotWords * 4;
+static_assert(kAmaxSlotBytes == DAMVS_AMAX_SLOT_BYTES, "damvs.h slot size");
 
 // c[i] holds conv_i's output for i = 0..6 (conv7/9/11 accumulate in place into c4/c2/c0).
 // Channel-blocked copies of the feature maps ([B][C/E][h][w][E], one 16-byte chunk per plane) for the one-lane warp
@@ -336,6 +343,8 @@ Workspace plan_ws(const damvs_stage* st, int B, int N, int D, int h, int w) {
   size_t o = 0;
   ws.status = o;  // the range status word at offset 0 (damvs_stage_status needs no shape)
   o += align_up(4);
+  ws.amax = o;  // fp32: the magnitude slots of the stage's activation tensors
+  if (st->dtype == DAMVS_F32) o += AM_SLOTS * kAmaxSlotBytes;
   ws.rt = o;
   o += align_up((size_t)B * (N > 1 ? N - 1 : 1) * 12 * 4);
   ws.feat = o;  // channel-blocked copies of the N feature maps (only when C spans several 16-B chunks)
@@ -404,7 +413,18 @@ ConvArgs conv_args(const damvs_stage* st, int li, int B, const Shapes& S, int li
   return a;
 }
 
-// U-Net through conv11 (+conv0 skip): the prob conv input ends in c[0].
+// layer i's input / output magnitude slots (-1: none): conv0 reads the volume's, convN writes c_N's, conv7 / conv9 write
+// the skip sums c4' / c2' that conv9 / conv11 read
+constexpr int kLayerSlots[10][2] = {{AM_VOL, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {6, 7}, {7, AM_C4S},
+                                    {AM_C4S, AM_C2S}, {AM_C2S, -1}};
+void set_slots(ConvArgs& a, const damvs_stage* st, char* amax, int layer) {
+  if (st->dtype != DAMVS_F32 || !amax) return;
+  a.in_amax = reinterpret_cast<const unsigned*>(amax + kLayerSlots[layer][0] * kAmaxSlotBytes);
+  a.out_amax = kLayerSlots[layer][1] < 0 ? nullptr : reinterpret_cast<unsigned*>(amax + kLayerSlots[layer][1] * kAmaxSlotBytes);
+}
+
+// U-Net through conv11 (+conv0 skip): the prob conv input ends in c[0]. fp32: the slots at ws + W.amax must hold the
+// volume's magnitude (and zeros for the rest) on entry.
 int run_unet(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, const void* vol, char* ws,
              const Workspace& W, int nlayers = 10) {
   const Shapes S = level_shapes(D, h, w);
@@ -420,6 +440,7 @@ int run_unet(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, c
   for (int i = 0; i < nlayers; ++i) {
     const Step& k = steps[i];
     ConvArgs a = conv_args(st, k.li, B, S, k.lin, k.lout, k.in, k.out, k.res);
+    set_slots(a, st, ws + W.amax, k.li);
     DAMVS_TRY(hip_check(launch_conv3d(s, st->dtype, a), "conv3d launch"));
   }
   return DAMVS_OK;
@@ -735,6 +756,10 @@ int damvs_stage_forward_probed(const damvs_stage* st, void* stream, int B, int N
                                : DAMVS_OK;
   };
   WarpArgs wa = warp_args(st, B, N, st->C, D, h, w, fv, rt, hyps, ws + W.vol);
+  if (st->dtype == DAMVS_F32) {  // fresh magnitude slots; the warp records the volume's
+    DAMVS_TRY(hip_check(hipMemsetAsync(ws + W.amax, 0, AM_SLOTS * kAmaxSlotBytes, s), "slot clear"));
+    wa.out_amax = reinterpret_cast<unsigned*>(ws + W.amax + AM_VOL * kAmaxSlotBytes);
+  }
   DAMVS_TRY(mark(0));
   DAMVS_TRY(hip_check(launch_warp_aggregate(s, st->dtype, st->mode, wa, blk), "warp_aggregate launch"));
   DAMVS_TRY(mark(1));
@@ -825,6 +850,12 @@ int damvs_costreg_logits(const damvs_stage* st, void* stream, int B, int D, int 
   if (workspace_bytes < W.total) return fail(DAMVS_E_WORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, W.total);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   char* ws = reinterpret_cast<char*>(workspace);
+  if (st->dtype == DAMVS_F32) {  // the handed-in volume's magnitude, measured once
+    DAMVS_TRY(hip_check(hipMemsetAsync(ws + W.amax, 0, AM_SLOTS * kAmaxSlotBytes, s), "slot clear"));
+    DAMVS_TRY(hip_check(launch_amax(s, static_cast<const float*>(volume), (long long)B * D * h * w * st->C,
+                                    reinterpret_cast<unsigned*>(ws + W.amax + AM_VOL * kAmaxSlotBytes)),
+                        "amax launch"));
+  }
   DAMVS_TRY(run_unet(st, s, B, D, h, w, volume, ws, W));
   return hip_check(launch_prob_conv(s, st->dtype, B, st->base, D, h, w, ws + W.c[0], st->prob_w, nullptr, logits),
                    "prob conv launch");
@@ -832,13 +863,28 @@ int damvs_costreg_logits(const damvs_stage* st, void* stream, int B, int D, int 
 
 int damvs_costreg_layer(const damvs_stage* st, void* stream, int layer, int B, int D, int h, int w, const void* in,
                         void* out) {
+  return damvs_costreg_layer_scaled(st, stream, layer, B, D, h, w, in, out, nullptr, nullptr);
+}
+
+int damvs_costreg_layer_scaled(const damvs_stage* st, void* stream, int layer, int B, int D, int h, int w,
+                               const void* in, void* out, const void* in_slot, void* out_slot) {
   if (!st || !in || !out) return fail(DAMVS_E_ARG, "null argument");
   if (layer < 0 || layer > 9) return fail(DAMVS_E_ARG, "layer %d not in 0..9", layer);
   DAMVS_TRY(check_stage_shape(st, B, 2, D, h, w));
   const Shapes S = level_shapes(D, h, w);
   const bool deconv = layer >= 7;  // conv7 / conv9 / conv11: relu(deconv) + skip, in place on `out`
   ConvArgs a = conv_args(st, layer, B, S, kLayerLevels[layer][0], kLayerLevels[layer][1], in, out, deconv ? out : nullptr);
+  if (st->dtype == DAMVS_F32) {
+    a.in_amax = static_cast<const unsigned*>(in_slot);
+    a.out_amax = static_cast<unsigned*>(out_slot);
+  }
   return hip_check(launch_conv3d(reinterpret_cast<hipStream_t>(stream), st->dtype, a), "conv3d launch");
+}
+
+int damvs_tensor_amax(void* stream, const float* x, long long n, void* slot) {
+  if (!x || !slot) return fail(DAMVS_E_ARG, "null argument");
+  if (n < 0) return fail(DAMVS_E_SHAPE, "n %lld", n);
+  return hip_check(launch_amax(reinterpret_cast<hipStream_t>(stream), x, n, static_cast<unsigned*>(slot)), "amax launch");
 }
 
 int damvs_stage_regress(const damvs_stage* st, void* stream, int B, int D, int h, int w, const void* c0,

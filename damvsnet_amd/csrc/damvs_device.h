@@ -73,6 +73,53 @@ __device__ __forceinline__ void mma_split32(const F16Pair& w, const F16Pair& x, 
   acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, w.h), __builtin_bit_cast(f16x8_t, x.h), acc, 0, 0, 0);
 }
 
+// ---------------------------------------------------------------- activation prescale (fp32 path, round 6)
+// The split pieces are f16: unscaled, |x| >= 65520 overflows the hi piece and |x| < 2^-3 leaves the lo piece subnormal
+// (absolute floor 2^-25). Every activation tensor of the stage (cost volume, U-Net levels) therefore carries its
+// magnitude: each producer records max |y| of what it stores (per wave, one vector atomic max of the float's bit pattern
+// -- non-negative floats order as unsigned integers, NaN above inf -- into one of kAmaxReps replicas of the tensor's
+// slot), and each consumer reads the slot at its start and splits x * 2^k instead of x, with k chosen so that the
+// tensor's maximum lands in [2^13, 2^14): both pieces are then normal f16 for every value down to max * 2^-17. Its
+// epilogue multiplies the accumulator by wscale * 2^-k. Power-of-two scaling is exact, and f16 / fp32 rounding of
+// normal numbers is scale-invariant, so wherever the unscaled pieces were both normal the result is bitwise the same;
+// elsewhere it is the exact fp32 product the unscaled split could not represent. Slots are zeroed per stage forward.
+
+struct Prescale {
+  float s, inv;  // x * s is split; the accumulator is scaled back by inv (= 1 / s)
+};
+// max of a slot's replicas (every lane of the wave must be active: each of the first kAmaxReps lanes loads one)
+__device__ __forceinline__ Prescale prescale_of(const unsigned* __restrict__ amax) {
+  if (!amax) return Prescale{1.f, 1.f};
+  const int lane = threadIdx.x & 63;
+  unsigned m = lane < kAmaxReps ? __hip_atomic_load(amax + lane * kAmaxStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+  m = __builtin_amdgcn_readfirstlane(m);
+  if (m == 0u) return Prescale{1.f, 1.f};  // an all-zero tensor
+  int e = (int)((m >> 23) & 0xff) - 127;  // floor(log2(max)); subnormal maxima count as 2^-127, NaN / inf as 2^128
+  int k = 13 - (e < -127 ? -127 : e);
+  k = k < -100 ? -100 : k > 100 ? 100 : k;  // s and 1 / s stay normal fp32, with the weights' 2^-k too
+  return Prescale{__uint_as_float((unsigned)(127 + k) << 23), __uint_as_float((unsigned)(127 - k) << 23)};
+}
+// |v| folded into a running maximum (bit patterns; NaN propagates)
+__device__ __forceinline__ unsigned amax_fold(unsigned m, float v) { return max(m, __float_as_uint(v) & 0x7fffffffu); }
+// one wave's maximum into replica r of the slot (every lane of the wave must be active)
+__device__ __forceinline__ void amax_flush(unsigned m, unsigned* __restrict__ amax, int r) {
+  if (!amax) return;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0 && m != 0u) atomicMax(amax + (r & (kAmaxReps - 1)) * kAmaxStride, m);
+}
+
+__device__ __forceinline__ float4 scale4(const float4& x, float s) { return make_float4(x.x * s, x.y * s, x.z * s, x.w * s); }
+// split8 of (a, b) * s
+__device__ __forceinline__ F16Pair split8s(const float4& a, const float4& b, float s) {
+  return split8(scale4(a, s), scale4(b, s));
+}
+__device__ __forceinline__ F16Pair split8s(const uint4& a, const uint4& b, float s) {
+  return split8s(__builtin_bit_cast(float4, a), __builtin_bit_cast(float4, b), s);
+}
+
 // MFMA K-fragment traits shared by the conv kernels. raw: one lane's 16-byte K fragment (A or B).
 //   mma(w, x, acc):     x as loaded from the activation tensor (fp32: split here, per use)
 //   stage(x):           the form an LDS tile keeps (fp32: split once when the tile is filled)

@@ -19,6 +19,10 @@ enum StoreType { ST_F32 = 0, ST_BF16 = 1 };
 enum AggMode { AGG_ADAPTIVE = 0, AGG_VARIANCE = 1, AGG_WARP_ONLY = 2 };
 
 constexpr int kMaxViews = 16;
+// magnitude slots of the fp32 prescale (damvs_device.h prescale_of; include/damvs.h DAMVS_AMAX_SLOT_BYTES)
+constexpr int kAmaxReps = 32;    // replicas per slot (one 128-byte line each): atomics spread over 32 addresses
+constexpr int kAmaxStride = 32;  // words between replicas
+constexpr int kAmaxSlotWords = kAmaxReps * kAmaxStride;
 constexpr int kMaxPhases = 8;
 
 // ---------------------------------------------------------------- warp + aggregation
@@ -37,6 +41,7 @@ struct WarpArgs {
   // computed rows; else a tile of tile_r rows x ppb / tile_r columns, tiles dealt strip by strip (tile_sw tiles wide,
   // top to bottom), so the blocks in flight on one XCD cover a compact 2D region of the reference image
   int tile_r, tile_sw, tiles_x;
+  unsigned* out_amax;  // fp32: magnitude slot of the written volume (damvs_device.h prescale_of), nullptr: none
 };
 
 // n / d for 0 <= n < 2^31 without a hardware divide: q = (umulhi(n, mul) + n) >> shift.
@@ -94,6 +99,10 @@ struct ConvArgs {
   // fp32: the phases of wgat32 (build_phases(., 32) at layer creation): K chunks and weight offsets at 32 K per chunk
   // (the taps are those of ph)
   int k32_chunks[kMaxPhases], k32_off[kMaxPhases];
+  // fp32 activation prescale (damvs_device.h prescale_of): the input tensor's magnitude slot (nullptr: unscaled) and
+  // the slot this layer's stored outputs are recorded into (nullptr: not recorded); bf16 ignores both
+  const unsigned* in_amax;
+  unsigned* out_amax;
 };
 
 // ---------------------------------------------------------------- 2D front-end convolutions
@@ -134,6 +143,8 @@ struct Conv2dArgs {
 hipError_t launch_proj_prepare(hipStream_t s, int B, int N, const float* proj, float* rt);
 // status[0] = 1 when any of the n floats of a, b or c is non-finite (sticky: damvs_stage_status clears it)
 hipError_t launch_finite_check(hipStream_t s, const float* a, const float* b, const float* c, long long n, int* status);
+// fold max |x| of n floats into a magnitude slot (damvs_device.h prescale_of)
+hipError_t launch_amax(hipStream_t s, const float* x, long long n, unsigned* slot);
 hipError_t launch_hyp_linear(hipStream_t s, int B, int D, int h, int w, const float* dv, int Dv, float* out);
 hipError_t launch_hyp_refine(hipStream_t s, int B, int D, int H, int W, int scale, const float* pd,
                              const float* pv, int hp, int wp, float* out);

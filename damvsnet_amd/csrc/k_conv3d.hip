@@ -67,18 +67,49 @@ constexpr int kGroups = 4;  // 16-voxel column groups per wave (64 output voxels
 #define DAMVS_DIAG_SKIP_EPI 0
 #endif
 
+// The fp32 prescale of a conv kernel's input (damvs_device.h prescale_of); bf16 kernels are unscaled (no load).
+template <typename T>
+__device__ __forceinline__ Prescale ps_in(const ConvArgs& a) {
+  if constexpr (sizeof(T) == 4) return prescale_of(a.in_amax);
+  else return Prescale{1.f, 1.f};
+}
+// the epilogue's accumulator scale: the weights' 2^-k (fp32) times the input's 2^-k
+template <typename T>
+__device__ __forceinline__ float ps_wscale(const ConvArgs& a, const Prescale& ps) {
+  if constexpr (sizeof(T) == 4) return a.wscale * ps.inv;
+  else return a.wscale;
+}
+// fold the stored values v[0..n) of an fp32 layer into the running output maximum (ok: the store is not dropped)
+template <typename T, int NV>
+__device__ __forceinline__ void am_fold(unsigned& am, bool ok, const float* v) {
+  if constexpr (sizeof(T) == 4) {
+    unsigned m = am;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) m = amax_fold(m, v[i]);
+    am = ok ? m : am;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void am_flush(const ConvArgs& a, unsigned am, int r) {
+  if constexpr (sizeof(T) == 4) amax_flush(am, a.out_amax, r);
+}
+// a loaded 16-byte fragment times the prescale (fp32; bf16 as is)
+__device__ __forceinline__ float4 ps_scale(const float4& x, float s) { return scale4(x, s); }
+__device__ __forceinline__ uint4 ps_scale(const uint4& x, float) { return x; }
+
 // Epilogue for 4 channels: bias, ReLU, skip add (after the ReLU, models/module.py:537-539), store.
 template <typename T>
 __device__ __forceinline__ void finish4(const ConvArgs& a, __amdgpu_buffer_rsrc_t ro, __amdgpu_buffer_rsrc_t rr,
                                         const typename BufIO<T>::quad& q, bool has_res, uint32_t off, bool ok,
-                                        const float* bias, const f32x4_t& acc) {
+                                        const float* bias, const f32x4_t& acc, float wsc, unsigned& am) {
   float r[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    r[i] = fmaf(acc[i], a.wscale, bias[i]);
+    r[i] = fmaf(acc[i], wsc, bias[i]);
     if (a.relu) r[i] = relu(r[i]);
   }
   if (has_res) BufIO<T>::addq(q, r);
+  am_fold<T, 4>(am, ok, r);
   BufIO<T>::stq(ro, ok ? off : kOOB, r);
   (void)rr;
 }
@@ -118,7 +149,10 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
   const int n = lane & 15, g = lane >> 4;
   const int Qtot = a.B * a.Dq * a.Hq * a.Wq;
   const int base = (qblk * 4 + wave) * (KG * 16);
-  if (base >= Qtot) return;
+  if (base >= Qtot) return;  // (whole waves: the rest keep all lanes to the end, as amax_flush needs)
+  const Prescale ps = ps_in<T>(a);
+  const float wsc = ps_wscale<T>(a, ps);
+  unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
 
   const int IS = a.in_stride, OS = a.out_stride;
   int zs[KG], ys[KG], xs[KG], pin[KG], pout[KG];
@@ -167,6 +201,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
       const bool ok = valid[j] && tv && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
                       (unsigned)ix < (unsigned)a.Wi;
       xf[j] = IO::frag(r0, ok ? (uint32_t)((pin[j] + tapoff) * a.Cin + ci) * ES : kOOB);
+      if constexpr (sizeof(T) == 4) xf[j] = scale4(xf[j], ps.s);
     }
     ci += rc;
     t += qt;
@@ -195,7 +230,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
                         (unsigned)ix < (unsigned)a.Wi;
         const uint32_t off = (uint32_t)((pin[j] + tapoff) * a.Cin + ci) * ES;
         const float4 lo4 = IO::frag(r0, ok ? off : kOOB), hi4 = IO::frag(r0, ok ? off + 16u : kOOB);
-        xf[j] = split8(lo4, hi4);
+        xf[j] = split8s(lo4, hi4, ps.s);
       }
       ci += rc;
       t += qt;
@@ -231,13 +266,15 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
       if (!lead) continue;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        r[i] = fmaf(r[i], a.wscale, b8[i]);
+        r[i] = fmaf(r[i], wsc, b8[i]);
         if (a.relu) r[i] = relu(r[i]);
       }
       const uint32_t off = valid[j] ? (uint32_t)(pout[j] * 8) * ES : kOOB;
       if (a.resid) Vox8<T>::add(rr, off, r);
+      am_fold<T, 8>(am, valid[j], r);
       Vox8<T>::store(ro, off, r);
     }
+    am_flush<T>(a, am, blockIdx.x * 4 + wave);
     return;
   }
   if constexpr (kSkip16) {
@@ -301,9 +338,10 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const uint32_t off = (uint32_t)(pout[j] * a.Cout + m * 16 + cg) * ES;
-      finish4<T>(a, ro, rr, q[j][m], a.resid != nullptr, off, valid[j] && cok[m], bias[m], acc[j][m]);
+      finish4<T>(a, ro, rr, q[j][m], a.resid != nullptr, off, valid[j] && cok[m], bias[m], acc[j][m], wsc, am);
     }
   }
+  am_flush<T>(a, am, blockIdx.x * 4 + wave);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -351,6 +389,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
   const int z0 = tz * LTD, y0 = ty * LTH, x0 = tx * LTW;
 
   // halo fill: chunk c = (row, col) with row = (hz, hy); one row is LHW contiguous voxels in HBM
+  const Prescale ps = ps_in<T>(a);
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * sizeof(T));
   const int vin0 = b * a.Di * a.Hi * a.Wi;
   stage_chunks<TILE_CHUNKS, 8>(tile, [&](int c) {
@@ -360,7 +399,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
     const bool ok = (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
     const uint32_t off = (uint32_t)(((vin0 + (iz * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16);
     return BufIO<T>::frag(rin, ok ? off : kOOB);
-  }, [](const raw& r) { return Frag<T>::stage(r); });
+  }, [&](const raw& r) { return Frag<T>::stage(ps_scale(r, ps.s)); });
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -478,6 +517,8 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
 #pragma unroll
     for (int i = 0; i < 4; ++i) bias[m][i] = cok[m] ? a.bias[co + i] : 0.f;
   }
+  const float wsc = ps_wscale<T>(a, ps);
+  unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
 #pragma unroll
   for (int j = 0; j < kLdsGroups; ++j) {
     const int oz = z0 + wave, oy = y0 + j, ox = x0 + n;
@@ -492,9 +533,10 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const uint32_t off = (uint32_t)(pout * a.Cout + m * 16 + g * 4) * ES;
-      finish4<T>(a, ro, rr, q[m], a.resid != nullptr, off, vok && cok[m], bias[m], acc[j][m]);
+      finish4<T>(a, ro, rr, q[m], a.resid != nullptr, off, vok && cok[m], bias[m], acc[j][m], wsc, am);
     }
   }
+  am_flush<T>(a, am, blockIdx.x * 4 + wave);
 }
 
 // Row-pair variant for Cout <= 8 (conv0 of every stage): a 16-row MFMA tile holds 8 channels of
@@ -531,6 +573,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, 
   const int b = tt / tiles_z;
   const int z0 = tz * LTD, y0 = ty * LTH, x0 = tx * LTW;
 
+  const Prescale ps = ps_in<T>(a);
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * sizeof(T));
   const int vin0 = b * a.Di * a.Hi * a.Wi;
   stage_chunks<TILE_CHUNKS, 8>(tile, [&](int c) {
@@ -540,7 +583,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, 
     const bool ok = (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
     const uint32_t off = (uint32_t)(((vin0 + (iz * a.Hi + iy) * a.Wi + x0 - 1) * CH + col) * 16);
     return BufIO<T>::frag(rin, ok ? off : kOOB);
-  }, [](const raw& r) { return Frag<T>::stage(r); });
+  }, [&](const raw& r) { return Frag<T>::stage(ps_scale(r, ps.s)); });
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -591,6 +634,8 @@ __global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, 
   float bias[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) bias[i] = cok ? a.bias[co + i] : 0.f;
+  const float wsc = ps_wscale<T>(a, ps);
+  unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
     const int oz = z0 + wave, oy = y0 + 2 * j + r, ox = x0 + n;
@@ -599,8 +644,9 @@ __global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, 
     const uint32_t off = (uint32_t)(pout * a.Cout + co) * ES;
     typename BufIO<T>::quad q;
     if (a.resid) q = BufIO<T>::ldq(rr, vok ? off : kOOB);
-    finish4<T>(a, ro, rr, q, a.resid != nullptr, off, vok, bias, acc[j]);
+    finish4<T>(a, ro, rr, q, a.resid != nullptr, off, vok, bias, acc[j], wsc, am);
   }
+  am_flush<T>(a, am, blockIdx.x * 4 + wave);
 }
 
 // z-sliding row-pair variant (conv0): a block owns an 8-row x TX-column output window over ZC
@@ -613,7 +659,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, 
 // the split-f16 form (ZForm<float>), the row-pair packing at 32 K per chunk (ConvArgs::wpack32).
 // Wave w owns row pair (y0 + 2w, y0 + 2w + 1); lane column n the output x = x0 + 16 xg + n.
 template <typename T, int CIN, int TXG>
-__global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 && CIN <= 16 ? 2 : 1) void conv3d_zslide_pair_kernel(const ConvArgs a, int tiles_x, int tiles_y,
+__global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 && CIN <= 8 ? 2 : 1) void conv3d_zslide_pair_kernel(const ConvArgs a, int tiles_x, int tiles_y,
                                                                  int nzc, int zc, int ntiles) {
   typedef ZForm<T> Z;
   typedef typename Z::frag frag;
@@ -637,6 +683,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 && CIN <= 16 ? 2 : 
   const int zend = min(zb + zc, a.Do);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * ES);
+  const Prescale ps = ps_in<T>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const float wsc = ps_wscale<T>(a, ps);
+  unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
@@ -660,7 +709,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 && CIN <= 16 ? 2 : 
         dst[c] = v[i][0];
       } else {
         const int vox = c / CH, q = c - vox * CH, sw = Z::template zsw<S>(vox % PW);
-        const F16Pair p = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+        const F16Pair p = split8s(v[i][0], v[i][1], ps.s);
         dst[vox * S + (q ^ sw)] = p.h;
         dst[vox * S + ((CH + q) ^ sw)] = p.l;
       }
@@ -779,9 +828,10 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 && CIN <= 16 ? 2 : 
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        v[i] = (PL == 1 ? acc[xg][i] : acc[xg][i] * a.wscale) + bias[i];  // 2^-k: exact
+        v[i] = (PL == 1 ? acc[xg][i] : acc[xg][i] * wsc) + bias[i];  // 2^-k: exact
         if (a.relu) v[i] = relu(v[i]);
       }
+      am_fold<T, 4>(am, vok, v);
       BufIO<T>::stq(ro, vok ? off : kOOB, v);
     }
     if (z + 1 < zend) store_plane(z + 2, cur);  // slot of plane z - 2, last read before the previous barrier
@@ -791,6 +841,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 && CIN <= 16 ? 2 : 
     step(z, pa, pb);
     if (z + 1 < zend) step(z + 1, pb, pa);
   }
+  am_flush<T>(a, am, blockIdx.x * 4 + wave);
 }
 
 // conv0 with each input plane's B fragments read from LDS once (round 3): input plane p feeds output planes p + 1,
@@ -831,6 +882,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (CIN == 32 ? 1 : 
   const int zend = min(zb + zc, a.Do);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * ES);
+  const Prescale ps = ps_in<T>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const float wsc = ps_wscale<T>(a, ps);
+  unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
@@ -854,7 +908,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (CIN == 32 ? 1 : 
         dst[c] = v[i][0];
       } else {
         const int vox = c / CH, q = c - vox * CH, sw = Z::template zsw<S>(vox % PW);
-        const F16Pair p = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+        const F16Pair p = split8s(v[i][0], v[i][1], ps.s);
         dst[vox * S + (q ^ sw)] = p.h;
         dst[vox * S + ((CH + q) ^ sw)] = p.l;
       }
@@ -899,9 +953,10 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (CIN == 32 ? 1 : 
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        v[i] = (PL == 1 ? acc[xg][i] : acc[xg][i] * a.wscale) + bias[i];  // 2^-k: exact
+        v[i] = (PL == 1 ? acc[xg][i] : acc[xg][i] * wsc) + bias[i];  // 2^-k: exact
         if (a.relu) v[i] = relu(v[i]);
       }
+      am_fold<T, 4>(am, vok, v);
       BufIO<T>::stq(ro, vok ? off : kOOB, v);
     }
   };
@@ -949,6 +1004,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (CIN == 32 ? 1 : 
     step(p, pa, pb);
     if (p + 1 <= zend) step(p + 1, pb, pa);
   }
+  am_flush<T>(a, am, blockIdx.x * 4 + wave);
 }
 
 // fp32 conv0 with the kernel depths on different waves (round 6). The input-plane walk above keeps all 36 / 18 A pairs
@@ -965,7 +1021,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (CIN == 32 ? 1 : 
 // 2 / 3 of its rate beside the MFMAs at full rate. Ring: 2 slots as in the walk; chain buffers double-buffered by the
 // output plane's parity.
 template <int CIN, int RP, int TXG>
-__global__ __launch_bounds__(192 * RP) DAMVS_WAVES(CIN == 32 ? 3 : 4) void conv0_dz_kernel(
+__global__ __launch_bounds__(192 * RP) DAMVS_WAVES(CIN == 8 ? 4 : 3) void conv0_dz_kernel(
     const ConvArgs a, int tiles_x, int tiles_y, int nzc, int zc, int ntiles) {
   typedef ZForm<float> Z;
   typedef Z::frag frag;
@@ -993,6 +1049,9 @@ __global__ __launch_bounds__(192 * RP) DAMVS_WAVES(CIN == 32 ? 3 : 4) void conv0
   const int zend = min(zb + zc, a.Do);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * ES);
+  const Prescale ps = ps_in<float>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const float wsc = ps_wscale<float>(a, ps);
+  unsigned am = 0u;  // max |stored value| (the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) DAMVS_INLINE {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
@@ -1013,7 +1072,7 @@ __global__ __launch_bounds__(192 * RP) DAMVS_WAVES(CIN == 32 ? 3 : 4) void conv0
       const int c = threadIdx.x + i * NT;
       if (c >= PH * PW * CH) continue;
       const int vox = c / CH, q = c - vox * CH, sw = Z::template zsw<S>(vox % PW);
-      const F16Pair pr = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+      const F16Pair pr = split8s(v[i][0], v[i][1], ps.s);
       dst[vox * S + (q ^ sw)] = pr.h;
       dst[vox * S + ((CH + q) ^ sw)] = pr.l;
     }
@@ -1086,9 +1145,10 @@ __global__ __launch_bounds__(192 * RP) DAMVS_WAVES(CIN == 32 ? 3 : 4) void conv0
           float v[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            v[i] = acc[xg][i] * a.wscale + bias[i];  // 2^-k: exact
+            v[i] = acc[xg][i] * wsc + bias[i];  // 2^-k: exact
             if (a.relu) v[i] = relu(v[i]);
           }
+          am_fold<float, 4>(am, vok, v);
           BufIO<float>::stq(ro, vok ? off : kOOB, v);
         }
       }
@@ -1100,6 +1160,7 @@ __global__ __launch_bounds__(192 * RP) DAMVS_WAVES(CIN == 32 ? 3 : 4) void conv0
     step(p, pa, pb);
     if (p + 1 <= zend) step(p + 1, pb, pa);
   }
+  am_flush<float>(a, am, blockIdx.x * 3 * RP + wave);
 }
 
 template <int CIN, int RP, int TXG>
@@ -1125,7 +1186,7 @@ bool conv0_dz_shape(int CIN, int& rp, int& txg) {
   const char* v = getenv("DAMVS_CONV0_DZ");
   rp = 4;
   txg = CIN == 8 ? 2 : 1;
-  if (!v) return true;
+  if (!v || !v[0]) return true;  // unset or empty: the default shape
   if (v[0] == '0') return false;
   const char* c = strchr(v, ',');
   rp = atoi(v);
@@ -1267,6 +1328,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : 1) void conv_
   const int zend = min(zb + zc, a.Do);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 16 * ES);
+  const Prescale ps = ps_in<T>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const float wsc = ps_wscale<T>(a, ps);
+  unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
@@ -1290,7 +1354,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : 1) void conv_
         dst[c] = v[i][0];
       } else {
         const int vox = c / CH, q = c - vox * CH, sw = Z::template zsw<S>(vox % PW);
-        const F16Pair p = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+        const F16Pair p = split8s(v[i][0], v[i][1], ps.s);
         dst[vox * S + (q ^ sw)] = p.h;
         dst[vox * S + ((CH + q) ^ sw)] = p.l;
       }
@@ -1359,9 +1423,10 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : 1) void conv_
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          v[i] = (PL == 1 ? acc[r][xg][i] : acc[r][xg][i] * a.wscale) + bias[i];  // 2^-k: exact
+          v[i] = (PL == 1 ? acc[r][xg][i] : acc[r][xg][i] * wsc) + bias[i];  // 2^-k: exact
           if (a.relu) v[i] = relu(v[i]);
         }
+        am_fold<T, 4>(am, ok, v);
         BufIO<T>::stq(ro, ok ? (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * 16 + g * 4) * (uint32_t)ES : kOOB, v);
       }
     if (z + 1 < zend) store_plane(z + 2, cur);
@@ -1371,6 +1436,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : 1) void conv_
     step(z, pa, pb);
     if (z + 1 < zend) step(z + 1, pb, pa);
   }
+  am_flush<T>(a, am, blockIdx.x * 4 + wave);
 }
 
 // Returns hipErrorNotSupported when no LDS variant fits this layer (caller falls back).
@@ -1435,6 +1501,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 2 ? 3 : 2) void decon
   const int zend = min(zb + zc, a.Di);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 16 * ES);
+  const Prescale ps = ps_in<T>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const float wsc = ps_wscale<T>(a, ps);
+  unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
@@ -1458,7 +1527,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 2 ? 3 : 2) void decon
         dst[c] = v[i][0];
       } else {
         const int vox = c / CH, q = c - vox * CH, sw = Z::template zsw<S>(vox % PW);
-        const F16Pair p = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+        const F16Pair p = split8s(v[i][0], v[i][1], ps.s);
         dst[vox * S + (q ^ sw)] = p.h;
         dst[vox * S + ((CH + q) ^ sw)] = p.l;
       }
@@ -1563,7 +1632,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 2 ? 3 : 2) void decon
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const float4 f = __builtin_bit_cast(float4, rq[k][i >> 2]);
-          v[i] = v[i] * a.wscale + b8[i];  // 2^-k: exact
+          v[i] = v[i] * wsc + b8[i];  // 2^-k: exact
           if (a.relu) v[i] = relu(v[i]);
           v[i] += (i & 3) == 0 ? f.x : (i & 3) == 1 ? f.y : (i & 3) == 2 ? f.z : f.w;
         }
@@ -1610,6 +1679,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
   const int zend = min(zb + zc, a.Di);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 32 * ES);
+  const Prescale ps = ps_in<T>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const float wsc = ps_wscale<T>(a, ps);
+  unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
@@ -1633,7 +1705,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
         dst[c] = v[i][0];
       } else {
         const int vox = c / CH, q = c - vox * CH, sw = Z::template zsw<S>(vox % PW);
-        const F16Pair p = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+        const F16Pair p = split8s(v[i][0], v[i][1], ps.s);
         dst[vox * S + (q ^ sw)] = p.h;
         dst[vox * S + ((CH + q) ^ sw)] = p.l;
       }
@@ -1745,12 +1817,15 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const float4 f = __builtin_bit_cast(float4, rq[k][i >> 2]);
-            v[i] = v[i] * a.wscale + b8[i];  // 2^-k: exact
+            v[i] = v[i] * wsc + b8[i];  // 2^-k: exact
             if (a.relu) v[i] = relu(v[i]);
             v[i] += (i & 3) == 0 ? f.x : (i & 3) == 1 ? f.y : (i & 3) == 2 ? f.z : f.w;
           }
         }
-        if (lead) Vox8<T>::store(ro, off[k], v);
+        if (lead) {
+          am_fold<T, 8>(am, off[k] != kOOB, v);
+          Vox8<T>::store(ro, off[k], v);
+        }
       }
     }
     if (qz + 1 < zend) store_plane(qz + 2, cur);
@@ -1760,6 +1835,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
     step(qz, pa, pb);
     if (qz + 1 < zend) step(qz + 1, pb, pa);
   }
+  am_flush<T>(a, am, blockIdx.x * 4 + (threadIdx.x >> 6));
 }
 
 // conv1 (Conv3d k3 s2 p1, 8 -> 16 channels) streamed along z: output plane z reads input planes
@@ -1798,6 +1874,9 @@ __global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a
   const int ix0 = 2 * ox0 - 1, iy0 = 2 * oy0 - 1;
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 8 * ES);
+  const Prescale ps = ps_in<T>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const float wsc = ps_wscale<T>(a, ps);
+  unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
@@ -1822,7 +1901,7 @@ __global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a
       } else {
         const int row = c / PW, col = c - row * PW, hp = col >> 1;
         const int p = row * PWE + (col & 1) * HCE + hp, sw = Z::template zsw<2>(hp);
-        const F16Pair q = split8(__builtin_bit_cast(float4, v[i][0]), __builtin_bit_cast(float4, v[i][1]));
+        const F16Pair q = split8s(v[i][0], v[i][1], ps.s);
         dst[p * 2 + sw] = q.h;
         dst[p * 2 + (1 ^ sw)] = q.l;
       }
@@ -1897,9 +1976,10 @@ __global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        v[i] = (PL == 1 ? acc[r][i] : acc[r][i] * a.wscale) + bias[i];  // 2^-k: exact
+        v[i] = (PL == 1 ? acc[r][i] : acc[r][i] * wsc) + bias[i];  // 2^-k: exact
         if (a.relu) v[i] = relu(v[i]);
       }
+      am_fold<T, 4>(am, ok, v);
       BufIO<T>::stq(ro, ok ? (uint32_t)((((b * a.Do + z) * a.Ho + oy) * a.Wo + ox) * 16 + g * 4) * (uint32_t)ES : kOOB, v);
     }
     if (more) {  // NS 5: slots of planes 2z - 3 and 2z - 2, last read before the previous barrier
@@ -1909,6 +1989,7 @@ __global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a
     }
     __syncthreads();
   }
+  am_flush<T>(a, am, blockIdx.x * 4 + wave);
 }
 
 bool deconv_zslide_disabled() {  // read per call: tests flip it between launches

@@ -12,6 +12,8 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include <algorithm>
+
 #include "damvs_device.h"
 
 namespace damvs {
@@ -587,6 +589,21 @@ __global__ __launch_bounds__(256) void finite_check_kernel(const float* __restri
   for (long long i = blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
     bad |= (a[i] * 0.f + b[i] * 0.f + c[i] * 0.f) != 0.f;  // x * 0 is 0 unless x is inf or NaN
   if (bad) __builtin_amdgcn_raw_buffer_store_b32(1u, make_rsrc(status, 4), 0, 0, 0);
+}
+
+// max |x| of n floats folded into a magnitude slot (damvs_device.h prescale_of): for tensors no product kernel recorded
+// (a volume handed to damvs_costreg_logits, damvs_tensor_amax). Grid-stride, one atomic per wave.
+__global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, long long n, unsigned* __restrict__ slot) {
+  unsigned m = 0u;
+  for (long long i = blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) m = amax_fold(m, x[i]);
+  amax_flush(m, slot, blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+}
+
+hipError_t launch_amax(hipStream_t s, const float* x, long long n, unsigned* slot) {
+  const long long blocks = std::min<long long>((n + 255) / 256, 2048);
+  if (blocks < 1) return hipSuccess;
+  hipLaunchKernelGGL(amax_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, n, slot);
+  return hipGetLastError();
 }
 
 hipError_t launch_regress(hipStream_t s, int B, int D, int h, int w, const float* logits, const float* hyps,

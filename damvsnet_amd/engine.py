@@ -157,13 +157,27 @@ class StageEngine:
                                                   R, out_y, fptrs, layout, ptr(rt), ptr(hyps), ptr(out)))
         return out
 
-    def unet_layer(self, layer, D, h, w, inp, out):
+    def unet_layer(self, layer, D, h, w, inp, out, in_slot=None, out_slot=None):
         """CostRegNet layer ``layer`` (0..9 = conv0..conv6, conv7, conv9, conv11) of a level-0 volume of
-        D x h x w; deconvs add into ``out`` in place (it holds the skip tensor)."""
+        D x h x w; deconvs add into ``out`` in place (it holds the skip tensor). ``in_slot`` / ``out_slot``: fp32
+        magnitude slots (new_slots rows) of the input / output tensor (damvs_costreg_layer_scaled); None: unscaled /
+        not recorded."""
         B = inp.shape[0]
-        check(self._lib.damvs_costreg_layer(self.handle, _capi.stream_ptr(self.device), layer, B, D, h, w, ptr(inp),
-                                            ptr(out)))
+        check(self._lib.damvs_costreg_layer_scaled(self.handle, _capi.stream_ptr(self.device), layer, B, D, h, w,
+                                                   ptr(inp), ptr(out), ptr(in_slot), ptr(out_slot)))
         return out
+
+    # ---- fp32 magnitude slots for layer-by-layer execution (include/damvs.h DAMVS_AMAX_SLOT_BYTES)
+    SLOT_WORDS = 1024  # DAMVS_AMAX_SLOT_BYTES / 4
+
+    def new_slots(self, n=10):
+        """n zeroed magnitude slots (int32 rows of SLOT_WORDS words) on the engine's device."""
+        return torch.zeros(n, self.SLOT_WORDS, dtype=torch.int32, device=self.device)
+
+    def tensor_amax(self, t, slot):
+        """Fold max |t| (a contiguous float32 device tensor) into ``slot`` (damvs_tensor_amax)."""
+        check(self._lib.damvs_tensor_amax(_capi.stream_ptr(self.device), ptr(t), t.numel(), ptr(slot)))
+        return slot
 
     def unet_buffers(self, B, D, h, w):
         """Level tensors c0..c6 (conv0..conv6 outputs, NDHWC) of a D x h x w volume."""

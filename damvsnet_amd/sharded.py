@@ -32,6 +32,12 @@ Results equal the unsharded stage: every voxel of the warp and every output of a
 kernel arithmetic from the same inputs (tests/test_sharded.py, tests/test_gpu_sharded.py). The front-end
 (FeatureNet, GeoFeatureFusion) and the hypotheses run replicated on every rank.
 
+fp32 magnitude slots (include/damvs.h DAMVS_AMAX_SLOT_BYTES): the fp32 path splits every activation tensor at a
+scale set by its largest magnitude, which the unsharded stage records with atomics as its kernels store. Sharded, each
+rank measures the part of a tensor it owns (its depth planes of the volume, or its slab's rows without the halos, which
+hold partial sums until they are refreshed) and one all-gather of those maxima gives every rank the whole tensor's:
+the same scale, so the same bits as the unsharded stage.
+
 Communication goes through a ``Comm``: ``TorchComm`` (torch.distributed; backend "nccl" = RCCL over xGMI, "gloo"
 for CPU tests) or ``ThreadGroup`` (P ranks as threads of one process: single-device rehearsal and tests).
 """
@@ -47,6 +53,30 @@ HALO = 8  # level-0 halo rows; level l carries HALO >> l (the U-Net has three st
 # U-Net schedule: (layer, input tensor, output tensor, output level); "v" = volume, "cN" = convN output
 _STEPS = ((0, "v", 0, 0), (1, 0, 1, 1), (2, 1, 2, 1), (3, 2, 3, 2), (4, 3, 4, 2), (5, 4, 5, 3), (6, 5, 6, 3),
           (7, 6, 4, 2), (8, 4, 2, 1), (9, 2, 0, 0))
+# fp32 magnitude slot of each layer's input and output (capi.cpp kLayerSlots): 0 = volume, 1..7 = c0..c6, 8 / 9 = the
+# conv7 / conv9 skip sums; conv11's output feeds the exact-fp32 prob conv (no slot)
+_SLOTS = ((0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (6, 7), (7, 8), (8, 9), (9, None))
+
+
+def _new_slots(eng):
+    """Zeroed magnitude slots of an fp32 engine (None: bf16, or an engine without slots)."""
+    if getattr(eng, "dtype", None) != torch.float32 or not hasattr(eng, "new_slots"):
+        return None
+    return eng.new_slots()
+
+
+def _fold_owned(comm: "Comm", slot, parts):
+    """slot := max |x| over every rank's ``parts`` (the tensor pieces this rank owns; None entries skipped): one
+    all-gather of the per-rank maxima. The slot holds the float's bits in its first word."""
+    dev = slot.device
+    m = torch.zeros(1, dtype=torch.float32, device=dev)
+    for p in parts:
+        if p is not None and p.numel():
+            m = torch.maximum(m, p.abs().amax().reshape(1).float())
+    bits = m.view(torch.int32)
+    got = comm.all_gather(bits)
+    slot.zero_()
+    slot[:1].copy_(torch.stack([g.to(dev) for g in got]).amax(0))
 
 
 def slab_rows(h: int, P: int):
@@ -240,20 +270,28 @@ def _halo_start(comm: Comm, t: torch.Tensor, hl: int):
     return finish
 
 
-def _costreg_sharded(comm: Comm, eng, vol, c, D: int, R: int, w: int):
+def _costreg_sharded(comm: Comm, eng, vol, c, D: int, R: int, w: int, slots=None, rows: int = 0):
     """The U-Net on the haloed slab with each layer's halo exchange overlapped: the batch runs as two halves, and
     a half's halo transfer is in flight while the other half's layer computes (the next layer of a half waits
-    only for that half's halos). Same kernels per voxel as one whole-batch launch: identical results."""
+    only for that half's halos). Same kernels per voxel as one whole-batch launch: identical results. fp32
+    (``slots``): after a layer, its output's magnitude over every rank's owned rows (``rows`` at level 0) sets the
+    slot the next layer reads."""
     B = vol.shape[0]
     halves = [(0, B // 2), (B // 2, B)] if B >= 2 else [(0, B)]
     pending = [None] * len(halves)
-    for layer, src, dst, level in _STEPS:
+    for (layer, src, dst, level), (sin, sout) in zip(_STEPS, _SLOTS):
         for i, (b0, b1) in enumerate(halves):
             if pending[i] is not None:
                 pending[i]()  # this half's halos of the previous layer's output
             x = vol if src == "v" else c[src]
-            eng.unet_layer(layer, D, R, w, x[b0:b1], c[dst][b0:b1])
+            if slots is None:
+                eng.unet_layer(layer, D, R, w, x[b0:b1], c[dst][b0:b1])
+            else:
+                eng.unet_layer(layer, D, R, w, x[b0:b1], c[dst][b0:b1], in_slot=slots[sin])
             pending[i] = _halo_start(comm, c[dst][b0:b1], HALO >> level)
+        if slots is not None and sout is not None:
+            hl = HALO >> level
+            _fold_owned(comm, slots[sout], [c[dst][:, :, hl:hl + (rows >> level)]])
     for fin in pending:
         fin()
 
@@ -283,6 +321,7 @@ def sharded_stage(comm: Comm, eng, feats, layout, rt, hyps, h: int, w: int, warp
     top = lo - (y0 - HALO)                          # ... start at this slab row
     n = hi - lo
 
+    slots = _new_slots(eng)
     hyps_s = torch.empty(B, D, R, w, device=dev, dtype=hyps.dtype)
     hyps_s[:, :, :top].zero_()
     hyps_s[:, :, top + n:].zero_()
@@ -294,12 +333,16 @@ def sharded_stage(comm: Comm, eng, feats, layout, rt, hyps, h: int, w: int, warp
     hook("warp")
     if warp == "rows":
         eng.warp_aggregate_rows(feats, rt, hyps_s, h, lo, n, top, vol, layout=layout)
+        if slots is not None:  # the rows this rank computed (halo rows too: exact volume rows)
+            _fold_owned(comm, slots[0], [vol[:, :, top:top + n]])
     else:
         ds = depth_planes(D, P)
         d0, d1 = ds[r], ds[r + 1]
         part = None
         if d1 > d0:
             part = eng.warp_aggregate(feats, None, hyps[:, d0:d1].contiguous(), rt=rt, layout=layout)
+        if slots is not None:  # this rank's depth planes
+            _fold_owned(comm, slots[0], [part])
         hook("all_to_all")
         ops, recvs = [], []
         for q in range(P):
@@ -316,7 +359,7 @@ def sharded_stage(comm: Comm, eng, feats, layout, rt, hyps, h: int, w: int, warp
 
     hook("costreg")
     c = eng.unet_buffers(B, D, R, w)
-    _costreg_sharded(comm, eng, vol, c, D, R, w)
+    _costreg_sharded(comm, eng, vol, c, D, R, w, slots, y1 - y0)
 
     hook("regress")
     depth, conf, var, prob = eng.regress_c0(c[0], hyps_s, want_prob=want_prob)
@@ -360,8 +403,15 @@ def _gathered_stage(comm: Comm, eng, feats, layout, rt, hyps, h: int, w: int, wa
     del got, mine
     hook("costreg")
     c = eng.unet_buffers(B, D, h, w)
-    for layer, src, dst, _level in _STEPS:
-        eng.unet_layer(layer, D, h, w, vol if src == "v" else c[src], c[dst])
+    slots = _new_slots(eng)
+    if slots is None:
+        for layer, src, dst, _level in _STEPS:
+            eng.unet_layer(layer, D, h, w, vol if src == "v" else c[src], c[dst])
+    else:  # every rank holds the whole volume: the kernels' own magnitude records are the whole tensors'
+        eng.tensor_amax(vol, slots[0])
+        for (layer, src, dst, _level), (sin, sout) in zip(_STEPS, _SLOTS):
+            eng.unet_layer(layer, D, h, w, vol if src == "v" else c[src], c[dst], in_slot=slots[sin],
+                           out_slot=None if sout is None else slots[sout])
     hook("regress")
     depth, conf, var, prob = eng.regress_c0(c[0], hyps, want_prob=want_prob)
     hook("end")

@@ -464,10 +464,11 @@ def test_depthnet_errors():
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_depthnet_range_status(dtype):
-    """The fp32 path's split-f16 products hold |x| < 65520 only (damvs_device.h mma_split32): features scaled so that
-    (ref - warp)^2 exceeds 65504 must raise DamvsRangeError (DAMVS_E_RANGE from damvs_stage_status), never return NaN
-    or finite-but-wrong maps. bf16 storage has the fp32 range: the same inputs give finite maps. The same features at
-    scale 1 pass on both paths, and a NaN input raises on both (ReLU keeps NaN, as torch.relu does)."""
+    """Range status (damvs_stage_status -> DamvsRangeError): non-finite inputs (NaN, inf) raise on both paths (ReLU
+    keeps NaN, as torch.relu does), and a good forward passes afterwards. Features scaled so that (ref - warp)^2
+    exceeds the f16 range (65504) no longer raise on the fp32 path: its split-f16 products run on per-tensor prescaled
+    activations since round 6 (damvs_device.h prescale_of; test_fp32_prescale_feature_scale_sweep checks them against
+    the oracle); bf16 storage has the fp32 range anyway."""
     from damvsnet_amd.cascade import CascadeMVSNet
     from damvsnet_amd._capi import DamvsRangeError
     net = CascadeMVSNet(ndepths=[48, 32, 8], compute_dtype=dtype)
@@ -480,17 +481,71 @@ def test_depthnet_range_status(dtype):
         assert torch.isfinite(out["depth"]).all()
         big = [f * 1000.0 for f in feats]
         assert max(float((big[0] - f).abs().max()) for f in big[1:]) ** 2 > 65504.0
-        if dtype == torch.float32:
-            with pytest.raises(DamvsRangeError, match="DAMVS_E_RANGE"):
-                run(big)
-        else:
-            assert torch.isfinite(run(big)["depth"]).all()
+        assert torch.isfinite(run(big)["depth"]).all()
         nan = [f.clone() for f in feats]
         nan[1][0, :, 100:104, 150:154] = float("nan")
-        with pytest.raises(DamvsRangeError):
+        with pytest.raises(DamvsRangeError, match="DAMVS_E_RANGE"):
             run(nan)
+        inf = [f.clone() for f in feats]
+        inf[0][0, :, 10:12, 20:22] = float("inf")
+        with pytest.raises(DamvsRangeError):
+            run(inf)
         out2 = run(feats)  # the status was read and cleared: a good forward passes again
         assert torch.equal(out2["depth"], out["depth"])
+
+
+# (stage, h, w, D, N): cfgB's three stages (640x512, 5 views, 48/32/8) and cfgC's stage 2 (592x800) at full size
+_SWEEP_CASES = [(0, 128, 160, 48, 5), (1, 256, 320, 32, 5), (2, 512, 640, 8, 5), (1, 592, 800, 32, 5)]
+
+
+@pytest.mark.parametrize("scale", [1e-3, 1e-2, 1e2, 1e3])
+@pytest.mark.parametrize("case", range(4), ids=["cfgB-s1", "cfgB-s2", "cfgB-s3", "cfgC-s2"])
+def test_fp32_prescale_feature_scale_sweep(case, scale):
+    """The fp32 path holds parity whatever the activation scale: the stage's features scaled by
+    1e-3 .. 1e3 put the cost volume ((ref - warp)^2, models/cas_mvsnet.py:64-76) at 1e-6 .. 1e6 of its usual
+    magnitude -- far under the f16 normal range, where unscaled split-f16 pieces lose their low bits, or far over
+    65504, where they overflow. With per-tensor prescaling (damvs_device.h prescale_of) the HIP depth is compared with
+    the oracle (oracle/mvs_oracle.py) run in float64 on identical inputs: every well-conditioned pixel (> 99 % of
+    them) holds the north-star 1e-3. Large scales sharpen the softmax over the depth planes into an argmax (logits
+    ~1e9 at x100), so a pixel whose two best planes' logits are closer than the arithmetic's error jumps between them
+    on any last-bit difference: the reference's own fp32 at cfgB stage 1 x100 / x1000 differs from float64 by up to
+    1.6e-3 / 3.0e-2 (measured on the oracle). Such pixels are excluded by their float64 logit margin (< 16x the
+    reference's own fp32 logit error at the pixel), not by the HIP result."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    s, h, w, D, N = _SWEEP_CASES[case]
+    if case == 3 and scale not in (1e-3, 1e3):
+        pytest.skip("full size: the two extreme scales")
+    C = (32, 16, 8)[s]
+    sd = model_state("depthnet_cfgA_adaptive")
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(sd, strict=True)
+    net = net.to(DEV).eval()
+    feats, P, hyps = depthnet_inputs(B=1, N=N, H=h, W=w, D=D, stage_idx=s, C=C)
+    feats = [f * scale for f in feats]
+    sd64 = {k: (v.double() if torch.is_floating_point(v) else v) for k, v in sd.items()}
+    cr = "cost_regularization.%d" % s
+    with torch.no_grad():
+        out = net.DepthNet(s, [cuda(f) for f in feats], cuda(P), cuda(hyps), D, net.cost_regularization[s])
+        l32 = O.costregnet(O.aggregate(feats, P, hyps, sd, s), sd, cr).squeeze(1)
+        l64 = O.costregnet(O.aggregate([f.double() for f in feats], P.double(), hyps.double(), sd64, s), sd64,
+                           cr).squeeze(1)
+        r32 = O.regression(l32, hyps)["depth"].double().numpy()
+        r64 = O.regression(l64, hyps.double())["depth"].numpy()
+    d = np_(out["depth"])
+    assert np.isfinite(d).all()
+    err, cond = pixel_rel(d, r64), pixel_rel(r32, r64)
+    # a pixel is ill-conditioned when its two largest float64 logits are closer than 16x the reference's own fp32
+    # logit error there: at large scales the softmax is an argmax, and such a pixel's depth jumps between two planes
+    # on any last-bit difference
+    top2 = torch.topk(l64, 2, dim=1).values
+    margin = (top2[:, 0] - top2[:, 1]).numpy()
+    lerr = (l32.double() - l64).abs().amax(1).numpy()
+    good = margin > 16 * lerr
+    print("prescale sweep %s x%g: HIP vs fp64 max %.3e mean %.3e (well-conditioned %.5f of pixels: max %.3e) | "
+          "reference fp32 vs fp64 max %.3e mean %.3e | |logit| max %.3g" % (
+              ("cfgB-s1", "cfgB-s2", "cfgB-s3", "cfgC-s2")[case], scale, err.max(), err.mean(), good.mean(),
+              err[good].max(), cond.max(), cond.mean(), float(l64.abs().max())))
+    assert good.mean() > 0.99 and err[good].max() < 1e-3, (good.mean(), err[good].max())
 
 
 def test_cascade_range_status_fp32():
@@ -778,8 +833,8 @@ def test_conv0_reuse_fp32_bitwise(s, D, H, W, monkeypatch):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("s,D,H,W,shape", [(0, 48, 40, 72, "4,1"), (0, 20, 36, 88, "4,1"), (1, 24, 40, 72, "4,1"),
-                                             (1, 32, 44, 80, "2,1"), (2, 8, 48, 96, "4,2"), (2, 8, 44, 80, "4,1"),
+@pytest.mark.parametrize("s,D,H,W,shape", [(0, 48, 40, 72, "4,1"), (0, 24, 32, 88, "4,1"), (1, 24, 40, 72, "4,1"),
+                                             (1, 32, 48, 80, "2,1"), (2, 8, 48, 96, "4,2"), (2, 8, 40, 88, "4,1"),
                                              (2, 16, 40, 72, "2,2"), (2, 8, 40, 72, "2,1")])
 def test_conv0_dz_fp32_bitwise(s, D, H, W, shape, monkeypatch):
     """fp32 conv0 with the kernel depths on different waves (conv0_dz_kernel, partial sums chained through LDS in the
@@ -799,6 +854,42 @@ def test_conv0_dz_fp32_bitwise(s, D, H, W, shape, monkeypatch):
     monkeypatch.setenv("DAMVS_CONV0_DZ", "0")
     monkeypatch.setenv("DAMVS_CONV0_REUSE", "1")
     b = eng.costreg_logits(vol).clone()
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("s", [0, 1, 2])
+def test_warp_corner_reuse_bitwise(s, dtype, monkeypatch):
+    """The split warp with per-view corner reuse (DAMVS_WARP_REUSE=1: a lane reloads a view's 4 corner records only when
+    its bilinear cell changed from the previous plane) against the plain pipeline: the same records and arithmetic,
+    bitwise, at N = 5 for the three stage shapes on refined per-pixel hypotheses (the pipeline's, where consecutive
+    planes sample nearby points of each epipolar line) and on stage-1 linear ones."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    from damvsnet_amd.engine import hypotheses, proj_prepare
+    from damvsnet_amd import synth
+    net = CascadeMVSNet(ndepths=[48, 32, 8], compute_dtype=dtype)
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    net = net.to(DEV).eval()
+    B, N, H, W = 2, 5, 256, 320
+    C, D, scale = {0: (32, 48, 4), 1: (16, 32, 2), 2: (8, 8, 1)}[s]
+    h, w = H // scale, W // scale
+    proj, _, dv = synth.cameras(B, N, H, W)
+    P = cuda(torch.from_numpy(proj["stage%d" % (s + 1)]))
+    g = torch.Generator(device=DEV).manual_seed(1)
+    if s == 0:
+        hyps = hypotheses(cuda(torch.from_numpy(dv)), D, H, W, scale)
+    else:
+        pd = 600 + 100 * torch.rand(B, H // (2 * scale), W // (2 * scale), device=DEV, generator=g)
+        pv = 2 + 20 * torch.rand(B, H // (2 * scale), W // (2 * scale), device=DEV, generator=g)
+        hyps = hypotheses(cuda(torch.from_numpy(dv)), D, H, W, scale, pd, pv)
+    feats = [torch.randn(B, h, w, C, generator=g, device=DEV).to(dtype) for _ in range(N)]
+    eng = net.DepthNet.engine(s, net.cost_regularization[s], torch.device(DEV))
+    rt = proj_prepare(P)
+    with torch.no_grad():
+        monkeypatch.setenv("DAMVS_WARP_REUSE", "1")
+        a = eng.warp_aggregate(feats, P, hyps, rt=rt).clone()
+        monkeypatch.setenv("DAMVS_WARP_REUSE", "0")
+        b = eng.warp_aggregate(feats, P, hyps, rt=rt).clone()
     assert torch.equal(a, b)
 
 
