@@ -34,6 +34,13 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-I" + INCLUDE
 # ops (v_pk_fma/mul/add_f32): with those, the warp kernels' lanes 48-63 computed wrong tap coordinates while MFMA
 # kernels of another stream shared the CU (DESIGN.md §4 "Concurrent streams"; profiles/r05/diag_streams/r05w).
 FILE_FLAGS = {"k_warp.hip": ["-fno-slp-vectorize"]}
+# Round 6 widened the rule to every kernel without MFMA instructions that can share a CU with another stream's MFMA
+# kernels (tests/test_isa_pins.py test_valu_kernels_carry_no_packed_fp32_ops): the plane-input conv2d layers
+# (k_planes.hip), the hypotheses / GeoFF depth pyramid / camera algebra (k_geometry.hip), the VALU prob conv,
+# regression, range check and magnitude kernels (k_regress.hip) and depth fusion (k_fusion.hip).
+# Both vectorizers are off there: the loop vectorizer, too, emits packed-FP32 ops (grid-stride loops by two).
+for _f in ("k_planes.hip", "k_geometry.hip", "k_regress.hip", "k_fusion.hip"):
+    FILE_FLAGS[_f] = ["-fno-slp-vectorize", "-fno-vectorize"]
 
 
 def sources():

@@ -160,7 +160,9 @@ hipError_t launch_block_channels(hipStream_t s, int store, const FeatPtrs& src, 
                                  int hw, int C);
 hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a);
 hipError_t launch_conv2d(hipStream_t s, int store, const Conv2dArgs& a);
-bool conv2d_wide_shape_ok(const Conv2dArgs& a);  // the wide kernel takes the layer (given 32-K phase data)
+bool conv2d_wide_shape_ok(const Conv2dArgs& a);
+// layers whose only inputs are fp32 planes (c0 = c1 = 0), on the VALU (k_planes.hip)
+hipError_t launch_conv2d_planes(hipStream_t s, int store, const Conv2dArgs& a);  // the wide kernel takes the layer (given 32-K phase data)
 struct BorderArgs {
   float corr[9 * 16];  // [tap][channel] of a 3x3 conv, channels < 16
 };

@@ -13,38 +13,13 @@
 
 #include <type_traits>
 
-#include "damvs_device.h"
+#include "conv2d_common.h"
 
 namespace damvs {
 
 namespace {
 
 template <typename T> using Frag2 = MmaFrag<T>;
-
-template <typename T>
-__device__ __forceinline__ void ld4(const T* p, float* r);
-template <>
-__device__ __forceinline__ void ld4<float>(const float* p, float* r) {
-  float4 v = *reinterpret_cast<const float4*>(p);
-  r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
-}
-template <>
-__device__ __forceinline__ void ld4<bf16_t>(const bf16_t* p, float* r) {
-  uint2 v = *reinterpret_cast<const uint2*>(p);
-  r[0] = __uint_as_float(v.x << 16); r[1] = __uint_as_float(v.x & 0xffff0000u);
-  r[2] = __uint_as_float(v.y << 16); r[3] = __uint_as_float(v.y & 0xffff0000u);
-}
-template <typename T>
-__device__ __forceinline__ void st4(T* p, const float* r);
-template <>
-__device__ __forceinline__ void st4<float>(float* p, const float* r) {
-  *reinterpret_cast<float4*>(p) = make_float4(r[0], r[1], r[2], r[3]);
-}
-template <>
-__device__ __forceinline__ void st4<bf16_t>(bf16_t* p, const float* r) {
-  *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)f2bf(r[0]) | ((uint32_t)f2bf(r[1]) << 16),
-                                            (uint32_t)f2bf(r[2]) | ((uint32_t)f2bf(r[3]) << 16));
-}
 
 template <typename T> struct T_is_bf16 { static constexpr bool value = false; };
 template <> struct T_is_bf16<bf16_t> { static constexpr bool value = true; };
@@ -56,32 +31,6 @@ template <> __device__ __forceinline__ float4 pack_vals<float>(const float* v) {
 template <> __device__ __forceinline__ uint4 pack_vals<bf16_t>(const float* v) {
   return make_uint4((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16), (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16),
                     (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16), (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16));
-}
-
-// Residual before ReLU, ReLU, (upsampled) residual after ReLU, store of 4 channels (32-bit indices:
-// the launcher keeps every operand below 2^31 elements).
-template <typename T>
-__device__ __forceinline__ void tail4(const Conv2dArgs& a, int b, int oy, int ox, int co, float* r) {
-  const uint32_t ob = (uint32_t)(((b * a.Ho + oy) * a.Wo + ox) * a.cout + co);
-  if (a.res_pre) {
-    float q[4];
-    ld4<T>(reinterpret_cast<const T*>(a.res_pre) + ob, q);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] += q[i];
-  }
-  if (a.relu) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = relu(r[i]);
-  }
-  if (a.res_post) {
-    const int up = a.post_up;  // 1, or 2 for a nearest-x2 upsampled source of half resolution
-    const uint32_t pb = (uint32_t)(((b * (a.Ho / up) + oy / up) * (a.Wo / up) + ox / up) * a.cout + co);
-    float q[4];
-    ld4<T>(reinterpret_cast<const T*>(a.res_post) + pb, q);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] += q[i];
-  }
-  st4<T>(reinterpret_cast<T*>(a.out) + ob, r);
 }
 
 // Implicit-GEMM conv on MFMA. A wave owns 64 output pixels (kG2 groups of 16) x MT 16-channel
@@ -1620,245 +1569,6 @@ hipError_t launch_lds2(hipStream_t s, const Conv2dArgs& a, bool dry = false) {
   }
 }
 
-// Direct conv for layers whose only inputs are fp32 planes (c0 = c1 = 0: FeatureNet's RGB conv
-// 3x3 3->8, GeoFeatureFusion's RGB+depth 5x5 4->8 and depth+depth 5x5 2->8 init convs). The MFMA
-// kernel would run these in its epilogue with half the lanes idle and one dependent load chain per
-// tap. Here (stride 1, padding K/2) one thread computes 2 vertically adjacent output pixels x all
-// COUT channels: the K+1 input rows they need are loaded row by row (K*NG branch-free coalesced
-// loads in flight per row, each row feeding both pixels); weights sit in LDS as wave-uniform
-// broadcast reads.
-template <typename T, int COUT, int K, int NG>
-__global__ __launch_bounds__(256) void conv2d_planes_kernel(const Conv2dArgs a, const float* __restrict__ wg) {
-  typedef float f32x2_t __attribute__((ext_vector_type(2)));
-  constexpr int P = K / 2;
-  const int Hp = (a.Ho + 1) / 2;
-  const int Qtot = a.B * Hp * a.Wo;  // host checks it fits in int
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= Qtot) return;
-  const int ox = q % a.Wo;
-  const int oy0 = (q / a.Wo) % Hp * 2;
-  const int b = q / (a.Wo * Hp);
-  // Weights are wave-uniform: scalar loads (restrict const argument) feed packed FMAs over channel
-  // pairs, (c, c+1) per v_pk_fma_f32 with one weight pair from SGPRs (per lane the same fused
-  // multiply-adds as the scalar form). Input row r feeds pixel 0 with kernel row r (r < K) and
-  // pixel 1 with kernel row r-1 (r > 0).
-  f32x2_t acc0[COUT / 2], acc1[COUT / 2];
-#pragma unroll
-  for (int c = 0; c < COUT / 2; ++c) acc0[c] = acc1[c] = (f32x2_t){a.bias[2 * c], a.bias[2 * c + 1]};
-  const float* gp[NG];
-#pragma unroll
-  for (int g = 0; g < NG; ++g) gp[g] = a.geo[g] + (size_t)b * a.geo_bstride[g];
-  const int cp = a.cout_pad;
-#pragma unroll 1  // (fully unrolled: all rows' loads hoisted, 1.2-2.4x slower)
-  for (int r = 0; r <= K; ++r) {
-    const int iy = oy0 - P + r;
-    const bool oky = (unsigned)iy < (unsigned)a.Hi;
-    const int rowoff = (oky ? iy : 0) * a.Wi;
-    float v[K][NG];
-#pragma unroll
-    for (int kx = 0; kx < K; ++kx) {
-      const int ix = ox - P + kx;
-      const bool ok = oky && (unsigned)ix < (unsigned)a.Wi;
-      const int off = rowoff + (ok ? ix : 0);
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        const float x = gp[g][off];  // clamped address, unconditional load
-        v[kx][g] = ok ? x : 0.f;
-      }
-    }
-    auto row = [&](const float* w, f32x2_t* acc) {
-#pragma unroll
-      for (int kx = 0; kx < K; ++kx)
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          const f32x2_t x = {v[kx][g], v[kx][g]};
-          const float* wt = w + (kx * NG + g) * cp;
-#pragma unroll
-          for (int c = 0; c < COUT / 2; ++c)
-            acc[c] = __builtin_elementwise_fma((f32x2_t){wt[2 * c], wt[2 * c + 1]}, x, acc[c]);
-        }
-    };
-    if (r < K) row(wg + (size_t)r * K * NG * cp, acc0);
-    if (r > 0) row(wg + (size_t)(r - 1) * K * NG * cp, acc1);
-  }
-  float o0[COUT], o1[COUT];
-#pragma unroll
-  for (int c = 0; c < COUT / 2; ++c) {
-    o0[2 * c] = acc0[c].x; o0[2 * c + 1] = acc0[c].y;
-    o1[2 * c] = acc1[c].x; o1[2 * c + 1] = acc1[c].y;
-  }
-  const bool two = oy0 + 1 < a.Ho;
-#pragma unroll
-  for (int c0 = 0; c0 < COUT; c0 += 4) {
-    if (c0 >= a.cout) break;
-    tail4<T>(a, b, oy0, ox, c0, o0 + c0);
-    if (two) tail4<T>(a, b, oy0 + 1, ox, c0, o1 + c0);
-  }
-}
-
-// Plane-only layers (as conv2d_planes_kernel) with 4 consecutive output columns x 2 rows per thread: each input row
-// arrives as three aligned 16-byte loads per plane (columns x0 - 4 .. x0 + 7) instead of K scalar loads per pixel
-// column, a quarter of the load instructions for the same fused multiply-adds (same order per output: bitwise the
-// one-column kernel). Needs Wi % 4 == 0 and 16-byte aligned planes (launch_planes checks); COUT 8.
-template <typename T, int COUT, int K, int NG>
-__global__ __launch_bounds__(256) void conv2d_planes4_kernel(const Conv2dArgs a, const float* __restrict__ wg) {
-  typedef float f32x2_t __attribute__((ext_vector_type(2)));
-  constexpr int P = K / 2;
-  const int Hp = (a.Ho + 1) / 2, Wg = a.Wo / 4;
-  const int Qtot = a.B * Hp * Wg;
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= Qtot) return;
-  const int ox0 = (q % Wg) * 4;
-  const int oy0 = (q / Wg) % Hp * 2;
-  const int b = q / (Wg * Hp);
-  f32x2_t acc[2][4][COUT / 2];  // [output row][column][channel pair]
-#pragma unroll
-  for (int c = 0; c < COUT / 2; ++c)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[0][j][c] = acc[1][j][c] = (f32x2_t){a.bias[2 * c], a.bias[2 * c + 1]};
-  __amdgpu_buffer_rsrc_t rg[NG];
-  uint32_t gb[NG];
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    rg[g] = make_rsrc(a.geo[g], ((long long)(a.B - 1) * a.geo_bstride[g] + (long long)a.Hi * a.Wi) * 4);
-    gb[g] = (uint32_t)((long long)b * a.geo_bstride[g]) * 4u;
-  }
-  const int cp = a.cout_pad;
-#pragma unroll 1
-  for (int r = 0; r <= K; ++r) {
-    const int iy = oy0 - P + r;
-    const bool oky = (unsigned)iy < (unsigned)a.Hi;
-    float v[NG][12];  // columns ox0 - 4 .. ox0 + 7
-#pragma unroll
-    for (int g = 0; g < NG; ++g)
-#pragma unroll
-      for (int h = 0; h < 3; ++h) {
-        const int ix = ox0 - 4 + 4 * h;
-        const bool ok = oky && ix >= 0 && ix < a.Wi;  // whole 16-byte groups: Wi % 4 == 0
-        const float4 f = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                        rg[g], ok ? (uint32_t)(iy * a.Wi + ix) * 4u : kOOB, gb[g], 0));
-        v[g][4 * h] = f.x; v[g][4 * h + 1] = f.y; v[g][4 * h + 2] = f.z; v[g][4 * h + 3] = f.w;
-      }
-    auto row = [&](const float* w, f32x2_t (*acc_r)[COUT / 2]) {
-#pragma unroll
-      for (int kx = 0; kx < K; ++kx)
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          const float* wt = w + (kx * NG + g) * cp;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float xv = v[g][4 - P + j + kx];
-            const f32x2_t x = {xv, xv};
-#pragma unroll
-            for (int c = 0; c < COUT / 2; ++c)
-              acc_r[j][c] = __builtin_elementwise_fma((f32x2_t){wt[2 * c], wt[2 * c + 1]}, x, acc_r[j][c]);
-          }
-        }
-    };
-    if (r < K) row(wg + (size_t)r * K * NG * cp, acc[0]);
-    if (r > 0) row(wg + (size_t)(r - 1) * K * NG * cp, acc[1]);
-  }
-  const bool two = oy0 + 1 < a.Ho;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float o0[COUT], o1[COUT];
-#pragma unroll
-    for (int c = 0; c < COUT / 2; ++c) {
-      o0[2 * c] = acc[0][j][c].x; o0[2 * c + 1] = acc[0][j][c].y;
-      o1[2 * c] = acc[1][j][c].x; o1[2 * c + 1] = acc[1][j][c].y;
-    }
-#pragma unroll
-    for (int c0 = 0; c0 < COUT; c0 += 4) {
-      if (c0 >= a.cout) break;
-      tail4<T>(a, b, oy0, ox0 + j, c0, o0 + c0);
-      if (two) tail4<T>(a, b, oy0 + 1, ox0 + j, c0, o1 + c0);
-    }
-  }
-}
-
-// Any other plane-only layer (stride 2, transposed; no production layer): one thread per output
-// pixel of a phase, all (<= 16) output channels.
-template <typename T>
-__global__ __launch_bounds__(256) void conv2d_planes_generic_kernel(const Conv2dArgs a) {
-  const int Qtot = a.B * a.Hq * a.Wq;
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  const Conv2dPhase& ph = a.ph[blockIdx.y];
-  if (q >= Qtot) return;
-  const int qx = q % a.Wq, qy = (q / a.Wq) % a.Hq, b = q / (a.Wq * a.Hq);
-  float acc[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) acc[c] = a.bias[c];
-  const float* wg = a.wgeo + (size_t)ph.g_off * a.cout_pad;
-  for (int t = 0; t < ph.ntaps; ++t) {
-    const int iy = qy * a.in_stride + ph.tap[t][0], ix = qx * a.in_stride + ph.tap[t][1];
-    if ((unsigned)iy >= (unsigned)a.Hi || (unsigned)ix >= (unsigned)a.Wi) continue;
-    for (int g = 0; g < a.ngeo; ++g) {
-      const float v = a.geo[g][b * a.geo_bstride[g] + iy * a.Wi + ix];
-      const float* w = wg + (t * a.ngeo + g) * a.cout_pad;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) acc[c] += w[c] * v;
-    }
-  }
-  const int oy = qy * a.out_stride + ph.py, ox = qx * a.out_stride + ph.px;
-  for (int c0 = 0; c0 < a.cout; c0 += 4) tail4<T>(a, b, oy, ox, c0, acc + c0);
-}
-
-// True when the layer is a plain (non-transposed) KxK conv with padding K/2 and dense row-major taps.
-bool planes_fast_ok(const Conv2dArgs& a, int K) {
-  if (a.nphase != 1 || a.out_stride != 1 || a.in_stride != 1 || (long long)a.B * a.Ho * a.Wo >= (1LL << 31) || a.ph[0].ntaps != K * K || a.ph[0].g_off != 0) return false;
-  for (int t = 0; t < K * K; ++t)
-    if (a.ph[0].tap[t][0] != t / K - K / 2 || a.ph[0].tap[t][1] != t % K - K / 2) return false;
-  return true;
-}
-
-template <typename T, int K>
-hipError_t launch_planes4_k(hipStream_t st, const Conv2dArgs& a) {
-  const long long Qtot = (long long)a.B * ((a.Ho + 1) / 2) * (a.Wo / 4);
-  dim3 grid((unsigned)((Qtot + 255) / 256));
-  switch (a.ngeo) {
-    case 1: hipLaunchKernelGGL((conv2d_planes4_kernel<T, 8, K, 1>), grid, dim3(256), 0, st, a, a.wgeo); break;
-    case 2: hipLaunchKernelGGL((conv2d_planes4_kernel<T, 8, K, 2>), grid, dim3(256), 0, st, a, a.wgeo); break;
-    case 3: hipLaunchKernelGGL((conv2d_planes4_kernel<T, 8, K, 3>), grid, dim3(256), 0, st, a, a.wgeo); break;
-    default: hipLaunchKernelGGL((conv2d_planes4_kernel<T, 8, K, 4>), grid, dim3(256), 0, st, a, a.wgeo); break;
-  }
-  return hipGetLastError();
-}
-
-// conv2d_planes4_kernel's conditions: 4-column groups of whole 16-byte plane pieces (DAMVS_PLANES4=0, read per call:
-// the one-column kernel)
-bool planes4_ok(const Conv2dArgs& a) {
-  const char* v = getenv("DAMVS_PLANES4");
-  if ((v && v[0] == '0') || a.cout > 8 || a.Wi % 4 || a.Wo != a.Wi) return false;
-  for (int g = 0; g < a.ngeo; ++g)
-    if (reinterpret_cast<uintptr_t>(a.geo[g]) % 16 || a.geo_bstride[g] % 4) return false;
-  return true;
-}
-
-template <typename T, int COUT, int K>
-hipError_t launch_planes_k(hipStream_t st, const Conv2dArgs& a) {
-  const long long Qtot = (long long)a.B * ((a.Ho + 1) / 2) * a.Wo;
-  dim3 grid((unsigned)((Qtot + 255) / 256));
-  switch (a.ngeo) {
-    case 1: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 1>), grid, dim3(256), 0, st, a, a.wgeo); break;
-    case 2: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 2>), grid, dim3(256), 0, st, a, a.wgeo); break;
-    case 3: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 3>), grid, dim3(256), 0, st, a, a.wgeo); break;
-    default: hipLaunchKernelGGL((conv2d_planes_kernel<T, COUT, K, 4>), grid, dim3(256), 0, st, a, a.wgeo); break;
-  }
-  return hipGetLastError();
-}
-
-// Returns hipErrorNotSupported when the layer is not of the fast form (caller uses the MFMA kernel).
-template <typename T>
-hipError_t launch_planes(hipStream_t st, const Conv2dArgs& a) {
-  const int K = a.ph[0].ntaps == 9 ? 3 : a.ph[0].ntaps == 25 ? 5 : 0;
-  if (K == 0 || a.ngeo < 1 || a.ngeo > 4 || a.cout > 16 || a.cout_pad < 16 || !planes_fast_ok(a, K))
-    return hipErrorNotSupported;
-  // 5x5 only: GeoFF stage-3 init convs 5.21-5.28 against 5.30-5.43 ms; at 3x3 (FeatureNet's RGB conv, half of each
-  // 12-column window unused, a quarter of the threads) features 2.86-2.89 against 2.77 ms (profiles/r03/ab_planes4.jsonl)
-  if (K == 5 && planes4_ok(a)) return launch_planes4_k<T, 5>(st, a);
-  if (a.cout <= 8) return K == 3 ? launch_planes_k<T, 8, 3>(st, a) : launch_planes_k<T, 8, 5>(st, a);
-  return K == 3 ? launch_planes_k<T, 16, 3>(st, a) : launch_planes_k<T, 16, 5>(st, a);
-}
 
 template <typename T, int MT, bool K32 = false>
 hipError_t launch_mt(hipStream_t s, const Conv2dArgs& a) {
@@ -1906,14 +1616,7 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
     return hipErrorInvalidValue;
   for (int g = 0; g < a.ngeo; ++g)
     if (((long long)(a.B - 1) * a.geo_bstride[g] + npix / a.B) * 4 >= lim) return hipErrorInvalidValue;
-  if (a.c0 + a.c1 == 0) {
-    const hipError_t e = launch_planes<T>(s, a);
-    if (e != hipErrorNotSupported) return e;
-    if (a.cout > 16 || a.cout_pad < 16) return hipErrorInvalidValue;
-    dim3 grid((unsigned)((a.B * a.Hq * a.Wq + 255) / 256), a.nphase);
-    hipLaunchKernelGGL(conv2d_planes_generic_kernel<T>, grid, dim3(256), 0, s, a);
-    return hipGetLastError();
-  }
+  if (a.c0 + a.c1 == 0) return launch_conv2d_planes(s, sizeof(T) == 2 ? ST_BF16 : ST_F32, a);  // k_planes.hip
   if (a.ngeo > 1) return hipErrorInvalidValue;  // the MFMA path takes at most one plane
   if (a.wide32) {  // fp32 layer with its 32-K split packing: the wide kernel, else the narrow halo kernel, else (unless
                    // the thin-layer LDS kernel takes it on the 16-K packing) the 32-K gather kernel, else

@@ -1180,13 +1180,18 @@ hipError_t launch_dz_t(hipStream_t s, const ConvArgs& a) {
   return hipGetLastError();
 }
 
-// DAMVS_CONV0_DZ (read per call): "0" = off (the input-plane walk / output-plane walk as DAMVS_CONV0_REUSE says), else
-// "RP,TXG" overrides the default block shape of conv0_dz_kernel
+// DAMVS_CONV0_DZ (read per call): "0" = off (the input-plane walk / output-plane walk as DAMVS_CONV0_REUSE says), "1"
+// or "RP,TXG" = on at every CIN (RP,TXG: the block shape); unset: on at CIN 32 only. Measured at cfgC B = 4
+// (tools/unet_layers.py, profiles/r06/layers_conv0_dz_r06e.txt): stage 1 (CIN 32) 1.787 -> 1.665 ms; stage 2 (CIN 16)
+// 2.074 -> 2.614 ms and stage 3 (CIN 8) 1.304 -> 1.577 ms slower -- with one accumulator chain per wave (TXG 1) each
+// B fragment's three split MFMAs depend on each other, where the walk interleaves three depths' accumulators; at CIN 32
+// the three waves per SIMD (against one) cover that latency.
 bool conv0_dz_shape(int CIN, int& rp, int& txg) {
   const char* v = getenv("DAMVS_CONV0_DZ");
   rp = 4;
   txg = CIN == 8 ? 2 : 1;
-  if (!v || !v[0]) return true;  // unset or empty: the default shape
+  if (!v || !v[0]) return CIN == 32;  // unset or empty: the default
+  if (v[0] == '1' && !v[1]) return true;
   if (v[0] == '0') return false;
   const char* c = strchr(v, ',');
   rp = atoi(v);

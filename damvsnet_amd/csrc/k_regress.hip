@@ -109,8 +109,9 @@ __global__ __launch_bounds__(256) void regress_kernel(int B, int D, int hw, cons
 // barrier per plane, next plane's global loads issued before this plane's FMAs; bf16 is widened once
 // per voxel at staging, not once per tap), every thread slides its 3x3x3 window over the planes keeping
 // the two open logits in registers, completed logits go to an LDS column [D][256] and the regression
-// runs from there. Logits never reach HBM. The channel sums run as packed fp32 FMAs (even / odd channel
-// partial sums, added at the end of the plane) with the 72 weights of one kernel row as scalar operands
+// runs from there. Logits never reach HBM. The channel sums run as fp32 FMAs (even / odd channel partial sums, added
+// at the end of the plane; packed FMAs until round 6, the same operations) with the 72 weights of one kernel row as
+// scalar operands
 // (the ky loop is not unrolled: all 216 weights at once would spill to VGPR lanes).
 constexpr int kTY = 8, kTX = 32, kHY = kTY + 2, kHX = kTX + 2;
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
@@ -187,7 +188,8 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
   for (int pl = 0; pl < D; ++pl) {
     if (pl + 1 < D) gload(pl + 1);
     const float4* tb = tile + (pl & 1) * FQ * NVOX + ty * kHX + tx;
-    f32x2_t c0 = {0.f, 0.f}, c1 = {0.f, 0.f}, c2 = {0.f, 0.f};
+    // even / odd channel partial sums per kernel depth (scalar FMAs: k_regress.hip is built without packed-FP32 ops)
+    float c0e = 0.f, c0o = 0.f, c1e = 0.f, c1o = 0.f, c2e = 0.f, c2o = 0.f;
 #pragma unroll 1
     for (int ky = 0; ky < 3; ++ky) {
       // wave-uniform weights through the scalar cache (SGPR operands), one kernel row per iteration
@@ -205,14 +207,16 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
         const float* w2 = wr + 18 * CB + kx * CB; // dz = 2
 #pragma unroll
         for (int c = 0; c < CB; c += 2) {
-          const f32x2_t x = {v[c], v[c + 1]};
-          c0 += (f32x2_t){w0[c], w0[c + 1]} * x;
-          c1 += (f32x2_t){w1[c], w1[c + 1]} * x;
-          c2 += (f32x2_t){w2[c], w2[c + 1]} * x;
+          c0e += w0[c] * v[c];
+          c0o += w0[c + 1] * v[c + 1];
+          c1e += w1[c] * v[c];
+          c1o += w1[c + 1] * v[c + 1];
+          c2e += w2[c] * v[c];
+          c2o += w2[c + 1] * v[c + 1];
         }
       }
     }
-    const float s0 = c0.x + c0.y, s1 = c1.x + c1.y, s2 = c2.x + c2.y;
+    const float s0 = c0e + c0o, s1 = c1e + c1o, s2 = c2e + c2o;
     if (TWO) {
       const int y = y0 + ty, x = x0 + tx;
       if (pl >= 1 && y < h && x < w) {

@@ -51,7 +51,6 @@ template <> struct Rec16<bf16_t> {
 struct Taps {
   uint32_t off[4];
   float wt[4];
-  int key;  // the nw corner (x0, y0): equal keys have equal corner records
 };
 __device__ __forceinline__ Taps bilinear_taps(int h, int w, uint32_t rec, float ix, float iy) {
   const bool inside = ix > -2.f && ix < (float)w + 1.f && iy > -2.f && iy < (float)h + 1.f;  // false for NaN
@@ -61,7 +60,6 @@ __device__ __forceinline__ Taps bilinear_taps(int h, int w, uint32_t rec, float 
   const float wx1 = cx - x0f, wx0 = (x0f + 1.f) - cx;
   const float wy1 = cy - y0f, wy0 = (y0f + 1.f) - cy;
   Taps t;
-  t.key = (y0 << 16) ^ (x0 & 0xffff);
   t.wt[0] = wx0 * wy0;
   t.wt[1] = wx1 * wy0;
   t.wt[2] = wx0 * wy1;
@@ -354,7 +352,7 @@ __device__ __forceinline__ float swz_xor4(float v) {
   return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x101F));  // and 0x1F, xor 4 (no LDS memory)
 }
 
-template <typename T, int C, int MODE, int NVC, bool RU = false>
+template <typename T, int C, int MODE, int NVC>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, kWarpBlock))) void warp_split_kernel(const WarpArgs a, const float* __restrict__ cams,
                                                                 int npix_blocks, int dchunk, int ndchunks) {
   constexpr int E = Stor<T>::E;  // channels per 16-byte chunk
@@ -511,46 +509,19 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, kWarpBlock))) void warp
 #pragma unroll
     for (int k = 0; k < 4; ++k) wt[k] = t.wt[k];
   };
-  // RU (corner reuse, NVC > 0): consecutive planes of one pixel sample nearby points of each view's epipolar line and
-  // often fall in the same bilinear cell (same nw corner); each view keeps its last sample's 4 corner records and
-  // their key, and a lane loads only when its cell changed (EXEC-masked loads: a wave whose lanes all stay in their
-  // cells issues none). Same records, same arithmetic: bitwise the plain pipeline.
-  constexpr int NR = RU ? NH : 1;
-  uint4 rc[NR][4];
-  int key[NR];
-#pragma unroll
-  for (int v = 0; v < NR; ++v) key[v] = (int)0x80000000;
-  auto issue_ru = [&](int v, const Taps& t, float* wt) {
-    if (t.key != key[v]) {
-      key[v] = t.key;
-      const __amdgpu_buffer_rsrc_t r = rs[v];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        rc[v][k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, t.off[k] + qoff, sb, 0));
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) wt[k] = t.wt[k];
-  };
   uint4 ra[4], rb[4];
   float wa[4], wb[4];
   float hyp = a.hyps[vox_of(d0)];
   float hyp_n = a.hyps[vox_of(min(d0 + 1, d1 - 1))];
-  if constexpr (RU) issue_ru(0, taps(0, hyp), wa);
-  else issue(0, taps(0, hyp), ra, wa);
+  issue(0, taps(0, hyp), ra, wa);
   for (int d = d0; d < d1; ++d) {
     const float hyp_nn = a.hyps[vox_of(min(d + 2, d1 - 1))];
     float acc[E], sq[E];
     init(acc, sq);
     auto step = [&](int v, const uint4* cur, const float* wcur, uint4* nxt, float* wnxt) {
-      if constexpr (RU) {
-        if (v + 1 < nv) issue_ru(v + 1, taps(v + 1, hyp), wnxt);
-        else issue_ru(0, taps(0, hyp_n), wnxt);
-        reduce(rc[v], wcur, acc, sq);
-      } else {
-        if (v + 1 < nv) issue(v + 1, taps(v + 1, hyp), nxt, wnxt);
-        else issue(0, taps(0, hyp_n), nxt, wnxt);
-        reduce(cur, wcur, acc, sq);
-      }
+      if (v + 1 < nv) issue(v + 1, taps(v + 1, hyp), nxt, wnxt);
+      else issue(0, taps(0, hyp_n), nxt, wnxt);
+      reduce(cur, wcur, acc, sq);
     };
     if constexpr (NVC > 0) {
 #pragma unroll
@@ -591,12 +562,6 @@ bool warp_split_enabled() {
   return !off && !warp_no_pipe();
 }
 
-// DAMVS_WARP_REUSE (read per call): 1 = the corner-reuse split kernel at N = 5 (warp_split_kernel RU), 0 = the plain one
-bool warp_reuse() {
-  const char* v = getenv("DAMVS_WARP_REUSE");
-  return v && v[0] == '1';
-}
-
 template <typename T, int C, bool BLK>
 int split_lanes(const WarpArgs& a) {
   constexpr int S = C * (int)sizeof(T) / 16;
@@ -617,9 +582,7 @@ void launch_k(hipStream_t s, const WarpArgs& a, dim3 grid, int npb, int dchunk, 
       // (build.py FILE_FLAGS) it passes every stream case and runs 2 % faster than the runtime loop (stages 1-3: 0.520 /
       // 0.749 / 0.535 against 0.532 / 0.766 / 0.548 ms, profiles/r05/diag_streams/r05y; DESIGN.md section 4
       // "Concurrent streams")
-      if (a.N == 5 && !runtime_views && warp_reuse())
-        hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, 4, true>), grid, dim3(kWarpBlock), 0, s, a, a.rt, npb, dchunk, ndc);
-      else if (a.N == 5 && !runtime_views)
+      if (a.N == 5 && !runtime_views)
         hipLaunchKernelGGL((warp_split_kernel<T, C, MODE, 4>), grid, dim3(kWarpBlock), 0, s, a, a.rt, npb, dchunk, ndc);
       // N = 7 (cfgD) unrolled too, except the fp32 8-channel maps: cfgD B=4 stages 1 / 2 bf16 2.392 / 2.462 -> 2.293 /
       // 2.393 ms, fp32 3.525 / 4.240 -> 3.438 / 4.041 ms; fp32 stage 3 3.174 -> 3.233 ms stays on the runtime loop

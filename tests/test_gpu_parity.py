@@ -857,42 +857,6 @@ def test_conv0_dz_fp32_bitwise(s, D, H, W, shape, monkeypatch):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
-@pytest.mark.parametrize("s", [0, 1, 2])
-def test_warp_corner_reuse_bitwise(s, dtype, monkeypatch):
-    """The split warp with per-view corner reuse (DAMVS_WARP_REUSE=1: a lane reloads a view's 4 corner records only when
-    its bilinear cell changed from the previous plane) against the plain pipeline: the same records and arithmetic,
-    bitwise, at N = 5 for the three stage shapes on refined per-pixel hypotheses (the pipeline's, where consecutive
-    planes sample nearby points of each epipolar line) and on stage-1 linear ones."""
-    from damvsnet_amd.cascade import CascadeMVSNet
-    from damvsnet_amd.engine import hypotheses, proj_prepare
-    from damvsnet_amd import synth
-    net = CascadeMVSNet(ndepths=[48, 32, 8], compute_dtype=dtype)
-    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
-    net = net.to(DEV).eval()
-    B, N, H, W = 2, 5, 256, 320
-    C, D, scale = {0: (32, 48, 4), 1: (16, 32, 2), 2: (8, 8, 1)}[s]
-    h, w = H // scale, W // scale
-    proj, _, dv = synth.cameras(B, N, H, W)
-    P = cuda(torch.from_numpy(proj["stage%d" % (s + 1)]))
-    g = torch.Generator(device=DEV).manual_seed(1)
-    if s == 0:
-        hyps = hypotheses(cuda(torch.from_numpy(dv)), D, H, W, scale)
-    else:
-        pd = 600 + 100 * torch.rand(B, H // (2 * scale), W // (2 * scale), device=DEV, generator=g)
-        pv = 2 + 20 * torch.rand(B, H // (2 * scale), W // (2 * scale), device=DEV, generator=g)
-        hyps = hypotheses(cuda(torch.from_numpy(dv)), D, H, W, scale, pd, pv)
-    feats = [torch.randn(B, h, w, C, generator=g, device=DEV).to(dtype) for _ in range(N)]
-    eng = net.DepthNet.engine(s, net.cost_regularization[s], torch.device(DEV))
-    rt = proj_prepare(P)
-    with torch.no_grad():
-        monkeypatch.setenv("DAMVS_WARP_REUSE", "1")
-        a = eng.warp_aggregate(feats, P, hyps, rt=rt).clone()
-        monkeypatch.setenv("DAMVS_WARP_REUSE", "0")
-        b = eng.warp_aggregate(feats, P, hyps, rt=rt).clone()
-    assert torch.equal(a, b)
-
-
 @pytest.mark.parametrize("s,D,H,W", [(1, 24, 40, 72), (2, 8, 48, 96), (0, 48, 40, 72)])
 def test_gather_conv3d_k32_vs_k16_fp32(s, D, H, W, monkeypatch):
     """fp32 gather-kernel layers (conv3 / conv5 / conv6 / conv7 and the tile kernels' fallbacks): the 32-K split form

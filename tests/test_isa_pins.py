@@ -61,3 +61,24 @@ def test_warp_kernels_carry_no_packed_fp32_ops():
     pk = re.compile(r"v_pk_(fma|mul|add|mov)_f32\b")
     bad = sorted(k for k, b in warp.items() if any(pk.match(t) for t in b))
     assert not bad, "warp kernels with packed-FP32 VALU ops: %s" % bad[:10]
+
+
+@pytest.mark.skipif(not _llvm_ok(), reason="no llvm-objdump")
+def test_valu_kernels_carry_no_packed_fp32_ops():
+    """Round 6 extends the warp's rule to every kernel without MFMA instructions: in the two-stream forward any of them
+    can share a CU with the other sub-batch's MFMA kernels, the condition under which the warp's packed-FP32 results
+    came back wrong in lanes 48-63 ("Concurrent streams"). The VALU-only units are built without
+    the SLP and loop vectorizers (build.py FILE_FLAGS) and write no explicit float2 arithmetic; kernels with MFMA
+    instructions (the co-runners in every measured case, never the victims) keep theirs."""
+    import re
+    import isa
+    from damvsnet_amd import build
+    for f in ("k_warp.hip", "k_planes.hip", "k_geometry.hip", "k_regress.hip", "k_fusion.hip"):
+        assert "-fno-slp-vectorize" in build.FILE_FLAGS.get(f, []), f
+    build.build()
+    ks = isa.disassemble()
+    pk = re.compile(r"v_pk_(fma|mul|add|mov)_f32\b")
+    valu = {k: b for k, b in ks.items() if not any(t.startswith("v_mfma") for t in b)}
+    assert len(valu) >= 100, len(valu)
+    bad = sorted(k for k, b in valu.items() if any(pk.match(t) for t in b))
+    assert not bad, "kernels without MFMA carrying packed-FP32 VALU ops: %s" % bad[:10]

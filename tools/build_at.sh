@@ -9,7 +9,7 @@ git -C $R archive $C damvsnet_amd/csrc include | tar -x -C $T
 objs=""
 for f in $T/damvsnet_amd/csrc/*.hip $T/damvsnet_amd/csrc/*.cpp; do
   o=$T/$(basename $f).o
-  fl=""; [ "$(basename $f)" = k_warp.hip ] && fl="-fno-slp-vectorize"   # as damvsnet_amd/build.py FILE_FLAGS
+  fl=$(python3 -c "import sys; sys.path.insert(0, '$(dirname $0)/..'); from damvsnet_amd.build import FILE_FLAGS; print(' '.join(FILE_FLAGS.get('$(basename "$f")', [])))")   # damvsnet_amd/build.py FILE_FLAGS
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $fl -I$T/include -I$T/damvsnet_amd/csrc -x hip -c $f -o $o &
   objs="$objs $o"
 done

@@ -9,7 +9,7 @@ mkdir -p "$R/damvsnet_amd/ab"
 objs=""
 for f in "$S"/csrc/*.hip "$S"/csrc/*.cpp; do
   o=$T/$(basename "$f").o
-  fl=""; [ "$(basename "$f")" = k_warp.hip ] && fl="-fno-slp-vectorize"   # as damvsnet_amd/build.py FILE_FLAGS
+  fl=$(python3 -c "import sys; sys.path.insert(0, '$(dirname $0)/..'); from damvsnet_amd.build import FILE_FLAGS; print(' '.join(FILE_FLAGS.get('$(basename "$f")', [])))")   # damvsnet_amd/build.py FILE_FLAGS
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $fl -I"$S/include" -I"$S/csrc" -x hip -c "$f" -o "$o" &
   objs="$objs $o"
 done
