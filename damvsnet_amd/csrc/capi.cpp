@@ -312,7 +312,8 @@ struct Workspace {
 
 // Magnitude slots of the fp32 stage's activation tensors (damvs_device.h prescale_of): the volume, conv0..conv6
 // outputs, conv7 / conv9 outputs after their in-place skip adds (c4', c2'). conv11's output feeds the exact-fp32 VALU
-// prob conv and needs none. kAmaxSlotBytes each, zeroed at the start of every stage forward.
+// prob conv and needs none. Per tensor B slots of kAmaxSlotBytes (one per batch element), zeroed at the start of every
+// stage forward.
 enum { AM_VOL = 0, AM_C0 = 1, AM_C4S = 8, AM_C2S = 9, AM_SLOTS = 10 };
 constexpr size_t kAmaxSlotBytes = (size_t)kAmaxSlotWords * 4;
 static_assert(kAmaxSlotBytes == DAMVS_AMAX_SLOT_BYTES, "damvs.h slot size");
@@ -344,7 +345,7 @@ Workspace plan_ws(const damvs_stage* st, int B, int N, int D, int h, int w) {
   ws.status = o;  // the range status word at offset 0 (damvs_stage_status needs no shape)
   o += align_up(4);
   ws.amax = o;  // fp32: the magnitude slots of the stage's activation tensors
-  if (st->dtype == DAMVS_F32) o += AM_SLOTS * kAmaxSlotBytes;
+  if (st->dtype == DAMVS_F32) o += align_up(AM_SLOTS * (size_t)B * kAmaxSlotBytes);
   ws.rt = o;
   o += align_up((size_t)B * (N > 1 ? N - 1 : 1) * 12 * 4);
   ws.feat = o;  // channel-blocked copies of the N feature maps (only when C spans several 16-B chunks)
@@ -417,10 +418,11 @@ ConvArgs conv_args(const damvs_stage* st, int li, int B, const Shapes& S, int li
 // the skip sums c4' / c2' that conv9 / conv11 read
 constexpr int kLayerSlots[10][2] = {{AM_VOL, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {6, 7}, {7, AM_C4S},
                                     {AM_C4S, AM_C2S}, {AM_C2S, -1}};
-void set_slots(ConvArgs& a, const damvs_stage* st, char* amax, int layer) {
+void set_slots(ConvArgs& a, const damvs_stage* st, char* amax, int layer, int B) {
   if (st->dtype != DAMVS_F32 || !amax) return;
-  a.in_amax = reinterpret_cast<const unsigned*>(amax + kLayerSlots[layer][0] * kAmaxSlotBytes);
-  a.out_amax = kLayerSlots[layer][1] < 0 ? nullptr : reinterpret_cast<unsigned*>(amax + kLayerSlots[layer][1] * kAmaxSlotBytes);
+  const size_t per = (size_t)B * kAmaxSlotBytes;  // a tensor's B slots
+  a.in_amax = reinterpret_cast<const unsigned*>(amax + kLayerSlots[layer][0] * per);
+  a.out_amax = kLayerSlots[layer][1] < 0 ? nullptr : reinterpret_cast<unsigned*>(amax + kLayerSlots[layer][1] * per);
 }
 
 // U-Net through conv11 (+conv0 skip): the prob conv input ends in c[0]. fp32: the slots at ws + W.amax must hold the
@@ -440,7 +442,7 @@ int run_unet(const damvs_stage* st, hipStream_t s, int B, int D, int h, int w, c
   for (int i = 0; i < nlayers; ++i) {
     const Step& k = steps[i];
     ConvArgs a = conv_args(st, k.li, B, S, k.lin, k.lout, k.in, k.out, k.res);
-    set_slots(a, st, ws + W.amax, k.li);
+    set_slots(a, st, ws + W.amax, k.li, B);
     DAMVS_TRY(hip_check(launch_conv3d(s, st->dtype, a), "conv3d launch"));
   }
   return DAMVS_OK;
@@ -757,8 +759,8 @@ int damvs_stage_forward_probed(const damvs_stage* st, void* stream, int B, int N
   };
   WarpArgs wa = warp_args(st, B, N, st->C, D, h, w, fv, rt, hyps, ws + W.vol);
   if (st->dtype == DAMVS_F32) {  // fresh magnitude slots; the warp records the volume's
-    DAMVS_TRY(hip_check(hipMemsetAsync(ws + W.amax, 0, AM_SLOTS * kAmaxSlotBytes, s), "slot clear"));
-    wa.out_amax = reinterpret_cast<unsigned*>(ws + W.amax + AM_VOL * kAmaxSlotBytes);
+    DAMVS_TRY(hip_check(hipMemsetAsync(ws + W.amax, 0, AM_SLOTS * (size_t)B * kAmaxSlotBytes, s), "slot clear"));
+    wa.out_amax = reinterpret_cast<unsigned*>(ws + W.amax + AM_VOL * (size_t)B * kAmaxSlotBytes);
   }
   DAMVS_TRY(mark(0));
   DAMVS_TRY(hip_check(launch_warp_aggregate(s, st->dtype, st->mode, wa, blk), "warp_aggregate launch"));
@@ -850,11 +852,13 @@ int damvs_costreg_logits(const damvs_stage* st, void* stream, int B, int D, int 
   if (workspace_bytes < W.total) return fail(DAMVS_E_WORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, W.total);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   char* ws = reinterpret_cast<char*>(workspace);
-  if (st->dtype == DAMVS_F32) {  // the handed-in volume's magnitude, measured once
-    DAMVS_TRY(hip_check(hipMemsetAsync(ws + W.amax, 0, AM_SLOTS * kAmaxSlotBytes, s), "slot clear"));
-    DAMVS_TRY(hip_check(launch_amax(s, static_cast<const float*>(volume), (long long)B * D * h * w * st->C,
-                                    reinterpret_cast<unsigned*>(ws + W.amax + AM_VOL * kAmaxSlotBytes)),
-                        "amax launch"));
+  if (st->dtype == DAMVS_F32) {  // the handed-in volume's magnitude per batch element, measured once
+    DAMVS_TRY(hip_check(hipMemsetAsync(ws + W.amax, 0, AM_SLOTS * (size_t)B * kAmaxSlotBytes, s), "slot clear"));
+    const long long n = (long long)D * h * w * st->C;
+    for (int b = 0; b < B; ++b)
+      DAMVS_TRY(hip_check(launch_amax(s, static_cast<const float*>(volume) + b * n, n,
+                                      reinterpret_cast<unsigned*>(ws + W.amax + (AM_VOL * (size_t)B + b) * kAmaxSlotBytes)),
+                          "amax launch"));
   }
   DAMVS_TRY(run_unet(st, s, B, D, h, w, volume, ws, W));
   return hip_check(launch_prob_conv(s, st->dtype, B, st->base, D, h, w, ws + W.c[0], st->prob_w, nullptr, logits),

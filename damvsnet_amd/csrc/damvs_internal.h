@@ -41,7 +41,7 @@ struct WarpArgs {
   // computed rows; else a tile of tile_r rows x ppb / tile_r columns, tiles dealt strip by strip (tile_sw tiles wide,
   // top to bottom), so the blocks in flight on one XCD cover a compact 2D region of the reference image
   int tile_r, tile_sw, tiles_x;
-  unsigned* out_amax;  // fp32: magnitude slot of the written volume (damvs_device.h prescale_of), nullptr: none
+  unsigned* out_amax;  // fp32: magnitude slots of the written volume, one per batch element (prescale_of), or nullptr
 };
 
 // n / d for 0 <= n < 2^31 without a hardware divide: q = (umulhi(n, mul) + n) >> shift.
@@ -99,8 +99,9 @@ struct ConvArgs {
   // fp32: the phases of wgat32 (build_phases(., 32) at layer creation): K chunks and weight offsets at 32 K per chunk
   // (the taps are those of ph)
   int k32_chunks[kMaxPhases], k32_off[kMaxPhases];
-  // fp32 activation prescale (damvs_device.h prescale_of): the input tensor's magnitude slot (nullptr: unscaled) and
-  // the slot this layer's stored outputs are recorded into (nullptr: not recorded); bf16 ignores both
+  // fp32 activation prescale (damvs_device.h prescale_of): the input tensor's magnitude slots (nullptr: unscaled) and
+  // the slots this layer's stored outputs are recorded into (nullptr: not recorded), one slot (kAmaxSlotWords words)
+  // per batch element: a sample's scales do not depend on the rest of its batch; bf16 ignores both
   const unsigned* in_amax;
   unsigned* out_amax;
 };

@@ -67,10 +67,12 @@ constexpr int kGroups = 4;  // 16-voxel column groups per wave (64 output voxels
 #define DAMVS_DIAG_SKIP_EPI 0
 #endif
 
-// The fp32 prescale of a conv kernel's input (damvs_device.h prescale_of); bf16 kernels are unscaled (no load).
+// The fp32 prescale of a conv kernel's input for batch element b (damvs_device.h prescale_of; one magnitude slot per
+// batch element, so a sample's scales -- and bits -- do not depend on the other samples of its batch); bf16 kernels are
+// unscaled (no load).
 template <typename T>
-__device__ __forceinline__ Prescale ps_in(const ConvArgs& a) {
-  if constexpr (sizeof(T) == 4) return prescale_of(a.in_amax);
+__device__ __forceinline__ Prescale ps_in(const ConvArgs& a, int b) {
+  if constexpr (sizeof(T) == 4) return prescale_of(a.in_amax ? a.in_amax + (size_t)b * kAmaxSlotWords : nullptr);
   else return Prescale{1.f, 1.f};
 }
 // the epilogue's accumulator scale: the weights' 2^-k (fp32) times the input's 2^-k
@@ -90,8 +92,8 @@ __device__ __forceinline__ void am_fold(unsigned& am, bool ok, const float* v) {
   }
 }
 template <typename T>
-__device__ __forceinline__ void am_flush(const ConvArgs& a, unsigned am, int r) {
-  if constexpr (sizeof(T) == 4) amax_flush(am, a.out_amax, r);
+__device__ __forceinline__ void am_flush(const ConvArgs& a, unsigned am, int b, int r) {
+  if constexpr (sizeof(T) == 4) amax_flush(am, a.out_amax ? a.out_amax + (size_t)b * kAmaxSlotWords : nullptr, r);
 }
 // a loaded 16-byte fragment times the prescale (fp32; bf16 as is)
 __device__ __forceinline__ float4 ps_scale(const float4& x, float s) { return scale4(x, s); }
@@ -150,7 +152,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
   const int Qtot = a.B * a.Dq * a.Hq * a.Wq;
   const int base = (qblk * 4 + wave) * (KG * 16);
   if (base >= Qtot) return;  // (whole waves: the rest keep all lanes to the end, as amax_flush needs)
-  const Prescale ps = ps_in<T>(a);
+  const Prescale ps = ps_in<T>(a, 0);  // with magnitude slots the launcher runs one batch element per launch
   const float wsc = ps_wscale<T>(a, ps);
   unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
 
@@ -274,7 +276,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
       am_fold<T, 8>(am, valid[j], r);
       Vox8<T>::store(ro, off, r);
     }
-    am_flush<T>(a, am, blockIdx.x * 4 + wave);
+    am_flush<T>(a, am, 0, blockIdx.x * 4 + wave);
     return;
   }
   if constexpr (kSkip16) {
@@ -341,7 +343,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
       finish4<T>(a, ro, rr, q[j][m], a.resid != nullptr, off, valid[j] && cok[m], bias[m], acc[j][m], wsc, am);
     }
   }
-  am_flush<T>(a, am, blockIdx.x * 4 + wave);
+  am_flush<T>(a, am, 0, blockIdx.x * 4 + wave);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -389,7 +391,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
   const int z0 = tz * LTD, y0 = ty * LTH, x0 = tx * LTW;
 
   // halo fill: chunk c = (row, col) with row = (hz, hy); one row is LHW contiguous voxels in HBM
-  const Prescale ps = ps_in<T>(a);
+  const Prescale ps = ps_in<T>(a, b);
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * sizeof(T));
   const int vin0 = b * a.Di * a.Hi * a.Wi;
   stage_chunks<TILE_CHUNKS, 8>(tile, [&](int c) {
@@ -536,7 +538,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const ConvArgs a, int t
       finish4<T>(a, ro, rr, q[m], a.resid != nullptr, off, vok && cok[m], bias[m], acc[j][m], wsc, am);
     }
   }
-  am_flush<T>(a, am, blockIdx.x * 4 + wave);
+  am_flush<T>(a, am, b, blockIdx.x * 4 + wave);
 }
 
 // Row-pair variant for Cout <= 8 (conv0 of every stage): a 16-row MFMA tile holds 8 channels of
@@ -573,7 +575,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, 
   const int b = tt / tiles_z;
   const int z0 = tz * LTD, y0 = ty * LTH, x0 = tx * LTW;
 
-  const Prescale ps = ps_in<T>(a);
+  const Prescale ps = ps_in<T>(a, b);
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * sizeof(T));
   const int vin0 = b * a.Di * a.Hi * a.Wi;
   stage_chunks<TILE_CHUNKS, 8>(tile, [&](int c) {
@@ -646,7 +648,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_pair_kernel(const ConvArgs a, 
     if (a.resid) q = BufIO<T>::ldq(rr, vok ? off : kOOB);
     finish4<T>(a, ro, rr, q, a.resid != nullptr, off, vok, bias, acc[j], wsc, am);
   }
-  am_flush<T>(a, am, blockIdx.x * 4 + wave);
+  am_flush<T>(a, am, b, blockIdx.x * 4 + wave);
 }
 
 // z-sliding row-pair variant (conv0): a block owns an 8-row x TX-column output window over ZC
@@ -683,7 +685,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 && CIN <= 8 ? 2 : 1
   const int zend = min(zb + zc, a.Do);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * ES);
-  const Prescale ps = ps_in<T>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const Prescale ps = ps_in<T>(a, b);  // fp32: the input tensor's magnitude (damvs_device.h)
   const float wsc = ps_wscale<T>(a, ps);
   unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) {
@@ -841,7 +843,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 && CIN <= 8 ? 2 : 1
     step(z, pa, pb);
     if (z + 1 < zend) step(z + 1, pb, pa);
   }
-  am_flush<T>(a, am, blockIdx.x * 4 + wave);
+  am_flush<T>(a, am, b, blockIdx.x * 4 + wave);
 }
 
 // conv0 with each input plane's B fragments read from LDS once (round 3): input plane p feeds output planes p + 1,
@@ -882,7 +884,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (CIN == 32 ? 1 : 
   const int zend = min(zb + zc, a.Do);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * ES);
-  const Prescale ps = ps_in<T>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const Prescale ps = ps_in<T>(a, b);  // fp32: the input tensor's magnitude (damvs_device.h)
   const float wsc = ps_wscale<T>(a, ps);
   unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) {
@@ -1004,7 +1006,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (CIN == 32 ? 1 : 
     step(p, pa, pb);
     if (p + 1 <= zend) step(p + 1, pb, pa);
   }
-  am_flush<T>(a, am, blockIdx.x * 4 + wave);
+  am_flush<T>(a, am, b, blockIdx.x * 4 + wave);
 }
 
 // fp32 conv0 with the kernel depths on different waves (round 6). The input-plane walk above keeps all 36 / 18 A pairs
@@ -1049,7 +1051,7 @@ __global__ __launch_bounds__(192 * RP) DAMVS_WAVES(CIN == 8 ? 4 : 3) void conv0_
   const int zend = min(zb + zc, a.Do);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * CIN * ES);
-  const Prescale ps = ps_in<float>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const Prescale ps = ps_in<float>(a, b);  // fp32: the input tensor's magnitude (damvs_device.h)
   const float wsc = ps_wscale<float>(a, ps);
   unsigned am = 0u;  // max |stored value| (the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) DAMVS_INLINE {
@@ -1160,7 +1162,7 @@ __global__ __launch_bounds__(192 * RP) DAMVS_WAVES(CIN == 8 ? 4 : 3) void conv0_
     step(p, pa, pb);
     if (p + 1 <= zend) step(p + 1, pb, pa);
   }
-  am_flush<float>(a, am, blockIdx.x * 3 * RP + wave);
+  am_flush<float>(a, am, b, blockIdx.x * 3 * RP + wave);
 }
 
 template <int CIN, int RP, int TXG>
@@ -1333,7 +1335,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : 1) void conv_
   const int zend = min(zb + zc, a.Do);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 16 * ES);
-  const Prescale ps = ps_in<T>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const Prescale ps = ps_in<T>(a, b);  // fp32: the input tensor's magnitude (damvs_device.h)
   const float wsc = ps_wscale<T>(a, ps);
   unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) {
@@ -1441,7 +1443,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? 2 : 1) void conv_
     step(z, pa, pb);
     if (z + 1 < zend) step(z + 1, pb, pa);
   }
-  am_flush<T>(a, am, blockIdx.x * 4 + wave);
+  am_flush<T>(a, am, b, blockIdx.x * 4 + wave);
 }
 
 // Returns hipErrorNotSupported when no LDS variant fits this layer (caller falls back).
@@ -1506,7 +1508,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 2 ? 3 : 2) void decon
   const int zend = min(zb + zc, a.Di);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 16 * ES);
-  const Prescale ps = ps_in<T>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const Prescale ps = ps_in<T>(a, b);  // fp32: the input tensor's magnitude (damvs_device.h)
   const float wsc = ps_wscale<T>(a, ps);
   unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) {
@@ -1684,7 +1686,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
   const int zend = min(zb + zc, a.Di);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 32 * ES);
-  const Prescale ps = ps_in<T>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const Prescale ps = ps_in<T>(a, b);  // fp32: the input tensor's magnitude (damvs_device.h)
   const float wsc = ps_wscale<T>(a, ps);
   unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) {
@@ -1840,7 +1842,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
     step(qz, pa, pb);
     if (qz + 1 < zend) step(qz + 1, pb, pa);
   }
-  am_flush<T>(a, am, blockIdx.x * 4 + (threadIdx.x >> 6));
+  am_flush<T>(a, am, b, blockIdx.x * 4 + (threadIdx.x >> 6));
 }
 
 // conv1 (Conv3d k3 s2 p1, 8 -> 16 channels) streamed along z: output plane z reads input planes
@@ -1879,7 +1881,7 @@ __global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a
   const int ix0 = 2 * ox0 - 1, iy0 = 2 * oy0 - 1;
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in, (long long)a.B * a.Di * a.Hi * a.Wi * 8 * ES);
-  const Prescale ps = ps_in<T>(a);  // fp32: the input tensor's magnitude (damvs_device.h)
+  const Prescale ps = ps_in<T>(a, b);  // fp32: the input tensor's magnitude (damvs_device.h)
   const float wsc = ps_wscale<T>(a, ps);
   unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
   auto load_plane = [&](int iz, uint4 (*v)[PL]) {
@@ -1994,7 +1996,7 @@ __global__ __launch_bounds__(256) void conv_s2_c8_zslide_kernel(const ConvArgs a
     }
     __syncthreads();
   }
-  am_flush<T>(a, am, blockIdx.x * 4 + wave);
+  am_flush<T>(a, am, b, blockIdx.x * 4 + wave);
 }
 
 bool deconv_zslide_disabled() {  // read per call: tests flip it between launches
@@ -2054,6 +2056,23 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
     }
     return hipGetLastError();
   }
+  if (sizeof(T) == 4 && a.B > 1 && (a.in_amax || a.out_amax)) {
+    // the gather kernel's waves can straddle batch elements, and the magnitude slots are per batch element: with slots
+    // it runs one batch element per launch (the mid-level layers: conv3, conv5, conv7 and fallbacks)
+    const long long in_b = (long long)a.Di * a.Hi * a.Wi * a.Cin * 4, out_b = (long long)a.Do * a.Ho * a.Wo * a.Cout * 4;
+    for (int b = 0; b < a.B; ++b) {
+      ConvArgs a1 = a;
+      a1.B = 1;
+      a1.in = static_cast<const char*>(a.in) + b * in_b;
+      a1.out = static_cast<char*>(a.out) + b * out_b;
+      a1.resid = a.resid ? static_cast<const char*>(a.resid) + b * out_b : nullptr;
+      a1.in_amax = a.in_amax ? a.in_amax + (size_t)b * kAmaxSlotWords : nullptr;
+      a1.out_amax = a.out_amax ? a.out_amax + (size_t)b * kAmaxSlotWords : nullptr;
+      const hipError_t e = launch_t<T>(s, a1);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   if (a.xpair) {
     if (a.MT != 1 || a.Cout != 8) return hipErrorInvalidValue;
     hipLaunchKernelGGL((conv3d_mfma_kernel<T, 1, true>), grid, dim3(256), 0, s, a, nq);
@@ -2103,6 +2122,8 @@ hipError_t launch_conv3d(hipStream_t s, int store, const ConvArgs& a0) {
       a1.in = static_cast<const char*>(a0.in) + b * in_b;
       a1.out = static_cast<char*>(a0.out) + b * out_b;
       a1.resid = a0.resid ? static_cast<const char*>(a0.resid) + b * out_b : nullptr;
+      a1.in_amax = a0.in_amax ? a0.in_amax + (size_t)b * kAmaxSlotWords : nullptr;  // per-sample magnitude slots
+      a1.out_amax = a0.out_amax ? a0.out_amax + (size_t)b * kAmaxSlotWords : nullptr;
       const hipError_t e = launch_conv3d(s, store, a1);
       if (e != hipSuccess) return e;
     }

@@ -330,7 +330,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, kWarpBlock))) DAMVS_WAV
       finish(d, acc, sq);
     }
   }
-  if constexpr (sizeof(T) == 4) amax_flush(am, a.out_amax, blockIdx.x * (BLOCK / 64) + (int)(threadIdx.x >> 6));
+  if constexpr (sizeof(T) == 4) amax_flush(am, a.out_amax ? a.out_amax + (size_t)b * kAmaxSlotWords : nullptr, blockIdx.x * (BLOCK / 64) + (int)(threadIdx.x >> 6));
 }
 
 // Channel-split form (NHWC maps whose pixel is S = C * sizeof(T) / 16 chunks of 16 bytes, S = 2, 4 or 8 -- 8: the
@@ -540,7 +540,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, kWarpBlock))) void warp
     hyp_n = hyp_nn;
     finish(d, acc, sq);
   }
-  if constexpr (sizeof(T) == 4) amax_flush(am, a.out_amax, blockIdx.x * (kWarpBlock / 64) + (int)(threadIdx.x >> 6));
+  if constexpr (sizeof(T) == 4) amax_flush(am, a.out_amax ? a.out_amax + (size_t)b * kAmaxSlotWords : nullptr, blockIdx.x * (kWarpBlock / 64) + (int)(threadIdx.x >> 6));
 }
 
 // Lanes per voxel the launcher uses for C-channel maps: the channel-split kernel for NHWC maps of 2, 4 or 8 16-byte

@@ -170,14 +170,16 @@ class StageEngine:
     # ---- fp32 magnitude slots for layer-by-layer execution (include/damvs.h DAMVS_AMAX_SLOT_BYTES)
     SLOT_WORDS = 1024  # DAMVS_AMAX_SLOT_BYTES / 4
 
-    def new_slots(self, n=10):
-        """n zeroed magnitude slots (int32 rows of SLOT_WORDS words) on the engine's device."""
-        return torch.zeros(n, self.SLOT_WORDS, dtype=torch.int32, device=self.device)
+    def new_slots(self, B, n=10):
+        """Zeroed magnitude slots of n tensors x B batch elements: int32 [n][B][SLOT_WORDS] on the engine's device
+        (slots[i] is tensor i's, one slot per batch element, as damvs_costreg_layer_scaled takes them)."""
+        return torch.zeros(n, B, self.SLOT_WORDS, dtype=torch.int32, device=self.device)
 
-    def tensor_amax(self, t, slot):
-        """Fold max |t| (a contiguous float32 device tensor) into ``slot`` (damvs_tensor_amax)."""
-        check(self._lib.damvs_tensor_amax(_capi.stream_ptr(self.device), ptr(t), t.numel(), ptr(slot)))
-        return slot
+    def tensor_amax(self, t, slots):
+        """Fold max |t[b]| of a contiguous float32 device tensor [B][...] into slots[b] (damvs_tensor_amax per b)."""
+        for b in range(t.shape[0]):
+            check(self._lib.damvs_tensor_amax(_capi.stream_ptr(self.device), ptr(t[b]), t[b].numel(), ptr(slots[b])))
+        return slots
 
     def unet_buffers(self, B, D, h, w):
         """Level tensors c0..c6 (conv0..conv6 outputs, NDHWC) of a D x h x w volume."""

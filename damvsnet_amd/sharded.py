@@ -58,25 +58,25 @@ _STEPS = ((0, "v", 0, 0), (1, 0, 1, 1), (2, 1, 2, 1), (3, 2, 3, 2), (4, 3, 4, 2)
 _SLOTS = ((0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (6, 7), (7, 8), (8, 9), (9, None))
 
 
-def _new_slots(eng):
-    """Zeroed magnitude slots of an fp32 engine (None: bf16, or an engine without slots)."""
+def _new_slots(eng, B):
+    """Zeroed magnitude slots [tensor][batch element][words] of an fp32 engine (None: bf16, or an engine without
+    slots)."""
     if getattr(eng, "dtype", None) != torch.float32 or not hasattr(eng, "new_slots"):
         return None
-    return eng.new_slots()
+    return eng.new_slots(B)
 
 
-def _fold_owned(comm: "Comm", slot, parts):
-    """slot := max |x| over every rank's ``parts`` (the tensor pieces this rank owns; None entries skipped): one
-    all-gather of the per-rank maxima. The slot holds the float's bits in its first word."""
-    dev = slot.device
-    m = torch.zeros(1, dtype=torch.float32, device=dev)
+def _fold_owned(comm: "Comm", slots, parts):
+    """slots[b] := max |x[b]| over every rank's ``parts`` (the [B, ...] tensor pieces this rank owns; None entries
+    skipped): one all-gather of the per-rank, per-sample maxima. A slot holds the float's bits in its first word."""
+    B, dev = slots.shape[0], slots.device
+    m = torch.zeros(B, dtype=torch.float32, device=dev)
     for p in parts:
         if p is not None and p.numel():
-            m = torch.maximum(m, p.abs().amax().reshape(1).float())
-    bits = m.view(torch.int32)
-    got = comm.all_gather(bits)
-    slot.zero_()
-    slot[:1].copy_(torch.stack([g.to(dev) for g in got]).amax(0))
+            m = torch.maximum(m, p.abs().reshape(B, -1).amax(1).float())
+    got = comm.all_gather(m.view(torch.int32))
+    slots.zero_()
+    slots[:, 0].copy_(torch.stack([g.to(dev) for g in got]).amax(0))
 
 
 def slab_rows(h: int, P: int):
@@ -287,7 +287,7 @@ def _costreg_sharded(comm: Comm, eng, vol, c, D: int, R: int, w: int, slots=None
             if slots is None:
                 eng.unet_layer(layer, D, R, w, x[b0:b1], c[dst][b0:b1])
             else:
-                eng.unet_layer(layer, D, R, w, x[b0:b1], c[dst][b0:b1], in_slot=slots[sin])
+                eng.unet_layer(layer, D, R, w, x[b0:b1], c[dst][b0:b1], in_slot=slots[sin][b0:b1])
             pending[i] = _halo_start(comm, c[dst][b0:b1], HALO >> level)
         if slots is not None and sout is not None:
             hl = HALO >> level
@@ -321,7 +321,7 @@ def sharded_stage(comm: Comm, eng, feats, layout, rt, hyps, h: int, w: int, warp
     top = lo - (y0 - HALO)                          # ... start at this slab row
     n = hi - lo
 
-    slots = _new_slots(eng)
+    slots = _new_slots(eng, B)
     hyps_s = torch.empty(B, D, R, w, device=dev, dtype=hyps.dtype)
     hyps_s[:, :, :top].zero_()
     hyps_s[:, :, top + n:].zero_()
@@ -403,7 +403,7 @@ def _gathered_stage(comm: Comm, eng, feats, layout, rt, hyps, h: int, w: int, wa
     del got, mine
     hook("costreg")
     c = eng.unet_buffers(B, D, h, w)
-    slots = _new_slots(eng)
+    slots = _new_slots(eng, B)
     if slots is None:
         for layer, src, dst, _level in _STEPS:
             eng.unet_layer(layer, D, h, w, vol if src == "v" else c[src], c[dst])

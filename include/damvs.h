@@ -180,22 +180,24 @@ int damvs_costreg_layer(const damvs_stage* st, void* stream, int layer, int B, i
                         void* out);
 
 /* Magnitude slots (fp32 stages). The fp32 path splits each activation x into f16 pieces x * 2^k = hi + lo with k
- * chosen per tensor from its largest magnitude, so large activations do not overflow the f16 range and small ones keep
- * their lo piece normal (the reference's fp32 convolutions have no range limit: models/cas_mvsnet.py:64-76,
- * models/module.py:510-541). damvs_stage_forward keeps the slots of its tensors in its workspace. A caller running the
- * U-Net layer by layer (sharded execution) owns them: one slot = DAMVS_AMAX_SLOT_BYTES of device memory, zeroed before
- * use; producers fold max |value| into it (atomically; bit patterns of non-negative floats compare as unsigned
- * integers), consumers read it. Any replica word may hold the tensor's maximum: to set a slot by hand, zero it and
- * write the float's bits (as uint32) into its first word. */
+ * chosen per tensor and batch element from its largest magnitude, so large activations do not overflow the f16 range
+ * and small ones keep their lo piece normal (the reference's fp32 convolutions have no range limit:
+ * models/cas_mvsnet.py:64-76, models/module.py:510-541), and a sample's result does not depend on the rest of its
+ * batch. damvs_stage_forward keeps the slots of its tensors in its workspace. A caller running the U-Net layer by layer
+ * (sharded execution) owns them: per tensor B slots of DAMVS_AMAX_SLOT_BYTES of device memory (slot b for batch
+ * element b, consecutive), zeroed before use; producers fold max |value| into them (atomically; bit patterns of
+ * non-negative floats compare as unsigned integers), consumers read them. Any replica word of a slot may hold the
+ * maximum: to set a slot by hand, zero it and write the float's bits (as uint32) into its first word. */
 #define DAMVS_AMAX_SLOT_BYTES 4096
 
-/* damvs_costreg_layer with magnitude slots (fp32; bf16 stages ignore them): in_slot = the input tensor's slot (NULL:
- * unscaled split, exact only while the activations stay inside [2^-3, 65504)), out_slot = the slot this layer's stored
- * outputs are folded into (NULL: not recorded). damvs_costreg_layer = both NULL. */
+/* damvs_costreg_layer with magnitude slots (fp32; bf16 stages ignore them): in_slot = the input tensor's B slots
+ * (NULL: unscaled split, exact only while the activations stay inside [2^-3, 65504)), out_slot = the B slots this
+ * layer's stored outputs are folded into (NULL: not recorded). damvs_costreg_layer = both NULL. */
 int damvs_costreg_layer_scaled(const damvs_stage* st, void* stream, int layer, int B, int D, int h, int w,
                                const void* in, void* out, const void* in_slot, void* out_slot);
 
-/* Fold max |x[i]| of n floats (device) into a magnitude slot (stream-ordered; the slot is not cleared). */
+/* Fold max |x[i]| of n floats (device) into one magnitude slot (stream-ordered; the slot is not cleared): call it
+ * per batch element with that element's slot. */
 int damvs_tensor_amax(void* stream, const float* x, long long n, void* slot);
 
 /* The tail of damvs_stage_forward: prob conv (models/module.py:541) + softmax regression, confidence and

@@ -548,6 +548,26 @@ def test_fp32_prescale_feature_scale_sweep(case, scale):
     assert good.mean() > 0.99 and err[good].max() < 1e-3, (good.mean(), err[good].max())
 
 
+@pytest.mark.parametrize("s", [0, 1, 2])
+def test_fp32_prescale_is_per_sample(s):
+    """The magnitude slots are per batch element: a sample's scales, and so its bits, do not depend on the other
+    samples of its batch -- here a batch whose other sample has features x 1000 (a volume 1e6 larger) gives the normal
+    sample bitwise the maps it gets alone (as the one- vs two-stream forward and sharded stages need)."""
+    from damvsnet_amd.cascade import CascadeMVSNet
+    C, D, h, w = {0: (32, 48, 64, 80), 1: (16, 32, 64, 80), 2: (8, 8, 128, 160)}[s]
+    net = CascadeMVSNet(ndepths=[48, 32, 8])
+    net.load_state_dict(model_state("depthnet_cfgA_adaptive"), strict=True)
+    net = net.to(DEV).eval()
+    feats, P, hyps = depthnet_inputs(B=2, N=5, H=h, W=w, D=D, stage_idx=s, C=C)
+    mixed = [torch.cat([f[:1] * 1000.0, f[1:]]) for f in feats]
+    with torch.no_grad():
+        both = net.DepthNet(s, [cuda(f) for f in mixed], cuda(P), cuda(hyps), D, net.cost_regularization[s])
+        alone = net.DepthNet(s, [cuda(f[1:]) for f in feats], cuda(P[1:]), cuda(hyps[1:]), D,
+                             net.cost_regularization[s])
+    for k in ("depth", "photometric_confidence", "variance", "prob_volume"):
+        assert torch.equal(both[k][1:], alone[k]), k
+
+
 def test_cascade_range_status_fp32():
     """CascadeMVSNet.forward reads every stage's range status once per forward (one and two sub-batch streams):
     images scaled so that the fp32 front-end's activations leave the f16 range raise DamvsRangeError."""
