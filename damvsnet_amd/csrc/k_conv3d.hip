@@ -152,13 +152,18 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
   const int Qtot = a.B * a.Dq * a.Hq * a.Wq;
   const int base = (qblk * 4 + wave) * (KG * 16);
   if (base >= Qtot) return;  // (whole waves: the rest keep all lanes to the end, as amax_flush needs)
-  const Prescale ps = ps_in<T>(a, 0);  // with magnitude slots the launcher runs one batch element per launch
-  const float wsc = ps_wscale<T>(a, ps);
-  unsigned am = 0u;  // max |stored value| (fp32: the output's magnitude slot)
+  // fp32 magnitude slots are per batch element: a wave's 64 voxels span at most two elements (the launcher takes B > 1
+  // only with Dq * Hq * Wq >= 64), b_lo and b_hi; each voxel's inputs are scaled by its own element's prescale, its
+  // accumulators scaled back by it, and its outputs folded into that element's slot
+  const int qpb = a.Dq * a.Hq * a.Wq;
+  const int b_lo = base / qpb, b_hi = (min(base + KG * 16, Qtot) - 1) / qpb;
+  const Prescale ps0 = ps_in<T>(a, b_lo), ps1 = b_hi != b_lo ? ps_in<T>(a, b_hi) : ps0;
+  unsigned am0 = 0u, am1 = 0u;  // max |stored value| of b_lo's and b_hi's voxels (fp32: their magnitude slots)
 
   const int IS = a.in_stride, OS = a.out_stride;
   int zs[KG], ys[KG], xs[KG], pin[KG], pout[KG];
-  bool valid[KG];
+  bool valid[KG], hij[KG];  // hij: the voxel belongs to b_hi
+  float sj[KG], wscj[KG];   // its input prescale, its accumulator scale
 #pragma unroll
   for (int j = 0; j < KG; ++j) {
     int q = base + j * 16 + n;
@@ -167,6 +172,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
     const int r1 = fdiv(a.div_wq, q), qx = q - r1 * a.Wq;
     const int r2 = fdiv(a.div_hq, r1), qy = r1 - r2 * a.Hq;
     const int b = fdiv(a.div_dq, r2), qz = r2 - b * a.Dq;
+    hij[j] = b != b_lo;
+    sj[j] = hij[j] ? ps1.s : ps0.s;
+    wscj[j] = ps_wscale<T>(a, hij[j] ? ps1 : ps0);
     zs[j] = qz * IS; ys[j] = qy * IS; xs[j] = qx * IS;
     pin[j] = ((b * a.Di + zs[j]) * a.Hi + ys[j]) * a.Wi + xs[j];
     pout[j] = ((b * a.Do + qz * OS + ph.pd) * a.Ho + qy * OS + ph.ph) * a.Wo + qx * OS + (XP ? (g >> 1) : ph.pw);
@@ -203,7 +211,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
       const bool ok = valid[j] && tv && (unsigned)iz < (unsigned)a.Di && (unsigned)iy < (unsigned)a.Hi &&
                       (unsigned)ix < (unsigned)a.Wi;
       xf[j] = IO::frag(r0, ok ? (uint32_t)((pin[j] + tapoff) * a.Cin + ci) * ES : kOOB);
-      if constexpr (sizeof(T) == 4) xf[j] = scale4(xf[j], ps.s);
+      if constexpr (sizeof(T) == 4) xf[j] = scale4(xf[j], sj[j]);
     }
     ci += rc;
     t += qt;
@@ -232,7 +240,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
                         (unsigned)ix < (unsigned)a.Wi;
         const uint32_t off = (uint32_t)((pin[j] + tapoff) * a.Cin + ci) * ES;
         const float4 lo4 = IO::frag(r0, ok ? off : kOOB), hi4 = IO::frag(r0, ok ? off + 16u : kOOB);
-        xf[j] = split8s(lo4, hi4, ps.s);
+        xf[j] = split8s(lo4, hi4, sj[j]);
       }
       ci += rc;
       t += qt;
@@ -268,15 +276,19 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
       if (!lead) continue;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        r[i] = fmaf(r[i], wsc, b8[i]);
+        r[i] = fmaf(r[i], wscj[j], b8[i]);
         if (a.relu) r[i] = relu(r[i]);
       }
       const uint32_t off = valid[j] ? (uint32_t)(pout[j] * 8) * ES : kOOB;
       if (a.resid) Vox8<T>::add(rr, off, r);
-      am_fold<T, 8>(am, valid[j], r);
+      unsigned amj = 0u;
+      am_fold<T, 8>(amj, valid[j], r);
+      am0 = hij[j] ? am0 : max(am0, amj);
+      am1 = hij[j] ? max(am1, amj) : am1;
       Vox8<T>::store(ro, off, r);
     }
-    am_flush<T>(a, am, 0, blockIdx.x * 4 + wave);
+    am_flush<T>(a, am0, b_lo, blockIdx.x * 4 + wave);
+    if (b_hi != b_lo) am_flush<T>(a, am1, b_hi, blockIdx.x * 4 + wave);
     return;
   }
   if constexpr (kSkip16) {
@@ -340,10 +352,14 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 ? 3 : 1
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const uint32_t off = (uint32_t)(pout[j] * a.Cout + m * 16 + cg) * ES;
-      finish4<T>(a, ro, rr, q[j][m], a.resid != nullptr, off, valid[j] && cok[m], bias[m], acc[j][m], wsc, am);
+      unsigned amj = 0u;
+      finish4<T>(a, ro, rr, q[j][m], a.resid != nullptr, off, valid[j] && cok[m], bias[m], acc[j][m], wscj[j], amj);
+      am0 = hij[j] ? am0 : max(am0, amj);
+      am1 = hij[j] ? max(am1, amj) : am1;
     }
   }
-  am_flush<T>(a, am, 0, blockIdx.x * 4 + wave);
+  am_flush<T>(a, am0, b_lo, blockIdx.x * 4 + wave);
+  if (b_hi != b_lo) am_flush<T>(a, am1, b_hi, blockIdx.x * 4 + wave);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2056,9 +2072,9 @@ hipError_t launch_t(hipStream_t s, const ConvArgs& a) {
     }
     return hipGetLastError();
   }
-  if (sizeof(T) == 4 && a.B > 1 && (a.in_amax || a.out_amax)) {
-    // the gather kernel's waves can straddle batch elements, and the magnitude slots are per batch element: with slots
-    // it runs one batch element per launch (the mid-level layers: conv3, conv5, conv7 and fallbacks)
+  if (sizeof(T) == 4 && a.B > 1 && (a.in_amax || a.out_amax) && a.Dq * a.Hq * a.Wq < kGroups * 16) {
+    // the gather kernel's waves straddle at most two batch elements (per-voxel prescales); a q-grid of fewer voxels
+    // than a wave runs one batch element per launch
     const long long in_b = (long long)a.Di * a.Hi * a.Wi * a.Cin * 4, out_b = (long long)a.Do * a.Ho * a.Wo * a.Cout * 4;
     for (int b = 0; b < a.B; ++b) {
       ConvArgs a1 = a;
