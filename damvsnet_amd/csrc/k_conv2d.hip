@@ -830,6 +830,14 @@ hipError_t launch_halo(hipStream_t s, const Conv2dArgs& a, bool dry = false) {
 #define DAMVS_WIDE_DIAG 0  // diagnostic builds only (tools/build_diag_wide.sh): skip parts of the K loop
 #endif
 constexpr int WC = 64, WR = 2;  // q-tile columns x rows
+// A wave whose q-columns past the grid leave it at most one valid 16-column N-group (the last tile column of the 200-
+// and 400-column grids of GeoFF stage 3: 8 / 16 valid columns of 64) runs its K loop on that N-group alone: no MFMAs
+// and B reads for the other three (2 or 3 valid groups run all 4). The fp32 rolling loop and the stride-2 AG loops; not
+// the stride-1 AG loops, whose second loop copy spilled (60-75 VGPRs). Build with -DDAMVS_WIDE_NG_SKIP=0 for the A/B.
+#ifndef DAMVS_WIDE_NG_SKIP
+#define DAMVS_WIDE_NG_SKIP 1
+#endif
+constexpr bool WIDE_NG_SKIP = DAMVS_WIDE_NG_SKIP;
 
 // Input halo geometry of a WR x WC q-tile for taps spanning `span` input pixels (IS = input stride). Stride 1: rows of
 // WC + span - 1 pixels. Stride 2: 2 (WR - 1) + span rows of 2 (WC - 1) + span columns, each row stored as its even
@@ -1152,10 +1160,14 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
       bh = base + Fm::slot(p0x, g);
       bl = base + Fm::slot(p0x, g + 4);
     };
+    // NG: the wave's N-groups that hold q-columns inside the grid (uniform per block: its tile column), the only ones
+    // whose MFMAs and B reads run -- the last tile column of a 200-column grid has 8 valid columns of 64
+    auto rs_loop = [&](auto NGc) DAMVS_INLINE {
+    constexpr int NG = decltype(NGc)::value;
     F16Pair b[NGW];
     baddr(0, 0);
 #pragma unroll
-    for (int j = 0; j < NGW; ++j) b[j] = F16Pair{hbuf[bh + j * 16 * SLOTS], hbuf[bl + j * 16 * SLOTS]};
+    for (int j = 0; j < NG; ++j) b[j] = F16Pair{hbuf[bh + j * 16 * SLOTS], hbuf[bl + j * 16 * SLOTS]};
     // PS: the tap's piece phase (0..2 load, 1..3 store; 4 none)
     auto rstep = [&](auto PS, const F16Pair (&cur)[4], F16Pair (&nxt)[4]) DAMVS_INLINE {
       constexpr int ps = decltype(PS)::value;
@@ -1178,14 +1190,14 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
       // the loads above stay above the MFMAs (the scheduler would otherwise sink them next to their uses, a chunk later)
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int j = 0; j < NGW; ++j) {
+      for (int j = 0; j < NG; ++j) {
 #pragma unroll
         for (int m = 0; m < 4; ++m) mma_split32(cur[m], b[j], acc[m][j]);
         b[j] = F16Pair{hbuf[bh + j * 16 * SLOTS], hbuf[bl + j * 16 * SLOTS]};
       }
       // per N-group: its 12 MFMAs, then its two B reads for the next chunk
 #pragma unroll
-      for (int j = 0; j < NGW; ++j) {
+      for (int j = 0; j < NG; ++j) {
         __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
@@ -1220,6 +1232,9 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
         }
       }
     }
+    };
+    if (WIDE_NG_SKIP && a.Wq - qx0 - wc <= 16) rs_loop(std::integral_constant<int, 1>{});
+    else rs_loop(std::integral_constant<int, NGW>{});
     __syncthreads();  // the epilogue's staging tiles overwrite the halo region other waves may still read
   } else if constexpr (AG && !SP) {
     // bf16 AG: the fp32 AG loop below with one 16-byte A fragment per cout tile (tile m of the wave's cout half at
@@ -1230,7 +1245,8 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
 #pragma unroll
       for (int m = 0; m < 4; ++m) x[m] = q[m * 64];
     };
-    auto gstep = [&](const raw (&cur)[4], raw (&nxt)[4]) DAMVS_INLINE {
+    auto gstep = [&](auto NGc, const raw (&cur)[4], raw (&nxt)[4]) DAMVS_INLINE {
+      constexpr int NG = decltype(NGc)::value;  // N-groups inside the q-grid
       int c1 = c, t1 = t + 1;
       if (t1 == nt) {
         c1 = c + 1 < nsl ? c + 1 : c;
@@ -1241,11 +1257,11 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
       const raw* hbs = hbuf + (NHB == 2 ? (c & 1) * HP * SLOTS : 0) + p0x * SLOTS + Fm::slot(p0x, g);
       raw bf[NGW];
 #pragma unroll
-      for (int j = 0; j < NGW; ++j) bf[j] = hbs[j * 64];
+      for (int j = 0; j < NG; ++j) bf[j] = hbs[j * 64];
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int j = 0; j < NGW; ++j) Frag2<bf16_t>::mma(cur[m], bf[j], acc[m][j]);
+        for (int j = 0; j < NG; ++j) Frag2<bf16_t>::mma(cur[m], bf[j], acc[m][j]);
       if (t == 0 && c + 1 < nsl) hload(c + 1);
       if (t == nt - 1 && c + 1 < nsl) {
         if (NHB == 1) __syncthreads();
@@ -1256,10 +1272,14 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
     };
     raw a0[4], a1[4];
     aload(a0, 0, 0);
-    for (int kk = 0; kk < nk; kk += 2) {
-      gstep(a0, a1);
-      if (kk + 1 < nk) gstep(a1, a0);
-    }
+    auto ag_loop = [&](auto NGc) DAMVS_INLINE {
+      for (int kk = 0; kk < nk; kk += 2) {
+        gstep(NGc, a0, a1);
+        if (kk + 1 < nk) gstep(NGc, a1, a0);
+      }
+    };
+    if (IS == 2 && WIDE_NG_SKIP && a.Wq - qx0 - wc <= 16) ag_loop(std::integral_constant<int, IS == 2 ? 1 : NGW>{});
+    else ag_loop(std::integral_constant<int, NGW>{});
     __syncthreads();
   } else if constexpr (AG) {
     const raw* wa = wsrc + wm * 512 + lane;  // the wave's cout half: tile m's hi at m * 128, lo at m * 128 + 64
@@ -1269,7 +1289,8 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
       for (int m = 0; m < 4; ++m) x[m] = F16Pair{q[m * 128], q[m * 128 + 64]};
     };
     // chunk (c, t) with A in `cur`; chunk (c, t) + 1 (clamped to the last) loaded into `nxt` first
-    auto gstep = [&](const F16Pair (&cur)[4], F16Pair (&nxt)[4]) DAMVS_INLINE {
+    auto gstep = [&](auto NGc, const F16Pair (&cur)[4], F16Pair (&nxt)[4]) DAMVS_INLINE {
+      constexpr int NG = decltype(NGc)::value;  // N-groups inside the q-grid
       int c1 = c, t1 = t + 1;
       if (t1 == nt) {
         t1 = 0;
@@ -1282,11 +1303,11 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
       const int sh = Fm::slot(p0x, g), sl = Fm::slot(p0x, g + 4);
       F16Pair bf[NGW];
 #pragma unroll
-      for (int j = 0; j < NGW; ++j) bf[j] = F16Pair{hb[j * 16 * SLOTS + sh], hb[j * 16 * SLOTS + sl]};
+      for (int j = 0; j < NG; ++j) bf[j] = F16Pair{hb[j * 16 * SLOTS + sh], hb[j * 16 * SLOTS + sl]};
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int j = 0; j < NGW; ++j) mma_split32(cur[m], bf[j], acc[m][j]);
+        for (int j = 0; j < NG; ++j) mma_split32(cur[m], bf[j], acc[m][j]);
       if (t == 0 && c + 1 < nsl) hload(c + 1);
       if (t == nt - 1 && c + 1 < nsl) {
         // two buffers: the one slice c - 1 used, which every wave left at the previous slice switch
@@ -1298,10 +1319,14 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
     };
     F16Pair a0[4], a1[4];
     aload(a0, 0, 0);
-    for (int kk = 0; kk < nk; kk += 2) {  // unrolled by two: the register sets alternate statically
-      gstep(a0, a1);
-      if (kk + 1 < nk) gstep(a1, a0);
-    }
+    auto ag_loop = [&](auto NGc) DAMVS_INLINE {
+      for (int kk = 0; kk < nk; kk += 2) {  // unrolled by two: the register sets alternate statically
+        gstep(NGc, a0, a1);
+        if (kk + 1 < nk) gstep(NGc, a1, a0);
+      }
+    };
+    if (IS == 2 && WIDE_NG_SKIP && a.Wq - qx0 - wc <= 16) ag_loop(std::integral_constant<int, IS == 2 ? 1 : NGW>{});
+    else ag_loop(std::integral_constant<int, NGW>{});
     __syncthreads();  // the epilogue's staging tiles overwrite the halo region other waves may still read
   } else {
     for (int kk = 0; kk < nk; kk += 2) {  // unrolled by two: the register sets alternate statically

@@ -373,13 +373,15 @@ def test_planes_four_columns_bitwise(k, ng, relu, pre, monkeypatch):
 
 # fp32 wide layers on the rolling K loop (conv2d_wide_kernel RS) against the AG loop (DAMVS_WIDE_RS=0): the same MFMA
 # sequence per accumulator, so bitwise equal. Stride-1 128-channel blocks: GeoBlock conv2 with the plane, two inputs +
-# plane + both residuals, the k5 s2 transposed decoder (phases of 9 / 6 / 6 / 4 taps), transposed k3 s1, ragged tiles.
+# plane + both residuals, the k5 s2 transposed decoder (phases of 9 / 6 / 6 / 4 taps), transposed k3 s1, ragged tiles
+# (W 70, 130, 200: a last tile column of at most 16 valid q-columns runs one N-group per wave).
 RS_CASES = [
     (False, 3, 1, 1, 0, 128, 0, (0,), 128, True, True, 0, (37, 151)),
     (False, 3, 1, 1, 0, 128, 128, (256,), 256, True, True, 2, (20, 24)),
     (True, 5, 2, 2, 1, 256, 0, (), 128, True, False, 1, (30, 70)),
     (True, 3, 1, 1, 0, 128, 0, (), 128, True, False, 0, (19, 130)),
     (False, 3, 1, 1, 0, 96, 0, (96,), 128, False, False, 0, (8, 64)),
+    (False, 3, 1, 1, 0, 256, 0, (256,), 256, True, True, 0, (6, 200)),  # GeoFF stage 3's 200-column grid
 ]
 
 
