@@ -46,6 +46,8 @@ CASES = {
     "G4 deconv 128->32 k5s2 B=4": (True, 5, 2, 2, 1, 128, 0, 0, 32, True, 4, 296, 400, False, 1),
     "M4 dec5 64->32 k5s2 B=4": (True, 5, 2, 2, 1, 64, 0, 0, 32, True, 4, 296, 400, False, 1),
     "Z4 dec 16->8 k5s2 full B=4": (True, 5, 2, 2, 1, 16, 0, 0, 8, True, 4, 592, 800, False, 1),
+    "FA feat conv1.0 8->16 k5s2 x20": (False, 5, 2, 2, 0, 8, 0, 0, 16, True, 20, 1184, 1600, False, 0),
+    "FB feat conv2.0 16->32 k5s2 x20": (False, 5, 2, 2, 0, 16, 0, 0, 32, True, 20, 592, 800, False, 0),
 }
 
 
