@@ -432,6 +432,154 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) != 2 ? 1 : CIN == 32 ? 
   }
 }
 
+// LDS-staged variant for the thin stride-2 5x5 convs (one tensor input of CIN 8 or 16 channels, padding 2, no plane):
+// FeatureNet's downsampling convs conv1.0 (8 -> 16 at 1184 x 1600) and conv2.0 (16 -> 32 at 592 x 800), which the
+// gather kernel runs at 0.3 of their HBM roofline (each input pixel fetched by ~6 output pixels' taps through L1;
+// models/module.py FeatureNet). A block owns a TR-row x 64-column output tile; its (2 TR + 3) x 131-pixel input halo is
+// read once with 16-byte loads (zero padding by range-checked buffer loads) and every B fragment is a ds_read_b128.
+// Each halo row is stored as its even then its odd columns (66 pixels each), so the 16 lanes of an N-group (16
+// consecutive output columns, input columns 2 apart) read 16 consecutive LDS pixels at every tap. Wave w owns columns
+// [16w, 16w + 16), group j output row j; a K chunk spans KC / CIN taps (per-lane tap offsets are compile-time constants
+// once the K loop unrolls, as in conv2d_lds_kernel).
+constexpr int S2W = 64, S2NC = 2 * (S2W - 1) + 5, S2HCP = (S2NC + 1) / 2, S2PITCH = 2 * S2HCP;
+
+template <int CH>
+__device__ constexpr int s2_toff(int t) {  // tap t = (ty, tx) of the 5 x 5 block, in 16-byte chunks
+  return t >= 25 ? s2_toff<CH>(24) : ((t / 5) * S2PITCH + (t % 5 & 1) * S2HCP + (t % 5 >> 1)) * CH;
+}
+
+template <typename T, int CIN, int MT, int TR>
+__global__ __launch_bounds__(256) void conv2d_lds_s2_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int ntiles) {
+  typedef BufIO<T> IO;
+  typedef typename IO::raw raw;
+  constexpr int E = Stor<T>::E;
+  constexpr int KC = 4 * E;
+  constexpr int CH = CIN / E;  // 16-byte chunks per pixel
+  constexpr int KCHUNKS = (25 * CIN + KC - 1) / KC;
+  constexpr int HR = 2 * (TR - 1) + 5;
+  constexpr int ROW = S2PITCH * CH;
+  constexpr int TILE_CHUNKS = HR * ROW;
+  constexpr uint32_t ES = sizeof(T);
+  static_assert(KC % CIN == 0, "a K chunk spans whole taps");
+  __shared__ raw tile[TILE_CHUNKS];
+
+  // XCD-aware bijective remap (consecutive tiles along x share an XCD and its L2)
+  const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
+  int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tx = tt % tiles_x;
+  tt /= tiles_x;
+  const int ty = tt % tiles_y;
+  const int b = tt / tiles_y;
+  const int y0 = ty * TR, x0 = tx * S2W;
+  const int iy0 = 2 * y0 - 2, ix0 = 2 * x0 - 2;
+
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in0, (long long)a.B * a.Hi * a.Wi * CIN * ES);
+  const int pin0 = b * a.Hi * a.Wi;
+  stage_chunks<TILE_CHUNKS, 8>(tile, [&](int c) {
+    const int row = c / ROW, rem = c - row * ROW;
+    const int p = rem / CH, ch = rem - p * CH;
+    const int par = p >= S2HCP;
+    const int col = 2 * (p - par * S2HCP) + par;
+    const int iy = iy0 + row, ix = ix0 + col;
+    const bool ok = col < S2NC && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+    const uint32_t off = (uint32_t)(((pin0 + iy * a.Wi + ix) * CH + ch) * 16);
+    return IO::frag(rin, ok ? off : kOOB);
+  }, [](const raw& r) { return Frag2<T>::stage(r); });
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  f32x4_t acc[TR][MT];
+#pragma unroll
+  for (int j = 0; j < TR; ++j)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const raw* tl = tile + (wave * 16 + n) * CH;
+  const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + lane;
+  const int gi = (g * E) / CIN;      // tap sub-index of this lane group
+  const int gc = (g * E) % CIN / E;  // 16-byte channel chunk within the pixel
+  auto fetch = [&](int s, raw* xf, raw* wf) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) wf[m] = wp[(size_t)(s * a.MTtot + m) * 64];
+    const int kt = (s * KC) / CIN;
+    int off = s2_toff<CH>(kt);
+    if constexpr (KC / CIN > 1) off = gi == 1 ? s2_toff<CH>(kt + 1) : off;
+    if constexpr (KC / CIN > 2) {
+      off = gi == 2 ? s2_toff<CH>(kt + 2) : off;
+      off = gi == 3 ? s2_toff<CH>(kt + 3) : off;
+    }
+    // taps past the 25th (K padding) read a valid pixel against zero weights
+    const raw* src = tl + off + gc;
+#pragma unroll
+    for (int j = 0; j < TR; ++j) xf[j] = src[2 * j * ROW];
+  };
+  raw xa[TR], wa[MT];
+  fetch(0, xa, wa);
+#pragma unroll
+  for (int s = 0; s < KCHUNKS; ++s) {
+    raw xb[TR], wb[MT];
+    if (s + 1 < KCHUNKS) fetch(s + 1, xb, wb);
+#pragma unroll
+    for (int j = 0; j < TR; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) Frag2<T>::mma_staged(wa[m], xa[j], acc[j][m]);
+    if (s + 1 < KCHUNKS) {
+#pragma unroll
+      for (int j = 0; j < TR; ++j) xa[j] = xb[j];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) wa[m] = wb[m];
+    }
+  }
+
+  // epilogue (as conv2d_lds_kernel)
+  typedef typename IO::quad quad;
+  const int up = a.post_up, us = a.post_up >> 1;
+  const long long nout = (long long)a.B * a.Ho * a.Wo * a.cout;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout * ES);
+  const __amdgpu_buffer_rsrc_t rpre = make_rsrc(a.res_pre ? a.res_pre : a.out, a.res_pre ? nout * ES : 0);
+  const __amdgpu_buffer_rsrc_t rpost = make_rsrc(a.res_post ? a.res_post : a.out, a.res_post ? nout / (up * up) * ES : 0);
+  float bias[MT][4];
+  bool cok[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int co = m * 16 + g * 4;
+    cok[m] = co < a.cout;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[m][i] = a.bias[co + i];  // padded to cout_pad
+  }
+  const int ox = x0 + wave * 16 + n;
+#pragma unroll
+  for (int j = 0; j < TR; ++j) {
+    const int oy = y0 + j;
+    const bool vok = oy < a.Ho && ox < a.Wo;
+    const int pout = (b * a.Ho + oy) * a.Wo + ox;
+    const int ppost = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
+    quad qpre[MT], qpost[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const bool ok = vok && cok[m];
+      const int co = m * 16 + g * 4;
+      if (a.res_pre) qpre[m] = IO::ldq(rpre, ok ? (uint32_t)(pout * a.cout + co) * ES : kOOB);
+      if (a.res_post) qpost[m] = IO::ldq(rpost, ok ? (uint32_t)(ppost * a.cout + co) * ES : kOOB);
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      float r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = fmaf(acc[j][m][i], a.wscale, bias[m][i]);
+      if (a.res_pre) IO::addq(qpre[m], r);
+      if (a.relu) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = relu(r[i]);
+      }
+      if (a.res_post) IO::addq(qpost[m], r);
+      const uint32_t off = (uint32_t)(pout * a.cout + m * 16 + g * 4) * ES;
+      IO::stq(ro, vok && cok[m] ? off : kOOB, r);
+    }
+  }
+}
+
 // Halo-tiled implicit GEMM for the wide layers (Cin a multiple of KC, in_stride 1: GeoFeatureFusion's
 // stride-1 GeoBlock convs, k3/k5 decoders and the k5 s2 transposed decoders' phases). A block owns a
 // 4-row x 64-column tile of the q-grid for one phase and MT 16-channel output tiles; wave w owns
@@ -1595,6 +1743,39 @@ hipError_t launch_lds2(hipStream_t s, const Conv2dArgs& a, bool dry = false) {
 }
 
 
+// True when the layer is a 5x5 stride-2 padding-2 conv with dense row-major taps (one phase, one tensor input).
+bool lds_s2_ok(const Conv2dArgs& a) {
+  if (a.nphase != 1 || a.out_stride != 1 || a.in_stride != 2 || a.ph[0].ntaps != 25 || a.ngeo != 0 || a.c1 != 0 ||
+      a.xpair)
+    return false;
+  for (int t = 0; t < 25; ++t)
+    if (a.ph[0].tap[t][0] != t / 5 - 2 || a.ph[0].tap[t][1] != t % 5 - 2) return false;
+  return true;
+}
+
+template <typename T, int CIN, int MT, int TR>
+hipError_t launch_lds_s2_t(hipStream_t s, const Conv2dArgs& a) {
+  const int tx = (a.Wo + S2W - 1) / S2W, ty = (a.Ho + TR - 1) / TR;
+  const long long nt = (long long)tx * ty * a.B;
+  hipLaunchKernelGGL((conv2d_lds_s2_kernel<T, CIN, MT, TR>), dim3((unsigned)nt), dim3(256), 0, s, a, tx, ty, (int)nt);
+  return hipGetLastError();
+}
+
+// Returns hipErrorNotSupported when the stride-2 LDS variant does not take the layer (CIN 8 / 16, cout <= 32);
+// DAMVS_CONV2D_LDS_S2=0 (read per call) leaves those layers to the gather kernel. Tile rows: 4 (LDS <= 47 KB), 2 for
+// fp32 CIN 16 (59 KB).
+template <typename T>
+hipError_t launch_lds_s2(hipStream_t s, const Conv2dArgs& a, bool dry = false) {
+  const char* v = getenv("DAMVS_CONV2D_LDS_S2");
+  if ((v && v[0] == '0') || !lds_s2_ok(a) || a.MTtot > 2 || (a.c0 != 8 && a.c0 != 16)) return hipErrorNotSupported;
+  if (dry) return hipSuccess;
+  const bool m2 = a.MTtot == 2;
+  constexpr bool SP = sizeof(T) == 4;
+  if (a.c0 == 8) return m2 ? launch_lds_s2_t<T, 8, 2, 4>(s, a) : launch_lds_s2_t<T, 8, 1, 4>(s, a);
+  return m2 ? launch_lds_s2_t<T, 16, 2, SP ? 2 : 4>(s, a) : launch_lds_s2_t<T, 16, 1, SP ? 2 : 4>(s, a);
+}
+
+
 template <typename T, int MT, bool K32 = false>
 hipError_t launch_mt(hipStream_t s, const Conv2dArgs& a) {
   const long long Qtot = (long long)a.B * a.Hq * a.Wq;
@@ -1654,7 +1835,9 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
         if (e != hipErrorNotSupported) return e;
       }
       // the layers the 16-K route gives to the LDS-tiled kernels stay there (thin 3x3 layers, 16-channel slices)
-      if (launch_lds2<T>(s, a, true) == hipSuccess || launch_halo<T>(s, a, true) == hipSuccess) return hipErrorNotSupported;
+      if (launch_lds2<T>(s, a, true) == hipSuccess || launch_lds_s2<T>(s, a, true) == hipSuccess ||
+          launch_halo<T>(s, a, true) == hipSuccess)
+        return hipErrorNotSupported;
       return launch_gather32<T>(s, a);
     }
     return hipErrorInvalidValue;
@@ -1672,6 +1855,8 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
   }
   {
     hipError_t e = launch_lds2<T>(s, a);
+    if (e != hipErrorNotSupported) return e;
+    e = launch_lds_s2<T>(s, a);
     if (e != hipErrorNotSupported) return e;
     e = launch_halo<T>(s, a);
     if (e != hipErrorNotSupported) return e;

@@ -71,6 +71,11 @@ CASES = [
     # 64-channel block at input stride 2 (2 x 64 q-tiles, 32-column waves): GeoBlock conv1 32+32+g -> 64, 32+g -> 64
     (False, 3, 2, 1, 0, 32, 32, (64,), 64, True, False, 0, (37, 151)),
     (False, 3, 2, 1, 0, 32, 0, (32,), 64, True, True, 0, (64, 130)),
+    # stride-2 5x5 LDS kernel (FeatureNet conv1.0 / conv2.0): ragged tiles, odd sizes, residual, cout 16 / 32
+    (False, 5, 2, 2, 0, 8, 0, (), 16, True, False, 0, (70, 262)),
+    (False, 5, 2, 2, 0, 16, 0, (), 32, True, False, 0, (37, 151)),
+    (False, 5, 2, 2, 0, 16, 0, (), 16, False, True, 0, (30, 66)),
+    (False, 5, 2, 2, 0, 8, 0, (), 32, True, True, 0, (9, 17)),
 ]
 
 
