@@ -144,24 +144,27 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
   const int ty = tid / kTX, tx = tid % kTX;
   const int y0 = blockIdx.y * kTY, x0 = blockIdx.x * kTX;
   const int b = blockIdx.z;
-  const T* fb = feat + (size_t)b * D * h * w * CB;
-  raw regs[PER_T];
-  auto gload = [&](int pl) {
+  // this thread's staged chunks: byte offset inside a plane (kOOB: outside the image or past the tile), the same for every
+  // plane; buffer loads over the sample's volume return zeros for kOOB (no branch, no 64-bit address math per plane)
+  const __amdgpu_buffer_rsrc_t rv = make_rsrc(feat + (size_t)b * D * h * w * CB, (long long)D * h * w * CB * sizeof(T));
+  const uint32_t pstride = (uint32_t)(h * w * CB * sizeof(T));
+  uint32_t voff[PER_T];
 #pragma unroll
-    for (int k = 0; k < PER_T; ++k) {
-      const int c = tid + k * 256;
-      raw v;
-      if constexpr (sizeof(T) == 4) v = make_float4(0.f, 0.f, 0.f, 0.f); else v = make_uint4(0u, 0u, 0u, 0u);
-      if (c < TILE_CHUNKS) {
-        const int vox = c / CH, part = c % CH;
-        const int yy = y0 - 1 + vox / kHX, xx = x0 - 1 + vox % kHX;
-        if (yy >= 0 && yy < h && xx >= 0 && xx < w)
-          v = *reinterpret_cast<const raw*>(fb + (((size_t)pl * h + yy) * w + xx) * CB + part * E);
-      }
-      regs[k] = v;
-    }
+  for (int k = 0; k < PER_T; ++k) {
+    const int c = tid + k * 256;
+    const int vox = c / CH, part = c % CH;
+    const int yy = y0 - 1 + vox / kHX, xx = x0 - 1 + vox % kHX;
+    const bool ok = c < TILE_CHUNKS && yy >= 0 && yy < h && xx >= 0 && xx < w;
+    voff[k] = ok ? (uint32_t)(((yy * w + xx) * CB + part * E) * sizeof(T)) : kOOB;
+  }
+  raw regs[PER_T];
+  auto gload = [&](int pl, raw (&regs)[PER_T]) {
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k)
+      regs[k] = __builtin_bit_cast(raw, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rv, voff[k] == kOOB ? kOOB : voff[k] + (uint32_t)pl * pstride, 0, 0));
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, const raw (&regs)[PER_T]) {
 #pragma unroll
     for (int k = 0; k < PER_T; ++k) {
       const int c = tid + k * 256;
@@ -181,12 +184,14 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
     }
   };
 
-  gload(0);
-  lstore(0);
-  __syncthreads();
   float am1 = 0.f, a0 = 0.f;
+  // plane pl's conv from LDS buffer pl & 1, plane pl + 1 loaded meanwhile (two planes ahead measured flat at fp32:
+  // profiles/r06/ab_prob_r06q)
+  gload(0, regs);
+  lstore(0, regs);
+  __syncthreads();
   for (int pl = 0; pl < D; ++pl) {
-    if (pl + 1 < D) gload(pl + 1);
+    if (pl + 1 < D) gload(pl + 1, regs);
     const float4* tb = tile + (pl & 1) * FQ * NVOX + ty * kHX + tx;
     // even / odd channel partial sums per kernel depth (scalar FMAs: k_regress.hip is built without packed-FP32 ops)
     float c0e = 0.f, c0o = 0.f, c1e = 0.f, c1o = 0.f, c2e = 0.f, c2o = 0.f;
@@ -228,7 +233,7 @@ __global__ __launch_bounds__(256) void prob_regress_kernel(int B, int D, int h, 
     }
     am1 = a0 + s1;
     a0 = s0;
-    if (pl + 1 < D) lstore((pl + 1) & 1);
+    if (pl + 1 < D) lstore((pl + 1) & 1, regs);
     __syncthreads();
   }
   if (TWO) {
@@ -521,6 +526,7 @@ hipError_t launch_pr_t(hipStream_t s, int B, int D, int h, int w, const void* fe
                        const float* prob_init, const float* hyps, float* depth, float* conf, float* var, float* prob) {
   const size_t smem = prob_regress_smem<T, CB>(D);
   if (smem > 160 * 1024) return hipErrorInvalidValue;
+  if ((long long)D * h * w * CB * (long long)sizeof(T) >= (1LL << 31)) return hipErrorInvalidValue;  // 32-bit offsets
   auto k = prob_regress_kernel<T, CB, false>;
   if (smem > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -537,6 +543,7 @@ template <typename T, int CB>
 hipError_t launch_pc_lds(hipStream_t s, int B, int D, int h, int w, const void* feat, const float* wprob,
                          const float* prob_init, float* logits) {
   const size_t smem = prob_regress_smem<T, CB>(0);
+  if ((long long)D * h * w * CB * (long long)sizeof(T) >= (1LL << 31)) return hipErrorInvalidValue;  // 32-bit offsets
   dim3 grid((w + kTX - 1) / kTX, (h + kTY - 1) / kTY, B);
   hipLaunchKernelGGL((prob_regress_kernel<T, CB, true>), grid, dim3(256), smem, s, B, D, h, w,
                      reinterpret_cast<const T*>(feat), wprob, prob_init, nullptr, nullptr, nullptr, nullptr, logits);

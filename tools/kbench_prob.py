@@ -2,7 +2,7 @@
 MFMA form (default for bf16) against the VALU prob_regress_kernel (DAMVS_PROB_MFMA=0), with and without the
 prob-volume write. One JSON line per (stage, kernel, prob).
 
-    python tools/kbench_prob.py [iters]"""
+    python tools/kbench_prob.py [iters] [f32]     (f32: the fp32 parity path's storage)"""
 import json
 import os
 import sys
@@ -12,9 +12,11 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(iters=20):
+def main(iters=20, dt=None):
     import bench
     H, W, N, nd, dtype, _ = bench.CONFIGS["cfgC"]
+    if dt == "f32":
+        dtype = torch.float32
     dev = torch.device("cuda")
     net, _ = bench.build_model(nd, dtype, dev)
     B = 4
@@ -39,7 +41,7 @@ def main(iters=20):
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / iters
                 vox = B * D * h * w
-                alg = vox * 16 + vox * 4 + (vox * 4 if want_prob else 0) + 3 * B * h * w * 4
+                alg = vox * 8 * c0.element_size() + vox * 4 + (vox * 4 if want_prob else 0) + 3 * B * h * w * 4
                 print(json.dumps({"stage": s + 1, "D": D, "hw": [h, w], "B": B, "kernel": kern, "prob_write": want_prob,
                                   "ms": round(ms, 4), "alg_GBps": round(alg / ms / 1e6, 1),
                                   "hbm_frac": round(alg / ms / 1e6 / 8000, 3)}), flush=True)
@@ -47,4 +49,4 @@ def main(iters=20):
 
 
 if __name__ == "__main__":
-    main(*(int(a) for a in sys.argv[1:]))
+    main(*(int(a) if a.isdigit() else a for a in sys.argv[1:]))
