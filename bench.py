@@ -357,14 +357,14 @@ def parity_path(args, nd, device, imgs, proj, dv, ins, world, steps=20, warmup=3
     net, _ = build_model(nd, torch.float32, device, args.frontend)
     with torch.no_grad():
         for _ in range(warmup):
-            net(imgs, proj, dv, ins, streams=args.streams)
+            net(imgs, proj, dv, ins, **stream_kw(args))
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):  # the range status accumulates over the steps and is read once after them
-            net(imgs, proj, dv, ins, streams=args.streams, check_range=False)
+            net(imgs, proj, dv, ins, check_range=False, **stream_kw(args))
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
@@ -407,7 +407,8 @@ def parity_path(args, nd, device, imgs, proj, dv, ins, world, steps=20, warmup=3
              "algorithmic_flops": int(unet_flops),
              "peak_note": "split-f16 ceiling: every fp32 product is three f16 MFMAs, 2.5 PFLOP/s dense f16 / 3"}
     return {"value": round(maps / elapsed, 4), "unit": "depth maps/s", "ms_per_step": round(elapsed / steps * 1e3, 3),
-            "steps": steps, "warmup": warmup, "dtype": "f32", "streams": args.streams, "batch_per_gpu": args.batch,
+            "steps": steps, "warmup": warmup, "dtype": "f32", "streams": args.streams, "stream_offset": eff_offset(args, "f32"),
+            "batch_per_gpu": args.batch,
             "range_status": "ok: every stage of every timed forward finite (damvs_stage_status, read after the steps)",
             "compute": "fp32 storage, fp32 warp / aggregation / regression; every conv product as split-f16 MFMAs "
                        "(x = hi + lo, hi*hi + hi*lo + lo*hi, fp32 accumulation; damvsnet_amd/csrc/damvs_device.h)",
@@ -415,6 +416,23 @@ def parity_path(args, nd, device, imgs, proj, dv, ins, world, steps=20, warmup=3
                      "(tests/test_gpu_fullsize.py fp32 at cfgC/D/E, tests/test_gpu_parity.py stage-isolated), and the "
                      "end-to-end fp32-vs-fp64 conditioning gates (tests/test_gpu_parity.py _check_forward_e2e)",
             "roofline": roof, "mfma_roofline": mroof, "hot_path_roofline": hp, "mfma_utilisation": mf}
+
+
+def eff_offset(args, dname):
+    """The sub-batch stream offset a forward of this dtype runs with (CascadeMVSNet.forward stream_offset="auto")."""
+    if args.streams < 2:
+        return None
+    if args.stream_offset:
+        return None if args.stream_offset == "none" else args.stream_offset
+    return "stage1.hypotheses" if dname == "f32" else None
+
+
+def stream_kw(args):
+    """The forward's sub-batch stream arguments (the offset only when given)."""
+    kw = {"streams": args.streams}
+    if args.stream_offset:
+        kw["stream_offset"] = None if args.stream_offset == "none" else args.stream_offset
+    return kw
 
 
 def main():
@@ -426,6 +444,9 @@ def main():
     ap.add_argument("--batch", type=int, default=4,
                     help="depth maps (reference views) per GPU per step; default 4 = the reference's own "
                          "test batch (scripts/test.sh:25 --batch_size=4), SURVEY.md 8(d) 'B=4 for throughput'")
+    ap.add_argument("--stream-offset", default=None,
+                    help="start sub-batch i + 1 when sub-batch i reaches this stage-hook point (e.g. stage1.hypotheses, "
+                         "'none'); default: the model's (fp32: stage1.hypotheses, bf16: none)")
     ap.add_argument("--streams", type=int, default=2,
                     help="sub-batches of the per-GPU batch on concurrent HIP streams in the timed steps "
                          "(bitwise the one-stream result; ms_per_stage / rooflines come from a one-stream pass)")
@@ -494,13 +515,13 @@ def main():
         pp = parity_path(args, nd, device, imgs, proj, dv, ins, world)
     with torch.no_grad():
         for _ in range(args.warmup):
-            net(imgs, proj, dv, ins, streams=args.streams)
+            net(imgs, proj, dv, ins, **stream_kw(args))
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):  # the range status accumulates over the steps and is read once after them
-            net(imgs, proj, dv, ins, streams=args.streams, check_range=False)
+            net(imgs, proj, dv, ins, check_range=False, **stream_kw(args))
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
@@ -548,7 +569,7 @@ def main():
             "config": {"workload": "%s: %s" % (args.config, desc), "batch_per_gpu": args.batch,
                        "frontend": args.frontend,
                        "global_batch": args.batch * world, "height": H, "width": W, "views": N,
-                       "ndepths": list(nd), "streams": args.streams,
+                       "ndepths": list(nd), "streams": args.streams, "stream_offset": eff_offset(args, dname),
                        "parallelism": "replicas x%d (reference views sharded over ranks)" % world},
             "ms_per_stage": phases,
             "latency_b1": lat,

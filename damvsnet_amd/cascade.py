@@ -123,11 +123,14 @@ class CascadeMVSNet(nn.Module):
             _SIDE_STREAMS[key] = pool
         return pool[:n]
 
-    def _forward_streams(self, imgs, proj_matrices, depth_values, intrinsics_matrices, nstreams, check_range=True):
+    def _forward_streams(self, imgs, proj_matrices, depth_values, intrinsics_matrices, nstreams, check_range=True,
+                         offset=None):
         """The batch as ``nstreams`` sub-batches of reference views on concurrent HIP streams, merged along the
         batch. Per sample every kernel sees the same inputs as in one batch, so the outputs are bitwise those of
         the single-stream forward (tests/test_gpu_streams.py); the gain is overlap between kernels with different
-        bounds (one sub-batch's TA-bound warp beside another's HBM / MFMA-bound U-Net or front-end)."""
+        bounds (one sub-batch's TA-bound warp beside another's HBM / MFMA-bound U-Net or front-end).
+        ``offset``: a stage-hook name ("stage1.hypotheses", ...); sub-batch i + 1 then starts when sub-batch i reaches
+        that point of its forward (an event on its stream), so the sub-batches run different layers side by side."""
         B = imgs.shape[0]
         cut = [B * i // nstreams for i in range(nstreams + 1)]
         main = torch.cuda.current_stream(imgs.device)
@@ -139,11 +142,23 @@ class CascadeMVSNet(nn.Module):
 
         pool = self._side_streams(nstreams, imgs.device)
         outs = []
+        gate = None  # the previous sub-batch's event at `offset`
         for st, a, b in zip(pool, cut[:-1], cut[1:]):
             st.wait_stream(main)
+            if gate is not None:
+                st.wait_event(gate)
+            mark = {}
+
+            def hook(name, st=st, mark=mark):
+                if name == offset:
+                    mark["ev"] = torch.cuda.Event()
+                    mark["ev"].record(st)
+
             with torch.cuda.stream(st):
                 outs.append(self.forward(part(imgs, a, b), part(proj_matrices, a, b), part(depth_values, a, b),
-                                         part(intrinsics_matrices, a, b), check_range=False))
+                                         part(intrinsics_matrices, a, b), check_range=False,
+                                         stage_hook=hook if offset else None))
+            gate = mark.get("ev")
 
         # batch-sized outputs allocated on the main stream, each stream copying its rows right after its own
         # forward (the copies overlap the other sub-batches' kernels instead of following all of them)
@@ -180,19 +195,23 @@ class CascadeMVSNet(nn.Module):
         return full
 
     def forward(self, imgs, proj_matrices, depth_values, intrinsics_matrices=None, stage_hook=None, depthnet=None,
-                streams=1, check_range=True):
+                streams=1, check_range=True, stream_offset="auto"):
         """``depthnet``: optional stage runner (stage_idx, NHWC features, proj, hyps, cost_regularization) -> dict,
         e.g. sharded.DepthShardedDepthNet (one depth map over several GPUs); default: this model's DepthNet.
         ``streams`` > 1 runs the batch as that many sub-batches on concurrent streams (_forward_streams; not with
-        a stage hook or a custom stage runner). ``check_range``: after the last stage, read every stage's range
+        a stage hook or a custom stage runner; ``stream_offset``: see _forward_streams; "auto": "stage1.hypotheses" for
+        fp32 storage, none for bf16 -- the measured best, profiles/r06/ab_rs2_offset_r06t: fp32 102.4-102.7 ->
+        103.1-103.3 maps/s, bf16 205.6 -> 203.7). ``check_range``: after the last stage, read every stage's range
         status (damvs_stage_status, one host sync per forward) and raise damvsnet_amd._capi.DamvsRangeError if any
         depth / confidence / variance is non-finite. With a custom ``depthnet`` runner the range status is that
         runner's business: sharded.DepthShardedDepthNet runs the stage as split layer calls, which do not write a
         status word, so no DamvsRangeError is raised on that path."""
         if streams > 1 and imgs.shape[0] > 1 and stage_hook is None and depthnet is None and imgs.is_cuda \
                 and not self.refine:
+            if stream_offset == "auto":
+                stream_offset = "stage1.hypotheses" if self.compute_dtype == torch.float32 else None
             return self._forward_streams(imgs, proj_matrices, depth_values, intrinsics_matrices,
-                                         min(int(streams), imgs.shape[0]), check_range)
+                                         min(int(streams), imgs.shape[0]), check_range, stream_offset)
         if self.refine:
             raise NotImplementedError("refine=True: the reference RefineNet forward is not runnable "
                                       "(models/module.py:602 calls F.cat)")

@@ -101,9 +101,11 @@ def test_warp_beside_unet_layers_on_another_stream(dtype, s, layout, N):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("streams", [2, 4])
+@pytest.mark.parametrize("streams,offset", [(2, None), (4, None), (2, "stage1.hypotheses"), (4, "stage2.geofusion")])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_forward_sub_batches_on_streams_bitwise(streams, dtype):
+def test_forward_sub_batches_on_streams_bitwise(streams, offset, dtype):
+    """Sub-batches on concurrent streams (optionally each starting when the previous one reaches ``offset``) give the
+    one-stream forward's bits."""
     from damvsnet_amd.cascade import CascadeMVSNet
     net = CascadeMVSNet(ndepths=[48, 32, 8], compute_dtype=dtype,
                         frontend_dtype=torch.bfloat16 if dtype == torch.bfloat16 else None)
@@ -115,7 +117,7 @@ def test_forward_sub_batches_on_streams_bitwise(streams, dtype):
     with torch.no_grad():
         ref = net(imgs, proj, dv)
         for _ in range(3):
-            got = net(imgs, proj, dv, streams=streams)
+            got = net(imgs, proj, dv, streams=streams, stream_offset=offset)
             torch.cuda.synchronize()
             for st in ("stage1", "stage2", "stage3"):
                 for k in ("depth", "photometric_confidence", "variance", "prob_volume", "depth_values"):
