@@ -1041,8 +1041,10 @@ template <> struct WideForm<float> {
 // RS (fp32, input stride 1, 128-channel block, taps spanning <= 3 pixels, >= 4 taps per phase): the rolling K loop
 // below (A one chunk ahead, B of the next chunk read as each N-group's MFMAs finish, the next slice's halo in two
 // 8-channel pieces per tap for the first taps of a slice, one barrier per slice).
-template <typename T, bool TWO, int IS, int WM, bool RS = false>
-__global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1) : IS == 1 ? 3 : 2) void conv2d_wide_kernel(
+// R1 (fp32, input stride 2, 128-channel block): a 1 x 64 q-tile, the 4 waves a 2 x 2 grid (cout half, 32-column half):
+// a 390-pixel halo (50 KB) instead of the 2-row tile's 650 (83 KB), so two blocks share a CU.
+template <typename T, bool TWO, int IS, int WM, bool RS = false, bool R1 = false>
+__global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 || R1 ? 2 : 1) : IS == 1 ? 3 : 2) void conv2d_wide_kernel(
     const Conv2dArgs a, int tiles_x, int tiles_y, int nsl, int dmin, int span) {
   typedef uint4 raw;
   typedef WideForm<T> Fm;
@@ -1050,10 +1052,12 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
   static_assert(!RS || (SP && IS == 1 && WM == 2), "rolling K loop: fp32, input stride 1, 128-channel block");
   constexpr int PL = Fm::PL, SLOTS = Fm::SLOTS;
   constexpr uint32_t ES = sizeof(T);
-  constexpr int WPER = RS ? 5 : IS == 1 ? 7 : 11;  // 8-channel halo pieces per thread: up to 320 / 448 / 704 pixels
-  constexpr bool HALFW = WM == 1 && IS == 2;     // waves of 32 q-columns
+  static_assert(!R1 || (SP && IS == 2 && WM == 2), "one-row tile: fp32, input stride 2, 128-channel block");
+  // 8-channel halo pieces per thread: up to 320 / 448 / 448 / 704 pixels
+  constexpr int WPER = RS ? 5 : IS == 1 || R1 ? 7 : 11;
+  constexpr bool HALFW = (WM == 1 && IS == 2) || R1;  // waves of 32 q-columns
   constexpr int NGW = HALFW ? 2 : 4;             // 16-column N-groups per wave
-  constexpr int WRT = HALFW ? 2 : 4 / WM;        // q-tile rows
+  constexpr int WRT = R1 ? 1 : HALFW ? 2 : 4 / WM;  // q-tile rows
   constexpr int AR = WM * 256 * PL;        // 16-byte slots of one K chunk's A fragments (WM x 4 cout tiles)
   constexpr int NA = WM * PL;              // A loads per thread and chunk
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1080,7 +1084,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
   const int tx = tl % tiles_x, ty = (tl / tiles_x) % tiles_y, b = tl / (tiles_x * tiles_y);
   const int qy0 = ty * WRT, qx0 = tx * WC;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = WM == 2 ? wave >> 1 : 0, wn = WM == 2 ? wave & 1 : HALFW ? wave >> 1 : wave;
+  const int wm = WM == 2 ? wave >> 1 : 0, wn = R1 ? 0 : WM == 2 ? wave & 1 : HALFW ? wave >> 1 : wave;
   const int wc = HALFW ? (wave & 1) * 32 : 0;  // the wave's first q-column in the tile
   const int n = lane & 15, g = lane >> 4;
   const int mt0 = blockIdx.y * 4 * WM;
@@ -1624,12 +1628,12 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 4 ? (IS == 1 ? 2 : 1)
   }
 }
 
-template <typename T, int IS, int WM, bool RS = false>
+template <typename T, int IS, int WM, bool RS = false, bool R1 = false>
 hipError_t launch_wide_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span) {
   constexpr bool SP = sizeof(T) == 4;
-  constexpr int WRT = WM == 1 && IS == 2 ? 2 : 4 / WM, AR = WM * 256 * WideForm<T>::PL, SLOTS = WideForm<T>::SLOTS;
+  constexpr int WRT = R1 ? 1 : WM == 1 && IS == 2 ? 2 : 4 / WM, AR = WM * 256 * WideForm<T>::PL, SLOTS = WideForm<T>::SLOTS;
   const WideHalo<IS, WRT> hg(span);
-  constexpr int NHB = IS == 1 && !(SP && WM == 1) ? 2 : 1, WPER = RS ? 5 : IS == 1 ? 7 : 11;
+  constexpr int NHB = IS == 1 && !(SP && WM == 1) ? 2 : 1, WPER = RS ? 5 : IS == 1 || R1 ? 7 : 11;
   constexpr bool AG = SP || !(WM == 1 && IS == 2);  // A fragments from L1 / L2, no A buffers in LDS (the kernel's AG)
   if (hg.hp * 4 > WPER * 256) return hipErrorNotSupported;
   size_t below_plane = (AG ? 0 : 2 * (size_t)AR * 16) + NHB * (size_t)hg.hp * SLOTS * 16;
@@ -1642,7 +1646,7 @@ hipError_t launch_wide_t(hipStream_t s, const Conv2dArgs& a, int dmin, int span)
   if (smem > 160 * 1024) return hipErrorNotSupported;
   const long long nblk = (long long)tx * ty * a.B * a.nphase;
   const dim3 grid((unsigned)nblk, (unsigned)(a.MTtot / (4 * WM)));
-  auto k = a.c1 > 0 ? conv2d_wide_kernel<T, true, IS, WM, RS> : conv2d_wide_kernel<T, false, IS, WM, RS>;
+  auto k = a.c1 > 0 ? conv2d_wide_kernel<T, true, IS, WM, RS, R1> : conv2d_wide_kernel<T, false, IS, WM, RS, R1>;
   if (smem > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)smem);
@@ -1697,9 +1701,20 @@ hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
   const bool rs_off = rsv && rsv[0] == '0';
   int dmin = 0, span = 0;
   if (off || !wide_shape_ok(a, dmin, span)) return hipErrorNotSupported;
-  if (a.MTtot % 8) return a.in_stride == 1 ? launch_wide_t<T, 1, 1>(s, a, dmin, span) : launch_wide_t<T, 2, 1>(s, a, dmin, span);
+  if (a.MTtot % 8) {
+    // fp32 64-channel block at input stride 2 (32-column waves, one block per CU): the 32-K gather kernel is faster
+    // (kbench2d H 91.6 -> 63.5 us, profiles/r06/ab_wide_s2r1_r06x/)
+    if (sizeof(T) == 4 && a.in_stride == 2) return hipErrorNotSupported;
+    return a.in_stride == 1 ? launch_wide_t<T, 1, 1>(s, a, dmin, span) : launch_wide_t<T, 2, 1>(s, a, dmin, span);
+  }
   if constexpr (sizeof(T) == 4) {
     if (a.in_stride == 1 && span <= 3 && !rs_off) return launch_wide_t<T, 1, 2, true>(s, a, dmin, span);
+  }
+  if constexpr (sizeof(T) == 4) {
+    // the fp32 stride-2 128-channel block on one-row tiles (two blocks per CU): kbench2d E 120 -> 103 us, parity path
+    // 103.0 -> 103.2-103.6 maps/s (profiles/r06/ab_wide_s2r1_r06x/); DAMVS_WIDE_S2R1=0 (read per call) keeps 2-row tiles
+    const char* r1 = getenv("DAMVS_WIDE_S2R1");
+    if (a.in_stride == 2 && !(r1 && r1[0] == '0')) return launch_wide_t<T, 2, 2, false, true>(s, a, dmin, span);
   }
   return a.in_stride == 1 ? launch_wide_t<T, 1, 2>(s, a, dmin, span) : launch_wide_t<T, 2, 2>(s, a, dmin, span);
 }

@@ -424,6 +424,46 @@ def test_wide_rolling_loop_bitwise(case, monkeypatch):
     assert torch.equal(y_rs, y_ag)
 
 
+# fp32 stride-2 128-channel wide layers on one-row q-tiles (the default, conv2d_wide_kernel R1) against the 2-row tiles
+# (DAMVS_WIDE_S2R1=0): the same AG loop per accumulator, so bitwise equal. GeoBlock conv1 (two inputs + plane), 128+g -> 256, ragged.
+S2R1_CASES = [
+    (False, 3, 2, 1, 0, 128, 128, (256,), 256, True, False, 0, (37, 151)),
+    (False, 3, 2, 1, 0, 128, 0, (128,), 256, True, False, 0, (20, 24)),
+    (False, 3, 2, 1, 0, 64, 64, (0,), 128, False, True, 0, (30, 400)),
+]
+
+
+@pytest.mark.parametrize("case", S2R1_CASES, ids=[str(i) for i in range(len(S2R1_CASES))])
+def test_wide_s2_one_row_tiles_bitwise(case, monkeypatch):
+    from damvsnet_amd.frontend_hip import HipConv2d, planes
+    tr, k, s, p, op, c0, c1, geo, cout, relu, pre, post_up, (H, W) = case
+    g = torch.Generator().manual_seed(11)
+    B = 2
+    cin = c0 + c1 + len(geo)
+    conv = nn.Conv2d(cin, cout, k, stride=s, padding=p)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.2)
+        conv.bias.copy_(torch.randn(conv.bias.shape, generator=g) * 0.1)
+    tensor_at = [c for c in range(cin) if c not in geo]
+    at = dict(c0=c0, c0_at=tensor_at[0])
+    if c1:
+        at.update(c1=c1, c1_at=tensor_at[c0])
+    L = HipConv2d(conv, torch.float32, relu, geo_at=geo, **at)
+    a = torch.randn(B, H, W, c0, generator=g).to(DEV)
+    b = torch.randn(B, H, W, c1, generator=g).to(DEV) if c1 else None
+    gp = planes(torch.randn(B, len(geo), H, W, generator=g).to(DEV)) if geo else ()
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    rp = torch.randn(B, Ho, Wo, L.cout_store, generator=g).to(DEV) if pre else None
+    run = lambda: L(B, H, W, a, b, geo=gp, res_pre=rp)  # noqa: E731
+    monkeypatch.setenv("DAMVS_WIDE_S2R1", "0")
+    y2 = run()
+    monkeypatch.delenv("DAMVS_WIDE_S2R1")  # default: one-row tiles
+    y1 = run()
+    torch.cuda.synchronize()
+    assert torch.isfinite(y2).all()
+    assert torch.equal(y1, y2)
+
+
 # fp32 layers on the 32-K gather kernel (conv2d_mfma_kernel K32: 8 channels per lane and K step, 16x16x32 split-f16
 # MFMAs) against the 16-K form (DAMVS_CONV2D_G32=0): the same products summed in another order, so equal to fp32
 # rounding. FeatureNet's k5 s2 convs, the 1x1 GeoBlock downsamples (two inputs + plane, stride 2), the FPN inner conv
