@@ -48,6 +48,8 @@ CASES = {
     "Z4 dec 16->8 k5s2 full B=4": (True, 5, 2, 2, 1, 16, 0, 0, 8, True, 4, 592, 800, False, 1),
     "FA feat conv1.0 8->16 k5s2 x20": (False, 5, 2, 2, 0, 8, 0, 0, 16, True, 20, 1184, 1600, False, 0),
     "FB feat conv2.0 16->32 k5s2 x20": (False, 5, 2, 2, 0, 16, 0, 0, 32, True, 20, 592, 800, False, 0),
+    "FC feat conv1.1 16->16 k3 x20": (False, 3, 1, 1, 0, 16, 0, 0, 16, True, 20, 592, 800, False, 0),
+    "FD feat conv2.1 32->32 k3 x20": (False, 3, 1, 1, 0, 32, 0, 0, 32, True, 20, 296, 400, False, 0),
 }
 
 
