@@ -231,6 +231,30 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout * ES);
   const __amdgpu_buffer_rsrc_t rpre = make_rsrc(a.res_pre ? a.res_pre : a.out, a.res_pre ? nout * ES : 0);
   const __amdgpu_buffer_rsrc_t rpost = make_rsrc(a.res_post ? a.res_post : a.out, a.res_post ? nout / (up * up) * ES : 0);
+  if constexpr (XP && sizeof(T) == 4) {
+    // fp32: every lane owns the 4 channels (16 bytes) of output x = 2 qx + (g >> 1) in channel half g & 1 -- no shuffle,
+    // every lane loads its residuals and stores (bf16, below: 8-byte halves, so the even lane group takes the record)
+    const int ch = (g & 1) * 4;
+    float b4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b4[i] = a.bias[ch + i];
+#pragma unroll
+    for (int j = 0; j < kG2; ++j) {
+      float r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = fmaf(acc[j][0][i], a.wscale, b4[i]);
+      const bool ok = valid[j];
+      const uint32_t o = ok ? (uint32_t)(pout[j] * 8 + ch) * ES : kOOB;
+      if (a.res_pre) IO::addq(IO::ldq(rpre, o), r);
+      if (a.relu) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = relu(r[i]);
+      }
+      if (a.res_post) IO::addq(IO::ldq(rpost, ok ? (uint32_t)(ppost[j] * 8 + ch) * ES : kOOB), r);
+      IO::stq(ro, o, r);
+    }
+    return;
+  }
   if constexpr (XP) {
     const bool lead = (g & 1) == 0;
     float b8[8];

@@ -1597,19 +1597,20 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 2 ? 3 : 2) void decon
 
   auto step = [&](int qz, uint4 (*cur)[PL], uint4 (*nxt)[PL]) {
     if (qz + 2 < zend) load_plane(qz + 3, nxt);
-    // output offsets and the skip records of this plane's 8 outputs, loaded before the MFMAs
+    // output offsets and the skip records of this plane's 8 outputs, loaded before the MFMAs. bf16: lane group g (even)
+    // owns the whole 16-byte record of output x = 2 qx + (g >> 1) (its partner's 4 channels by a shuffle); fp32: every
+    // lane owns its 4 channels' 16 bytes (channel half g & 1), so all lanes load and store and no shuffle is needed
     uint32_t off[8];
-    uint4 rq[8][PL];
+    uint4 rq[8][1];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int pd = k >> 2, py = (k >> 1) & 1, r = k & 1;
       const int qy = qy0 + 2 * wave + r;
-      const bool ok = lead && qy < a.Hi && qx < a.Wi;
+      const bool ok = (PL == 2 || lead) && qy < a.Hi && qx < a.Wi;
       const int oz = 2 * qz + pd, oy = 2 * qy + py, ox = 2 * qx + (g >> 1);
-      off[k] = ok ? (uint32_t)((((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * 8) * (uint32_t)ES : kOOB;
-#pragma unroll
-      for (int h = 0; h < PL; ++h)  // zero when there is no skip tensor (empty range)
-        rq[k][h] = BufIO<bf16_t>::frag(rr, off[k] == kOOB ? kOOB : off[k] + 16u * h);
+      off[k] = ok ? (uint32_t)((((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * 8) * (uint32_t)ES + (PL == 2 ? 16u * (g & 1) : 0u)
+                  : kOOB;
+      rq[k][0] = BufIO<bf16_t>::frag(rr, off[k]);  // zero when there is no skip tensor (empty range)
     }
     const uint4* p0 = ring + (qz & 3) * PLANE + lbase;        // q-plane qz (z offset 0)
     const uint4* p1 = ring + ((qz + 1) & 3) * PLANE + lbase;  // q-plane qz + 1 (z offset +1)
@@ -1634,9 +1635,22 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 2 ? 3 : 2) void decon
               Z::mma(w, Z::bread(src + r * PW * S, lch, CH, lsw), acc[(pd * 2 + py) * 2 + r]);
           }
       }
-    // epilogue per output: partner channels, bias, ReLU, skip (after the ReLU), 16-byte store
+    // epilogue per output: (bf16: partner channels,) bias, ReLU, skip (after the ReLU), 16-byte store
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
+      if constexpr (PL == 2) {
+        const float4 f = __builtin_bit_cast(float4, rq[k][0]);
+        const float sk[4] = {f.x, f.y, f.z, f.w};
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = acc[k][i] * wsc + b8[(g & 1) * 4 + i];  // 2^-k: exact
+          if (a.relu) v[i] = relu(v[i]);
+          v[i] += sk[i];
+        }
+        BufIO<T>::stq(ro, off[k], v);
+        continue;
+      }
       float v[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -1650,14 +1664,6 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(sizeof(T) == 2 ? 3 : 2) void decon
           v[i] += b8[i];
           if (a.relu) v[i] = relu(v[i]);
           v[i] += __uint_as_float((i & 1) ? (q4[i >> 1] & 0xffff0000u) : (q4[i >> 1] << 16));
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float4 f = __builtin_bit_cast(float4, rq[k][i >> 2]);
-          v[i] = v[i] * wsc + b8[i];  // 2^-k: exact
-          if (a.relu) v[i] = relu(v[i]);
-          v[i] += (i & 3) == 0 ? f.x : (i & 3) == 1 ? f.y : (i & 3) == 2 ? f.z : f.w;
         }
       }
       if (lead) Vox8<T>::store(ro, off[k], v);
@@ -1776,18 +1782,20 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
     for (int pd = 0; pd < 2; ++pd) {
       // this half's 8 skip records (k = (py, px, r)): bf16 requested before its MFMAs; fp32 (twice the registers, beside
       // 27 A pairs) after them
+      // bf16: lead lanes own 8 channels (a 16-byte record, partner's 4 by a shuffle); fp32: every lane its own 4 channels
+      // co .. co + 3 (16 bytes), no shuffle
       uint32_t off[8];
-      uint4 rq[8][PL];
+      uint4 rq[8];
       auto skip_load = [&]() {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const int py = k >> 2, px = (k >> 1) & 1, r = k & 1;
           const int qy = qy0 + 2 * wave + r;
-          const bool ok = lead && qy < a.Hi && qx < a.Wi;
+          const bool ok = (PL == 2 || lead) && qy < a.Hi && qx < a.Wi;
           const int oz = 2 * qz + pd, oy = 2 * qy + py, ox = 2 * qx + px;
-          off[k] = ok ? (uint32_t)((((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * 16 + (co & 8)) * (uint32_t)ES : kOOB;
-#pragma unroll
-          for (int h = 0; h < PL; ++h) rq[k][h] = BufIO<bf16_t>::frag(rr, off[k] == kOOB ? kOOB : off[k] + 16u * h);
+          off[k] = ok ? (uint32_t)((((b * a.Do + oz) * a.Ho + oy) * a.Wo + ox) * 16 + (PL == 2 ? co : (co & 8))) * (uint32_t)ES
+                      : kOOB;
+          rq[k] = BufIO<bf16_t>::frag(rr, off[k]);
         }
       };
       if constexpr (PL == 1) skip_load();
@@ -1822,6 +1830,20 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
       if constexpr (PL == 2) skip_load();
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
+        if constexpr (PL == 2) {
+          const float4 f = __builtin_bit_cast(float4, rq[k]);
+          const float sk[4] = {f.x, f.y, f.z, f.w};
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[i] = acc[k][i] * wsc + b8[(co & 4) + i];  // 2^-k: exact
+            if (a.relu) v[i] = relu(v[i]);
+            v[i] += sk[i];
+          }
+          am_fold<T, 4>(am, off[k] != kOOB, v);
+          BufIO<T>::stq(ro, off[k], v);
+          continue;
+        }
         float v[8];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1829,20 +1851,12 @@ __global__ __launch_bounds__(256) DAMVS_WAVES(ALDS ? 2 : 1) void deconv_c16_zsli
           v[4 + i] = __shfl_down(acc[k][i], 16);
         }
         if constexpr (PL == 1) {
-          const uint32_t q4[4] = {rq[k][0].x, rq[k][0].y, rq[k][0].z, rq[k][0].w};
+          const uint32_t q4[4] = {rq[k].x, rq[k].y, rq[k].z, rq[k].w};
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             v[i] += b8[i];
             if (a.relu) v[i] = relu(v[i]);
             v[i] += __uint_as_float((i & 1) ? (q4[i >> 1] & 0xffff0000u) : (q4[i >> 1] << 16));
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const float4 f = __builtin_bit_cast(float4, rq[k][i >> 2]);
-            v[i] = v[i] * wsc + b8[i];  // 2^-k: exact
-            if (a.relu) v[i] = relu(v[i]);
-            v[i] += (i & 3) == 0 ? f.x : (i & 3) == 1 ? f.y : (i & 3) == 2 ? f.z : f.w;
           }
         }
         if (lead) {
