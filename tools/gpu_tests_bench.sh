@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-6 GPU pass: TESTS (pytest files, "" skips; K = a -k expression), then (BENCH=1) the default bench line.
+# GPU pass: TESTS (pytest files, "" skips; K = a -k expression), then (BENCH=1) the default bench line.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R && mkdir -p gpurun_out/r06
 TAG=${TAG:-r06}
 if [ -n "${TESTS-}" ]; then
