@@ -87,6 +87,7 @@ __device__ __forceinline__ void mma_split32(const F16Pair& w, const F16Pair& x, 
 struct Prescale {
   float s, inv;  // x * s is split; the accumulator is scaled back by inv (= 1 / s)
 };
+__device__ __forceinline__ Prescale prescale_from_max(unsigned m);
 // max of a slot's replicas (every lane of the wave must be active: each of the first kAmaxReps lanes loads one)
 __device__ __forceinline__ Prescale prescale_of(const unsigned* __restrict__ amax) {
   if (!amax) return Prescale{1.f, 1.f};
@@ -94,7 +95,10 @@ __device__ __forceinline__ Prescale prescale_of(const unsigned* __restrict__ ama
   unsigned m = lane < kAmaxReps ? __hip_atomic_load(amax + lane * kAmaxStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
 #pragma unroll
   for (int o = 32; o; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
-  m = __builtin_amdgcn_readfirstlane(m);
+  return prescale_from_max(__builtin_amdgcn_readfirstlane(m));
+}
+// the scale of a tensor whose max |x| has the bit pattern m (uniform)
+__device__ __forceinline__ Prescale prescale_from_max(unsigned m) {
   if (m == 0u) return Prescale{1.f, 1.f};  // an all-zero tensor
   int e = (int)((m >> 23) & 0xff) - 127;  // floor(log2(max)); subnormal maxima count as 2^-127, NaN / inf as 2^128
   int k = 13 - (e < -127 ? -127 : e);

@@ -368,12 +368,65 @@ def test_planes_four_columns_bitwise(k, ng, relu, pre, monkeypatch):
     gp = planes(torch.randn(B, ng, H, W, generator=g).to(DEV))
     res = torch.randn(B, H, W, cout, generator=g).to(DEV, torch.bfloat16) if pre else None
     L = HipConv2d(conv, torch.bfloat16, relu, geo_at=tuple(range(ng)), c0=0, c1=0, c1_at=0)
+    monkeypatch.setenv("DAMVS_PLANES_MFMA", "0")  # the VALU kernels (the MFMA form takes these layers by default)
     outs = []
     for flag in ("1", "0"):
         monkeypatch.setenv("DAMVS_PLANES4", flag)
         outs.append(L(B, H, W, None, None, geo=gp, res_pre=res).clone())
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+# The plane-only layers on split-f16 MFMAs (conv2d_planes_mfma_kernel, the default for cout 4 / 8 at Wi % 4 == 0) against
+# float64 F.conv2d and against the VALU kernels (DAMVS_PLANES_MFMA=0): FeatureNet's RGB conv (3x3, 3 planes), GeoFF's
+# RGB+depth (5x5, 4) and depth+depth (5x5, 2) init convs, 1 plane, cout 4; ragged 16 x 64 tiles (H 37 / 21, W 200 / 36),
+# residuals before / after ReLU; plane magnitudes from 1e-6 to 3e4 (the block prescale keeps both f16 pieces normal).
+PLANES_MFMA_CASES = [
+    (3, 3, 8, True, False, 0, (37, 200), 1.0),
+    (5, 4, 8, True, False, 0, (21, 36), 1.0),
+    (5, 2, 8, True, True, 0, (37, 200), 1.0),
+    (5, 1, 4, False, False, 2, (22, 68), 1.0),
+    (3, 3, 8, True, False, 0, (16, 64), 3e4),
+    (5, 4, 8, False, False, 0, (21, 36), 1e-6),
+]
+
+
+@pytest.mark.parametrize("case", PLANES_MFMA_CASES, ids=[str(i) for i in range(len(PLANES_MFMA_CASES))])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_planes_mfma_vs_fp64_and_valu(case, dtype, monkeypatch):
+    from damvsnet_amd.frontend_hip import HipConv2d, planes
+    k, ng, cout, relu, pre, post_up, (H, W), mag = case
+    g = torch.Generator().manual_seed(11 * k + ng + cout)
+    B = 2
+    conv = nn.Conv2d(ng, cout, k, padding=k // 2)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.2)
+        conv.bias.copy_(torch.randn(conv.bias.shape, generator=g) * 0.1 * mag)
+    x = torch.randn(B, ng, H, W, generator=g) * mag
+    gp = planes(x.to(DEV))
+    res = torch.randn(B, H, W, cout, generator=g) * mag if pre else None
+    post = torch.randn(B, H // max(post_up, 1), W // max(post_up, 1), cout, generator=g) * mag if post_up else None
+    if dtype == torch.bfloat16:
+        res = res.to(dtype).float() if res is not None else None
+        post = post.to(dtype).float() if post is not None else None
+    with torch.no_grad():
+        ref = F.conv2d(x.double(), conv.weight.double(), conv.bias.double(), padding=k // 2).permute(0, 2, 3, 1)
+    ref = ref + res.double() if res is not None else ref
+    ref = F.relu(ref) if relu else ref
+    if post is not None:
+        ref = ref + F.interpolate(post.double().permute(0, 3, 1, 2), scale_factor=post_up, mode="nearest").permute(0, 2, 3, 1)
+    L = HipConv2d(conv, dtype, relu, geo_at=tuple(range(ng)), c0=0, c1=0, c1_at=0)
+    run = lambda: L(B, H, W, None, None, geo=gp, res_pre=res.to(DEV, dtype) if res is not None else None,
+                    res_post=post.to(DEV, dtype) if post is not None else None, post_up=max(post_up, 1)).clone()
+    got = run()
+    monkeypatch.setenv("DAMVS_PLANES_MFMA", "0")
+    valu = run()
+    torch.cuda.synchronize()
+    got, valu = got.double().cpu()[..., :cout], valu.double().cpu()[..., :cout]
+    e64, ev = rel_max(got.numpy(), ref.numpy()), rel_max(got.numpy(), valu.numpy())
+    print("planes mfma %s k%d ng%d mag %g: vs fp64 %.2e, vs VALU %.2e" % (dtype, k, ng, mag, e64, ev))
+    tol = 2e-6 if dtype == torch.float32 else 1e-2
+    assert e64 < tol and ev < (tol if dtype == torch.float32 else 1e-2)
 
 
 # fp32 wide layers on the rolling K loop (conv2d_wide_kernel RS) against the AG loop (DAMVS_WIDE_RS=0): the same MFMA
