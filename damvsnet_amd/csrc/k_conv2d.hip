@@ -316,13 +316,18 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) == 2 && MT == 4 && !TWO
   }
 }
 
-// LDS-staged variant for the thin stride-1 3x3 layers (one tensor input of CIN <= 32 channels, no
-// fp32 plane): the full-resolution FeatureNet / GeoFeatureFusion convs that the global-gather
+// LDS-staged variant for the thin stride-1 3x3 layers (one tensor input of CIN <= 32 channels, at most
+// one fp32 plane): the full-resolution FeatureNet / GeoFeatureFusion convs that the global-gather
 // kernel runs TA-bound (each input pixel is fetched by 9 taps through L1). A block owns an
 // 8-row x 64-column output tile; its (8+2) x (64+2) x CIN halo is read once with 16-byte loads
 // (zero padding by range-checked buffer loads) and every B fragment is a ds_read_b128. Wave w owns
 // columns [16w, 16w+16), group j output row j. For CIN < KC a K chunk spans KC/CIN taps; the
 // per-lane tap offsets are compile-time constants once the K loop unrolls (see conv3d_lds_kernel).
+// Round 6: the GeoBlock convs' depth plane (cat(g, y) / cat(x, g): 16+g -> 16 / 32 at half resolution, which ran on
+// the gather kernel at 0.2-0.3 of their HBM roofline) as the gather kernel's trailing K chunk (one value per tap,
+// rounded to the compute type), its (8+2) x (64+2) fp32 halo staged beside the tensor halo: the same MFMA sequence
+// per accumulator as the gather kernel (chunks in packed order, then the plane chunk), so bitwise its results. bf16
+// only: GeoFF stage 3 5.18 -> 4.99 ms, bench 205.9 -> 208.5 maps/s in one call (profiles/r06/ab_lds_plane).
 constexpr int L2H = 8, L2W = 64, L2HH = L2H + 2, L2HW = L2W + 2;
 
 template <int CH>
@@ -343,6 +348,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) != 2 ? 1 : CIN == 32 ? 
   constexpr uint32_t ES = sizeof(T);
   static_assert(KC % CIN == 0 || CIN % KC == 0, "chunking");
   __shared__ raw tile[TILE_CHUNKS];
+  __shared__ float ptile[L2HH * L2HW];  // the plane's halo (a.ngeo == 1)
 
   // XCD-aware bijective remap (consecutive tiles along x share an XCD and its L2)
   const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
@@ -361,6 +367,16 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) != 2 ? 1 : CIN == 32 ? 
     const uint32_t off = (uint32_t)(((pin0 + iy * a.Wi + x0 - 1) * CH + col) * 16);
     return IO::frag(rin, ok ? off : kOOB);
   }, [](const raw& r) { return Frag2<T>::stage(r); });
+  if (a.ngeo) {
+    const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.geo[0], ((long long)(a.B - 1) * a.geo_bstride[0] + (long long)a.Hi * a.Wi) * 4);
+    const int pg0 = b * (int)a.geo_bstride[0];
+    for (int p = threadIdx.x; p < L2HH * L2HW; p += 256) {
+      const int row = p / L2HW, col = p - row * L2HW;
+      const int iy = y0 - 1 + row, ix = x0 - 1 + col;
+      const bool ok = (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+      ptile[p] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, ok ? (uint32_t)(pg0 + iy * a.Wi + ix) * 4u : kOOB, 0, 0));
+    }
+  }
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -405,6 +421,25 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) != 2 ? 1 : CIN == 32 ? 
       for (int j = 0; j < L2H; ++j) xa[j] = xb[j];
 #pragma unroll
       for (int m = 0; m < MT; ++m) wa[m] = wb[m];
+    }
+  }
+  if (a.ngeo) {  // the plane chunk (packed after the tensor chunks): lane group g holds taps g E .. g E + E - 1
+    static_assert(9 <= KC, "one plane chunk");
+    raw wg[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) wg[m] = wp[(size_t)(KCHUNKS * a.MTtot + m) * 64];
+    const float* pt = ptile + wave * 16 + n;
+#pragma unroll
+    for (int j = 0; j < L2H; ++j) {
+      float v[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int t = g * E + e;
+        v[e] = t < 9 ? pt[(j + t / 3) * L2HW + t % 3] : 0.f;
+      }
+      const raw x = pack_vals<T>(v);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) Frag2<T>::mma(wg[m], x, acc[j][m]);
     }
   }
 
@@ -1745,8 +1780,12 @@ hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
 
 // True when the layer is a plain 3x3 stride-1 padding-1 conv with dense row-major taps.
 bool lds3_ok(const Conv2dArgs& a) {
-  if (a.nphase != 1 || a.out_stride != 1 || a.in_stride != 1 || a.ph[0].ntaps != 9 || a.ngeo != 0 || a.c1 != 0 ||
-      a.Ho != a.Hi || a.Wo != a.Wi)
+  // at most one plane, next to at most 16 channels (the layers the gather kernel ran; 32+g goes to the halo kernel);
+  // DAMVS_CONV2D_LDS_PLANE=0 (read per call): planes stay on the gather kernel
+  const char* pv = getenv("DAMVS_CONV2D_LDS_PLANE");
+  const int maxg = (pv && pv[0] == '0') || a.c0 > 16 ? 0 : 1;
+  if (a.nphase != 1 || a.out_stride != 1 || a.in_stride != 1 || a.ph[0].ntaps != 9 || a.ngeo > maxg || a.c1 != 0 ||
+      a.Ho != a.Hi || a.Wo != a.Wi || (a.ngeo && a.ph[0].gchunks != 1))
     return false;
   for (int t = 0; t < 9; ++t)
     if (a.ph[0].tap[t][0] != t / 3 - 1 || a.ph[0].tap[t][1] != t % 3 - 1) return false;
@@ -1768,7 +1807,9 @@ hipError_t launch_lds2(hipStream_t s, const Conv2dArgs& a, bool dry = false) {
     const char* v = getenv("DAMVS_CONV2D_NO_LDS");
     return v && v[0] == '1';
   }();
-  if (off || !lds3_ok(a) || a.MTtot > 2 || (sizeof(T) == 4 && a.c0 > 16)) return hipErrorNotSupported;  // LDS <= 42 KB
+  // fp32 layers with a plane stay on the 32-K gather kernel (kbench J 27.8 against 31.2 us on the 16-K LDS form; bench
+  // flat, profiles/r06/ab_lds_plane)
+  if (off || !lds3_ok(a) || a.MTtot > 2 || (sizeof(T) == 4 && (a.c0 > 16 || a.ngeo))) return hipErrorNotSupported;  // LDS <= 42 KB
   if (dry) return a.c0 == 8 || a.c0 == 16 || (sizeof(T) == 2 && a.c0 == 32) ? hipSuccess : hipErrorNotSupported;
   const int MT = a.MTtot;
   switch (a.c0) {

@@ -71,6 +71,10 @@ CASES = [
     # 64-channel block at input stride 2 (2 x 64 q-tiles, 32-column waves): GeoBlock conv1 32+32+g -> 64, 32+g -> 64
     (False, 3, 2, 1, 0, 32, 32, (64,), 64, True, False, 0, (37, 151)),
     (False, 3, 2, 1, 0, 32, 0, (32,), 64, True, True, 0, (64, 130)),
+    # LDS-tiled 3x3 kernel with the GeoBlock depth plane (round 6): cat(g, y) 16+g -> 16, cat(x, g) 16+g -> 32, ragged
+    (False, 3, 1, 1, 0, 16, 0, (0,), 16, True, True, 0, (37, 151)),
+    (False, 3, 1, 1, 0, 16, 0, (16,), 32, True, False, 0, (20, 70)),
+    (False, 3, 1, 1, 0, 8, 0, (8,), 16, False, False, 2, (22, 64)),
     # stride-2 5x5 LDS kernel (FeatureNet conv1.0 / conv2.0): ragged tiles, odd sizes, residual, cout 16 / 32
     (False, 5, 2, 2, 0, 8, 0, (), 16, True, False, 0, (70, 262)),
     (False, 5, 2, 2, 0, 16, 0, (), 32, True, False, 0, (37, 151)),
@@ -373,6 +377,42 @@ def test_planes_four_columns_bitwise(k, ng, relu, pre, monkeypatch):
     for flag in ("1", "0"):
         monkeypatch.setenv("DAMVS_PLANES4", flag)
         outs.append(L(B, H, W, None, None, geo=gp, res_pre=res).clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
+# The LDS-tiled 3x3 kernel with a depth plane (conv2d_lds_kernel, round 6) against the gather kernel it replaces
+# (DAMVS_CONV2D_LDS_PLANE=0): the same MFMA sequence per accumulator (tensor chunks, then the plane chunk), so bitwise
+# equal in bf16 (fp32: the gather kernel is the 32-K form, compared against torch in test_conv2d_layer_vs_torch).
+LDS_PLANE_CASES = [
+    (16, (0,), 16, True, True, 0, (37, 151)),   # GeoBlock conv2: cat(g2, y) 16+g -> 16, identity residual
+    (16, (16,), 32, True, False, 0, (20, 70)),  # GeoBlock conv1 at stride 1: cat(x, g1) 16+g -> 32
+    (8, (8,), 16, False, False, 2, (22, 64)),   # 8+g -> 16, upsampled residual after ReLU
+]
+
+
+@pytest.mark.parametrize("case", LDS_PLANE_CASES, ids=[str(i) for i in range(len(LDS_PLANE_CASES))])
+def test_lds_plane_bitwise_vs_gather(case, monkeypatch):
+    from damvsnet_amd.frontend_hip import HipConv2d, planes
+    c0, geo, cout, relu, pre, post_up, (H, W) = case
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(c0 * 7 + cout + H)
+    B, cin = 2, c0 + 1
+    conv = nn.Conv2d(cin, cout, 3, padding=1)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.2)
+        conv.bias.copy_(torch.randn(conv.bias.shape, generator=g) * 0.1)
+    x = nhwc(torch.randn(B, c0, H, W, generator=g)).to(DEV, dt)
+    gp = planes(torch.randn(B, 1, H, W, generator=g).to(DEV))
+    tensor_at = [c for c in range(cin) if c not in geo]
+    L = HipConv2d(conv, dt, relu, geo_at=geo, c0=c0, c0_at=tensor_at[0])
+    res = torch.randn(B, H, W, L.cout_store, generator=g).to(DEV, dt) if pre else None
+    post = torch.randn(B, H // max(post_up, 1), W // max(post_up, 1), L.cout_store, generator=g).to(DEV, dt) \
+        if post_up else None
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DAMVS_CONV2D_LDS_PLANE", flag)
+        outs.append(L(B, H, W, x, None, geo=gp, res_pre=res, res_post=post, post_up=max(post_up, 1)).clone())
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
 
