@@ -491,6 +491,101 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) != 2 ? 1 : CIN == 32 ? 
   }
 }
 
+// LDS-staged x-pair transposed conv (bf16, round 6): the 16 -> 8 channel stride-2 ConvTranspose layers whose two
+// x-pair phases (build_phases_xpair: py = 0, 1; MFMA row r = (x parity r >> 3, channel r & 7)) read input offsets
+// -1 .. 1 -- GeoFeatureFusion's full-resolution k5 s2 decoders, which the x-pair gather kernel ran at ~0.2 of their
+// HBM roofline (each input pixel fetched through L1 by every tap of both phases). A block owns 8 x 64 input-grid
+// positions for BOTH phases: its (8+2) x (64+2) x 16-channel halo is read once (as conv2d_lds_kernel's), each phase's
+// taps are looked up per lane and chunk from the phase's tap list (K entry s KC + g E = tap t, channel half), and the
+// epilogue is the x-pair gather kernel's (lane group g + 1 hands its 4 channels to g; residuals, ReLU, 16-byte
+// records). Per phase and accumulator the same MFMA sequence as the gather kernel (chunks in packed order, padding taps
+// as zeros), so bitwise its results.
+__global__ __launch_bounds__(256) void conv2d_xpair_lds_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int ntiles) {
+  typedef BufIO<bf16_t> IO;
+  typedef typename IO::raw raw;
+  constexpr int E = 8, KC = 32, CH = 2;  // 16 channels: two 16-byte chunks per pixel
+  constexpr int ROW = L2HW * CH;
+  constexpr int TILE_CHUNKS = L2HH * ROW;
+  constexpr uint32_t ES = 2;
+  __shared__ raw tile[TILE_CHUNKS];
+  __shared__ int s_toff[2][16];  // per phase: tap t's halo offset in 16-byte chunks (-1: padding tap)
+
+  const int bid = blockIdx.x, q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
+  int tt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tx = tt % tiles_x; tt /= tiles_x;
+  const int ty = tt % tiles_y;
+  const int b = tt / tiles_y;
+  const int y0 = ty * L2H, x0 = tx * L2W;
+  if (threadIdx.x < 32) {
+    const int p = threadIdx.x >> 4, t = threadIdx.x & 15;
+    s_toff[p][t] = t < a.ph[p].ntaps ? ((a.ph[p].tap[t][0] + 1) * L2HW + a.ph[p].tap[t][1] + 1) * CH : -1;
+  }
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in0, (long long)a.B * a.Hi * a.Wi * 16 * ES);
+  const int pin0 = b * a.Hi * a.Wi;
+  stage_chunks<TILE_CHUNKS, 8>(tile, [&](int c) {
+    const int row = c / ROW, col = c - row * ROW;
+    const int iy = y0 - 1 + row, ix = x0 - 1 + col / CH;
+    const bool ok = (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+    const uint32_t off = (uint32_t)(((pin0 + iy * a.Wi + x0 - 1) * CH + col) * 16);
+    return IO::frag(rin, ok ? off : kOOB);
+  }, [](const raw& r) { return r; });
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const raw* tl = tile + (wave * 16 + n) * CH + (g & 1);  // the lane's column and channel half
+  const long long nout = (long long)a.B * a.Ho * a.Wo * 8;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout * ES);
+  const __amdgpu_buffer_rsrc_t rpre = make_rsrc(a.res_pre ? a.res_pre : a.out, a.res_pre ? nout * ES : 0);
+  const int up = a.post_up, us = a.post_up >> 1;
+  const __amdgpu_buffer_rsrc_t rpost = make_rsrc(a.res_post ? a.res_post : a.out, a.res_post ? nout / (up * up) * ES : 0);
+  float b8[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b8[i] = a.bias[i];
+  const int qx = x0 + wave * 16 + n;
+#pragma unroll 1
+  for (int p = 0; p < 2; ++p) {
+    const Conv2dPhase& ph = a.ph[p];
+    const raw* __restrict__ wp = reinterpret_cast<const raw*>(a.wpack) + (size_t)ph.w_off * 64 + lane;  // MTtot 1
+    f32x4_t acc[L2H];
+#pragma unroll
+    for (int j = 0; j < L2H; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < ph.kchunks; ++s) {
+      const raw w = wp[(size_t)s * 64];
+      const int off = s_toff[p][(s * KC + g * E) >> 4];  // 16 channels a tap: lane group g holds tap 2 s + (g >> 1)
+      raw x[L2H];
+#pragma unroll
+      for (int j = 0; j < L2H; ++j) x[j] = off >= 0 ? tl[off + j * ROW] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int j = 0; j < L2H; ++j) Frag2<bf16_t>::mma(w, x[j], acc[j]);
+    }
+    // epilogue (the x-pair gather kernel's): output x = 2 qx + (g >> 1), y = 2 qy + py
+    const bool lead = (g & 1) == 0;
+    const int ox = 2 * qx + (g >> 1);
+#pragma unroll
+    for (int j = 0; j < L2H; ++j) {
+      float r[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        r[i] = fmaf(acc[j][i], a.wscale, b8[i]);
+        r[4 + i] = fmaf(__shfl_down(acc[j][i], 16), a.wscale, b8[4 + i]);
+      }
+      if (!lead) continue;
+      const int qy = y0 + j, oy = 2 * qy + ph.py;
+      const bool ok = qy < a.Hi && qx < a.Wi && oy < a.Ho && ox < a.Wo;
+      const int pout = (b * a.Ho + oy) * a.Wo + ox;
+      const int ppost = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
+      if (a.res_pre) Vox8<bf16_t>::add(rpre, ok ? (uint32_t)(pout * 8) * ES : kOOB, r);
+      if (a.relu) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = relu(r[i]);
+      }
+      if (a.res_post) Vox8<bf16_t>::add(rpost, ok ? (uint32_t)(ppost * 8) * ES : kOOB, r);
+      Vox8<bf16_t>::store(ro, ok ? (uint32_t)(pout * 8) * ES : kOOB, r);
+    }
+  }
+}
+
 // LDS-staged variant for the thin stride-2 5x5 convs (one tensor input of CIN 8 or 16 channels, padding 2, no plane):
 // FeatureNet's downsampling convs conv1.0 (8 -> 16 at 1184 x 1600) and conv2.0 (16 -> 32 at 592 x 800), which the
 // gather kernel runs at 0.3 of their HBM roofline (each input pixel fetched by ~6 output pixels' taps through L1;
@@ -1778,6 +1873,23 @@ hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
   return a.in_stride == 1 ? launch_wide_t<T, 1, 2>(s, a, dmin, span) : launch_wide_t<T, 2, 2>(s, a, dmin, span);
 }
 
+// conv2d_xpair_lds_kernel's layers: x-pair phases of a 16-channel single-input transposed stride-2 conv whose taps
+// all lie in -1 .. 1 (DAMVS_CONV2D_XPAIR_LDS=0, read per call: the XP gather kernel)
+bool xpair_lds_ok(const Conv2dArgs& a) {
+  const char* v = getenv("DAMVS_CONV2D_XPAIR_LDS");
+  if ((v && v[0] == '0') || a.c0 != 16 || a.c1 != 0 || a.in_stride != 1 || a.out_stride != 2 || a.Hq != a.Hi ||
+      a.Wq != a.Wi)
+    return false;
+  for (int p = 0; p < 2; ++p) {
+    if (a.ph[p].ntaps > 16 || a.ph[p].kchunks != (a.ph[p].ntaps * 16 + 31) / 32 || a.ph[p].gchunks != 0 ||
+        a.ph[p].py != p)
+      return false;
+    for (int t = 0; t < a.ph[p].ntaps; ++t)
+      if (a.ph[p].tap[t][0] < -1 || a.ph[p].tap[t][0] > 1 || a.ph[p].tap[t][1] < -1 || a.ph[p].tap[t][1] > 1) return false;
+  }
+  return true;
+}
+
 // True when the layer is a plain 3x3 stride-1 padding-1 conv with dense row-major taps.
 bool lds3_ok(const Conv2dArgs& a) {
   // at most one plane, next to at most 16 channels (the layers the gather kernel ran; 32+g goes to the halo kernel);
@@ -1922,8 +2034,16 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
     }
     return hipErrorInvalidValue;
   }
-  if (a.xpair) {  // x-pair phases (built at layer creation): only the XP gather kernel runs them
+  if (a.xpair) {  // x-pair phases (built at layer creation): the LDS x-pair kernel where it fits, else the XP gather kernel
     if (a.cout != 8 || a.MTtot != 1 || a.ngeo != 0 || a.nphase != 2) return hipErrorInvalidValue;
+    if constexpr (T_is_bf16<T>::value) {
+      if (xpair_lds_ok(a)) {
+        const int tx = (a.Wq + L2W - 1) / L2W, ty = (a.Hq + L2H - 1) / L2H;
+        const long long nt = (long long)tx * ty * a.B;
+        hipLaunchKernelGGL(conv2d_xpair_lds_kernel, dim3((unsigned)nt), dim3(256), 0, s, a, tx, ty, (int)nt);
+        return hipGetLastError();
+      }
+    }
     const long long Qtot = (long long)a.B * a.Hq * a.Wq;
     const int nq = (int)((Qtot + 4LL * kG2 * 16 - 1) / (4LL * kG2 * 16));
     const dim3 grid((unsigned)(nq * a.nphase), 1);

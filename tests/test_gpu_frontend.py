@@ -417,6 +417,42 @@ def test_lds_plane_bitwise_vs_gather(case, monkeypatch):
     assert torch.equal(outs[0], outs[1])
 
 
+# The LDS-staged x-pair transposed conv (conv2d_xpair_lds_kernel, bf16, round 6) against the x-pair gather kernel
+# (DAMVS_CONV2D_XPAIR_LDS=0): the same MFMA sequence per accumulator, so bitwise equal. k5 s2 (GeoFF's full-resolution
+# decoders) and k4 s2 (FPN top's transposed term), ragged tiles, residuals before / after ReLU.
+XPAIR_LDS_CASES = [
+    (5, 2, 1, True, True, 2, (37, 151)),
+    (5, 2, 1, False, False, 0, (20, 64)),
+    (4, 1, 0, False, True, 1, (9, 70)),
+]
+
+
+@pytest.mark.parametrize("case", XPAIR_LDS_CASES, ids=[str(i) for i in range(len(XPAIR_LDS_CASES))])
+def test_xpair_lds_bitwise_vs_gather(case, monkeypatch):
+    from damvsnet_amd.frontend_hip import HipConv2d
+    k, p, op, relu, pre, post_up, (H, W) = case
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(k * 31 + H + W)
+    B = 2
+    conv = nn.ConvTranspose2d(16, 8, k, stride=2, padding=p, output_padding=op)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.2)
+        conv.bias.copy_(torch.randn(conv.bias.shape, generator=g) * 0.1)
+    L = HipConv2d(conv, dt, relu, c0=16, c0_at=0)
+    Ho, Wo = (H - 1) * 2 - 2 * p + k + op, (W - 1) * 2 - 2 * p + k + op
+    x = nhwc(torch.randn(B, 16, H, W, generator=g)).to(DEV, dt)
+    res = torch.randn(B, Ho, Wo, L.cout_store, generator=g).to(DEV, dt) if pre else None
+    post = torch.randn(B, Ho // max(post_up, 1), Wo // max(post_up, 1), L.cout_store, generator=g).to(DEV, dt) \
+        if post_up else None
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DAMVS_CONV2D_XPAIR_LDS", flag)
+        outs.append(L(B, H, W, x, None, res_pre=res, res_post=post, post_up=max(post_up, 1)).clone())
+    torch.cuda.synchronize()
+    assert outs[0].shape == (B, Ho, Wo, L.cout_store)
+    assert torch.equal(outs[0], outs[1])
+
+
 # The plane-only layers on split-f16 MFMAs (conv2d_planes_mfma_kernel, the default for cout 4 / 8 at Wi % 4 == 0) against
 # float64 F.conv2d and against the VALU kernels (DAMVS_PLANES_MFMA=0): FeatureNet's RGB conv (3x3, 3 planes), GeoFF's
 # RGB+depth (5x5, 4) and depth+depth (5x5, 2) init convs, 1 plane, cout 4; ragged 16 x 64 tiles (H 37 / 21, W 200 / 36),
