@@ -20,6 +20,7 @@ sys.path.insert(0, REPO)
 CASES = {
     "A conv0.1 8->8 k3 full x5": (False, 3, 1, 1, 0, 8, 0, 0, 8, True, 5, 1184, 1600, False, 0),
     "B inner2 8->32 k1 +up2 x5": (False, 1, 1, 0, 0, 8, 0, 0, 32, False, 5, 1184, 1600, False, 2),
+    "B1 inner1 16->32 k1 +up2 x20": (False, 1, 1, 0, 0, 16, 0, 0, 32, False, 20, 592, 800, False, 2),
     "C out3 32->8 k3 full x5": (False, 3, 1, 1, 0, 32, 0, 0, 8, False, 5, 1184, 1600, False, 0),
     "D geo conv2 128+g->128 r4": (False, 3, 1, 1, 0, 128, 0, 1, 128, True, 1, 296, 400, True, 0),
     "E geo conv1 128+g->256 s2": (False, 3, 2, 1, 0, 128, 0, 1, 256, True, 1, 296, 400, False, 0),
