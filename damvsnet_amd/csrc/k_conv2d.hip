@@ -491,7 +491,7 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) != 2 ? 1 : CIN == 32 ? 
   }
 }
 
-// LDS-staged x-pair transposed conv (bf16, round 6): the 16 -> 8 channel stride-2 ConvTranspose layers whose two
+// LDS-staged x-pair transposed conv (round 6; bf16, and fp32 on the 16-K split form): the 16 -> 8 channel stride-2 ConvTranspose layers whose two
 // x-pair phases (build_phases_xpair: py = 0, 1; MFMA row r = (x parity r >> 3, channel r & 7)) read input offsets
 // -1 .. 1 -- GeoFeatureFusion's full-resolution k5 s2 decoders, which the x-pair gather kernel ran at ~0.2 of their
 // HBM roofline (each input pixel fetched through L1 by every tap of both phases). A block owns 8 x 64 input-grid
@@ -500,13 +500,14 @@ __global__ __launch_bounds__(256) DAMVS_WAVES((sizeof(T) != 2 ? 1 : CIN == 32 ? 
 // epilogue is the x-pair gather kernel's (lane group g + 1 hands its 4 channels to g; residuals, ReLU, 16-byte
 // records). Per phase and accumulator the same MFMA sequence as the gather kernel (chunks in packed order, padding taps
 // as zeros), so bitwise its results.
+template <typename T>
 __global__ __launch_bounds__(256) void conv2d_xpair_lds_kernel(const Conv2dArgs a, int tiles_x, int tiles_y, int ntiles) {
-  typedef BufIO<bf16_t> IO;
+  typedef BufIO<T> IO;
   typedef typename IO::raw raw;
-  constexpr int E = 8, KC = 32, CH = 2;  // 16 channels: two 16-byte chunks per pixel
+  constexpr int E = Stor<T>::E, KC = 4 * E, CH = 16 / E;  // 16 channels: CH 16-byte chunks per pixel
   constexpr int ROW = L2HW * CH;
   constexpr int TILE_CHUNKS = L2HH * ROW;
-  constexpr uint32_t ES = 2;
+  constexpr uint32_t ES = sizeof(T);
   __shared__ raw tile[TILE_CHUNKS];
   __shared__ int s_toff[2][16];  // per phase: tap t's halo offset in 16-byte chunks (-1: padding tap)
 
@@ -533,7 +534,7 @@ __global__ __launch_bounds__(256) void conv2d_xpair_lds_kernel(const Conv2dArgs 
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
-  const raw* tl = tile + (wave * 16 + n) * CH + (g & 1);  // the lane's column and channel half
+  const raw* tl = tile + (wave * 16 + n) * CH + (g * E) % 16 / E;  // the lane's column and channel chunk
   const long long nout = (long long)a.B * a.Ho * a.Wo * 8;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, nout * ES);
   const __amdgpu_buffer_rsrc_t rpre = make_rsrc(a.res_pre ? a.res_pre : a.out, a.res_pre ? nout * ES : 0);
@@ -552,36 +553,58 @@ __global__ __launch_bounds__(256) void conv2d_xpair_lds_kernel(const Conv2dArgs 
     for (int j = 0; j < L2H; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     for (int s = 0; s < ph.kchunks; ++s) {
       const raw w = wp[(size_t)s * 64];
-      const int off = s_toff[p][(s * KC + g * E) >> 4];  // 16 channels a tap: lane group g holds tap 2 s + (g >> 1)
+      const int off = s_toff[p][(s * KC + g * E) >> 4];  // 16 channels a tap (bf16: lane group g holds tap 2 s + (g >> 1))
       raw x[L2H];
 #pragma unroll
-      for (int j = 0; j < L2H; ++j) x[j] = off >= 0 ? tl[off + j * ROW] : make_uint4(0u, 0u, 0u, 0u);
+      for (int j = 0; j < L2H; ++j) x[j] = off >= 0 ? tl[off + j * ROW] : Frag2<T>::zero();
 #pragma unroll
-      for (int j = 0; j < L2H; ++j) Frag2<bf16_t>::mma(w, x[j], acc[j]);
+      for (int j = 0; j < L2H; ++j) Frag2<T>::mma(w, x[j], acc[j]);
     }
     // epilogue (the x-pair gather kernel's): output x = 2 qx + (g >> 1), y = 2 qy + py
-    const bool lead = (g & 1) == 0;
     const int ox = 2 * qx + (g >> 1);
+    if constexpr (sizeof(T) == 4) {  // fp32: every lane its 4 channels (16 bytes) of channel half g & 1
+      const int ch = (g & 1) * 4;
 #pragma unroll
-    for (int j = 0; j < L2H; ++j) {
-      float r[8];
+      for (int j = 0; j < L2H; ++j) {
+        float r[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        r[i] = fmaf(acc[j][i], a.wscale, b8[i]);
-        r[4 + i] = fmaf(__shfl_down(acc[j][i], 16), a.wscale, b8[4 + i]);
+        for (int i = 0; i < 4; ++i) r[i] = fmaf(acc[j][i], a.wscale, b8[ch + i]);
+        const int qy = y0 + j, oy = 2 * qy + ph.py;
+        const bool ok = qy < a.Hi && qx < a.Wi && oy < a.Ho && ox < a.Wo;
+        const int pout = (b * a.Ho + oy) * a.Wo + ox;
+        const int ppost = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
+        const uint32_t o = ok ? (uint32_t)(pout * 8 + ch) * ES : kOOB;
+        if (a.res_pre) IO::addq(IO::ldq(rpre, o), r);
+        if (a.relu) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) r[i] = relu(r[i]);
+        }
+        if (a.res_post) IO::addq(IO::ldq(rpost, ok ? (uint32_t)(ppost * 8 + ch) * ES : kOOB), r);
+        IO::stq(ro, o, r);
       }
-      if (!lead) continue;
-      const int qy = y0 + j, oy = 2 * qy + ph.py;
-      const bool ok = qy < a.Hi && qx < a.Wi && oy < a.Ho && ox < a.Wo;
-      const int pout = (b * a.Ho + oy) * a.Wo + ox;
-      const int ppost = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
-      if (a.res_pre) Vox8<bf16_t>::add(rpre, ok ? (uint32_t)(pout * 8) * ES : kOOB, r);
-      if (a.relu) {
+    } else {
+      const bool lead = (g & 1) == 0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) r[i] = relu(r[i]);
+      for (int j = 0; j < L2H; ++j) {
+        float r[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          r[i] = fmaf(acc[j][i], a.wscale, b8[i]);
+          r[4 + i] = fmaf(__shfl_down(acc[j][i], 16), a.wscale, b8[4 + i]);
+        }
+        if (!lead) continue;
+        const int qy = y0 + j, oy = 2 * qy + ph.py;
+        const bool ok = qy < a.Hi && qx < a.Wi && oy < a.Ho && ox < a.Wo;
+        const int pout = (b * a.Ho + oy) * a.Wo + ox;
+        const int ppost = (b * (a.Ho >> us) + (oy >> us)) * (a.Wo >> us) + (ox >> us);
+        if (a.res_pre) Vox8<T>::add(rpre, ok ? (uint32_t)(pout * 8) * ES : kOOB, r);
+        if (a.relu) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) r[i] = relu(r[i]);
+        }
+        if (a.res_post) Vox8<T>::add(rpost, ok ? (uint32_t)(ppost * 8) * ES : kOOB, r);
+        Vox8<T>::store(ro, ok ? (uint32_t)(pout * 8) * ES : kOOB, r);
       }
-      if (a.res_post) Vox8<bf16_t>::add(rpost, ok ? (uint32_t)(ppost * 8) * ES : kOOB, r);
-      Vox8<bf16_t>::store(ro, ok ? (uint32_t)(pout * 8) * ES : kOOB, r);
     }
   }
 }
@@ -1875,13 +1898,13 @@ hipError_t launch_wide(hipStream_t s, const Conv2dArgs& a) {
 
 // conv2d_xpair_lds_kernel's layers: x-pair phases of a 16-channel single-input transposed stride-2 conv whose taps
 // all lie in -1 .. 1 (DAMVS_CONV2D_XPAIR_LDS=0, read per call: the XP gather kernel)
-bool xpair_lds_ok(const Conv2dArgs& a) {
+bool xpair_lds_ok(const Conv2dArgs& a, int KC) {
   const char* v = getenv("DAMVS_CONV2D_XPAIR_LDS");
   if ((v && v[0] == '0') || a.c0 != 16 || a.c1 != 0 || a.in_stride != 1 || a.out_stride != 2 || a.Hq != a.Hi ||
       a.Wq != a.Wi)
     return false;
   for (int p = 0; p < 2; ++p) {
-    if (a.ph[p].ntaps > 16 || a.ph[p].kchunks != (a.ph[p].ntaps * 16 + 31) / 32 || a.ph[p].gchunks != 0 ||
+    if (a.ph[p].ntaps > 16 || a.ph[p].kchunks != (a.ph[p].ntaps * 16 + KC - 1) / KC || a.ph[p].gchunks != 0 ||
         a.ph[p].py != p)
       return false;
     for (int t = 0; t < a.ph[p].ntaps; ++t)
@@ -2036,13 +2059,11 @@ hipError_t launch_t(hipStream_t s, const Conv2dArgs& a) {
   }
   if (a.xpair) {  // x-pair phases (built at layer creation): the LDS x-pair kernel where it fits, else the XP gather kernel
     if (a.cout != 8 || a.MTtot != 1 || a.ngeo != 0 || a.nphase != 2) return hipErrorInvalidValue;
-    if constexpr (T_is_bf16<T>::value) {
-      if (xpair_lds_ok(a)) {
-        const int tx = (a.Wq + L2W - 1) / L2W, ty = (a.Hq + L2H - 1) / L2H;
-        const long long nt = (long long)tx * ty * a.B;
-        hipLaunchKernelGGL(conv2d_xpair_lds_kernel, dim3((unsigned)nt), dim3(256), 0, s, a, tx, ty, (int)nt);
-        return hipGetLastError();
-      }
+    if (xpair_lds_ok(a, 4 * Stor<T>::E)) {
+      const int tx = (a.Wq + L2W - 1) / L2W, ty = (a.Hq + L2H - 1) / L2H;
+      const long long nt = (long long)tx * ty * a.B;
+      hipLaunchKernelGGL(conv2d_xpair_lds_kernel<T>, dim3((unsigned)nt), dim3(256), 0, s, a, tx, ty, (int)nt);
+      return hipGetLastError();
     }
     const long long Qtot = (long long)a.B * a.Hq * a.Wq;
     const int nq = (int)((Qtot + 4LL * kG2 * 16 - 1) / (4LL * kG2 * 16));

@@ -417,7 +417,7 @@ def test_lds_plane_bitwise_vs_gather(case, monkeypatch):
     assert torch.equal(outs[0], outs[1])
 
 
-# The LDS-staged x-pair transposed conv (conv2d_xpair_lds_kernel, bf16, round 6) against the x-pair gather kernel
+# The LDS-staged x-pair transposed conv (conv2d_xpair_lds_kernel, bf16 and fp32, round 6) against the x-pair gather kernel
 # (DAMVS_CONV2D_XPAIR_LDS=0): the same MFMA sequence per accumulator, so bitwise equal. k5 s2 (GeoFF's full-resolution
 # decoders) and k4 s2 (FPN top's transposed term), ragged tiles, residuals before / after ReLU.
 XPAIR_LDS_CASES = [
@@ -428,10 +428,10 @@ XPAIR_LDS_CASES = [
 
 
 @pytest.mark.parametrize("case", XPAIR_LDS_CASES, ids=[str(i) for i in range(len(XPAIR_LDS_CASES))])
-def test_xpair_lds_bitwise_vs_gather(case, monkeypatch):
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32], ids=["bf16", "f32"])
+def test_xpair_lds_bitwise_vs_gather(case, dt, monkeypatch):
     from damvsnet_amd.frontend_hip import HipConv2d
     k, p, op, relu, pre, post_up, (H, W) = case
-    dt = torch.bfloat16
     g = torch.Generator().manual_seed(k * 31 + H + W)
     B = 2
     conv = nn.ConvTranspose2d(16, 8, k, stride=2, padding=p, output_padding=op)
